@@ -1,0 +1,725 @@
+"""CPU restatement of the reference ray-march render path (TEST INFRASTRUCTURE ONLY).
+
+This module is the parity oracle for the HIP path in ``neural_raytracing_amd``.  It is
+eager PyTorch on the CPU, written from a text reading of
+``prashantraina/neural_raytracing`` (``pytorch3d/pathtracer``); the reference itself is never
+imported or executed (SURVEY.md §8c records that running it is denied).  Every function names
+the reference file:line it restates.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this package, and only as the checker.
+
+Parity pin: ``tests/test_oracle.py::test_reference_checksum`` rebuilds the single reference
+run recorded in BASELINE.md §2 (same seeds, same construction order, same render call) and
+checks ``out.abs().sum() == 4511.5146484375``.  That is the only output of the reference that
+exists; everything else is pinned by known-answer tests derived from the code.
+
+Conventions: the reference computes on tensors shaped ``[N, W, H, B, C]`` (cameras, tile
+rows, tile cols, bundle, channels).  The restatement keeps those shapes where they change
+arithmetic (batched BLAS calls, squeeze quirks) so results match op for op.
+"""
+import math
+import random
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+# ---------------------------------------------------------------------------------------------
+# Fourier-feature skip MLP  (neural_blocks.py:12-86, utils.py:33-40)
+# ---------------------------------------------------------------------------------------------
+
+def fourier_encode(x, basis):
+    """``[x, sin(xB), cos(xB)]`` -- utils.py:37-40 (fourier2)."""
+    proj = x @ basis
+    return torch.cat([x, proj.sin(), proj.cos()], dim=-1)
+
+
+def leaky_relu(x):
+    # neural_blocks.py:26 default activation (negative_slope 0.01)
+    return F.leaky_relu(x)
+
+
+def softplus(x):
+    # sdfs.py:29 (F.softplus) and nn.Softplus() -- beta 1, threshold 20
+    return F.softplus(x)
+
+
+ACTIVATIONS = {"leaky_relu": leaky_relu, "softplus": softplus}
+
+
+class SkipMLP(nn.Module):
+    """Restatement of ``SkipConnMLP`` (neural_blocks.py:12-86).
+
+    The RNG consumption order of the constructor is the reference's: the Fourier basis
+    (``sigma * randn(freqs, in).T``, utils.py:33-36), then the hidden ``nn.Linear`` list in
+    index order (:46-51), then ``init`` (:53), then ``out`` (:55), then the optional zero / xavier
+    re-initialisation over ``[init, out, *layers]`` (:56-71).
+    """
+
+    def __init__(self, num_layers=8, hidden_size=64, in_size=3, out=3, skip=3, freqs=16,
+                 sigma=32, activation="leaky_relu", latent_size=0, zero_init=False,
+                 xavier_init=False):
+        super().__init__()
+        self.in_size = in_size
+        self.basis_p = sigma * torch.randn(freqs, in_size).T
+        self.dim_p = 2 * freqs + in_size + latent_size
+        self.skip = skip
+        self.latent_size = latent_size
+        self.layers = nn.ModuleList([
+            nn.Linear(hidden_size + self.dim_p if self.is_skip(i, num_layers) else hidden_size,
+                      hidden_size)
+            for i in range(num_layers)
+        ])
+        self.init = nn.Linear(self.dim_p, hidden_size)
+        self.out = nn.Linear(hidden_size, out)
+        self.act_name = activation
+        ordered = [self.init, self.out, *self.layers]
+        if zero_init:
+            for lin in ordered:
+                nn.init.zeros_(lin.weight)
+            for lin in ordered:
+                nn.init.zeros_(lin.bias)
+        if xavier_init:
+            for lin in ordered:
+                nn.init.xavier_uniform_(lin.weight)
+            for lin in ordered:
+                nn.init.zeros_(lin.bias)
+
+    def is_skip(self, i, n=None):
+        n = len(self.layers) if n is None else n
+        return i != n - 1 and i % self.skip == 0
+
+    def forward(self, p, latent=None):
+        act = ACTIVATIONS[self.act_name]
+        lead = p.shape[:-1]
+        enc = fourier_encode(p.reshape(-1, self.in_size), self.basis_p)
+        if latent is not None:
+            enc = torch.cat([enc, latent.reshape(-1, self.latent_size)], dim=-1)
+        h = self.init(enc)
+        for i, lin in enumerate(self.layers):
+            if self.is_skip(i):
+                h = torch.cat([h, enc], dim=-1)
+            h = lin(act(h))
+        y = self.out(act(h))
+        return y.reshape(lead + (y.shape[-1],))
+
+
+# ---------------------------------------------------------------------------------------------
+# Shapes  (shapes/sdfs.py, utils.py:386-387)
+# ---------------------------------------------------------------------------------------------
+
+def smooth_min(v, k: float = 32.0, dim: int = 0):
+    """utils.py:385-387: ``-log(clamp(sum(exp(-k v)), 1e-4)) / k``."""
+    return -torch.exp(-k * v).sum(dim).clamp(min=1e-4).log() / k
+
+
+def unit_sphere_sdf(p):
+    """SPHERE_SDF, sdfs.py:13."""
+    return torch.norm(p, dim=-1) - 1
+
+
+class SphereBlobSDF(nn.Module):
+    """Restatement of ``SphereSDF`` (sdfs.py:16-44).
+
+    ``shift`` is normally ``SkipMLP(8, 128, F=32, softplus, zero_init)``; the ``shift_*``
+    arguments let a test or bench substitute a different residual MLP (e.g. 8x256).
+    """
+
+    def __init__(self, n=128, shift_layers=8, shift_hidden=128, shift_freqs=32,
+                 shift_zero_init=True):
+        super().__init__()
+        self.centers = nn.Parameter(0.3 * torch.rand(n, 3) - 0.15)
+        self.radii = nn.Parameter(0.2 * torch.rand(n) - 0.1)
+        self.tfs = nn.Parameter(torch.zeros(n, 3, 3))
+        self.shift = SkipMLP(num_layers=shift_layers, hidden_size=shift_hidden, in_size=3, out=1,
+                             freqs=shift_freqs, activation="softplus",
+                             zero_init=shift_zero_init)
+
+    def spheres(self, p):
+        # sdfs.py:37-43
+        tfs = self.tfs + torch.eye(3).unsqueeze(0)
+        flat = p.reshape(-1, 3).unsqueeze(0)
+        q = torch.einsum("ijk,ibk->ibj", tfs, flat.expand(tfs.shape[0], -1, -1))
+        q = q - self.centers.unsqueeze(1)
+        sd = q.norm(p=2, dim=-1) - self.radii.unsqueeze(-1)
+        return smooth_min(sd, k=32.0).reshape(p.shape[:-1])
+
+    def forward(self, p):
+        out = self.spheres(p)
+        return out + self.shift(p).reshape_as(out)
+
+
+class MarchedSDF:
+    """Restatement of ``SDF`` (sdfs.py:89-277): sphere tracing, coarse scan, normals."""
+
+    def __init__(self, sdf=unit_sphere_sdf, epsilon=1e-3, max_steps=32, dist=2.2):
+        self.sdf = sdf
+        self.epsilon = epsilon
+        self.max_steps = max_steps
+        self.dist = dist
+
+    def __len__(self):
+        return 1
+
+    def coarse_scan(self, origin, direction, jitter=None):
+        """sdfs.py:232-249.  ``jitter`` replaces the reference's ``random.random()``."""
+        n = 128
+        if jitter is None:
+            jitter = random.random()
+        max_t = self.dist + jitter * (2 / n)
+        step = max_t / n
+        with torch.no_grad():
+            best = self.sdf(origin).squeeze(-1)
+            idx = torch.zeros_like(best, dtype=torch.long)
+            for i in range(n):
+                s = self.sdf(origin + step * (i + 1) * direction).squeeze(-1)
+                idx = torch.where(s < best, i + 1, idx)
+                best = torch.minimum(best, s)
+        best_pos = origin + idx.unsqueeze(-1).unsqueeze(-1) * step * direction
+        return self.sdf(best_pos), best_pos
+
+    def march(self, origin, direction, max_t=10):
+        """Fixed-step sphere tracing, sdfs.py:114-131 (every ray, every step)."""
+        t = torch.zeros(origin.shape[:-1] + (1,))
+        live = torch.ones(t.shape[:-1], dtype=torch.bool)
+        hit = torch.zeros_like(live)
+        with torch.no_grad():
+            for _ in range(self.max_steps):
+                live = live & (t < max_t).squeeze(-1)
+                d = self.sdf(origin + direction * t)
+                now = live & (d <= self.epsilon)
+                hit = hit | now
+                live = live & ~now
+                t = torch.where(live.unsqueeze(-1), t + d.unsqueeze(-1), t)
+        return t, hit
+
+    def gradient(self, p):
+        """sdfs.py:184-197 (autograd normal, un-normalised)."""
+        with torch.enable_grad():
+            p = p.detach().requires_grad_()
+            out = self.sdf(p)
+            (g,) = torch.autograd.grad(out, p, torch.ones_like(out), create_graph=False)
+        return g
+
+    def intersect(self, rays, max_t=10, active=True, primary=True, jitter=None):
+        """sdfs.py:111-160.  Returns (interaction dict, hit mask)."""
+        origin, direction = rays.split(3, dim=-1)
+        t, hit = self.march(origin, direction, max_t)
+        p = origin + t * direction
+        throughput = 0
+        if primary:
+            thr, _ = self.coarse_scan(origin, direction, jitter)
+            throughput = -1000 * thr
+        it = Interaction(p=p, t=t.squeeze(), throughput=throughput)
+        n = torch.zeros_like(p)
+        if hit.any():
+            raw = self.gradient(p[hit])
+            it.raw_normals = raw
+            n[hit] = F.normalize(raw, eps=1e-6, dim=-1)
+            p[hit] = p[hit] + n[hit] * self.epsilon * 5
+        it.set_normals(n)
+        it.wi = it.to_local(-direction)
+        return it, hit
+
+    def intersect_test(self, rays, max_t=10, active=True):
+        """Shadow-ray march from t0 = 100*eps, sdfs.py:162-181."""
+        origin, direction = rays.split(3, dim=-1)
+        t = torch.zeros(origin.shape[:-1] + (1,)) + 1e2 * self.epsilon
+        live = torch.ones(t.shape[:-1], dtype=torch.bool)
+        with torch.no_grad():
+            for _ in range(self.max_steps):
+                d = self.sdf(origin + direction * t)
+                now = live & (d < self.epsilon)
+                t = torch.where(live.unsqueeze(-1), t + d.unsqueeze(-1), t)
+                live = live & ~now
+        return (t >= max_t).squeeze(-1) | live
+
+
+# ---------------------------------------------------------------------------------------------
+# Interaction frames  (interaction.py:9-119)
+# ---------------------------------------------------------------------------------------------
+
+def shading_frame(n):
+    """coordinate_system, interaction.py:9-27: columns [s, t, n]."""
+    n = F.normalize(n, eps=1e-7, dim=-1)
+    x, y, z = n.split(1, dim=-1)
+    sign = torch.where(z >= 0, 1.0, -1.0)
+    sz = sign + z
+    a = -torch.where(sz.abs() < 1e-6, torch.tensor(1e-6), sz).reciprocal()
+    b = x * y * a
+    s = torch.cat([(x * x * a * sign) + 1, b * sign, x * -sign], dim=-1)
+    s = F.normalize(s, eps=1e-7, dim=-1)
+    t = F.normalize(s.cross(n, dim=-1), eps=1e-7, dim=-1)
+    s = F.normalize(n.cross(t, dim=-1), eps=1e-7, dim=-1)
+    return torch.stack([s, t, n], dim=-1)
+
+
+def frame_to_local(frame, w):
+    """interaction.py:37-41 (the /3 of the mean cancels in the normalize, but is kept)."""
+    w = w.unsqueeze(-1).expand_as(frame)
+    return F.normalize((frame * w).mean(dim=-2), eps=1e-7, dim=-1)
+
+
+def frame_from_local(frame, v):
+    """interaction.py:44-51."""
+    s, t, n = frame.split(1, dim=-1)
+    x, y, z = v.split(1, dim=-1)
+    w = s.squeeze(-1) * x + t.squeeze(-1) * y + n.squeeze(-1) * z
+    return F.normalize(w, eps=1e-7, dim=-1)
+
+
+class Interaction:
+    """MixedInteraction (interaction.py:61-106) as a plain attribute bag."""
+
+    def __init__(self, p, t=None, throughput=None, with_logits=True):
+        self.p = p
+        self.t = t
+        self.throughput = throughput
+        self.with_logits = with_logits
+        self.n = None
+        self.frame = None
+        self.wi = None
+
+    def set_normals(self, n):
+        self.n = n
+        self.frame = shading_frame(n)
+
+    def to_local(self, w):
+        return frame_to_local(self.frame, w)
+
+    def from_local(self, v):
+        return frame_from_local(self.frame, v)
+
+
+# ---------------------------------------------------------------------------------------------
+# BSDF helpers  (utils.py:43-51, 152-155, 234-258; bsdf/bsdfs.py)
+# ---------------------------------------------------------------------------------------------
+
+def nonzero_eps(v, eps: float = 1e-7):
+    """utils.py:43-51: values with |v| < eps become +eps."""
+    return torch.where(v.abs() < eps, torch.tensor(eps), v)
+
+
+def rodrigues(v, axis, c, s):
+    """rotate_vector, utils.py:152-155."""
+    return v * c + axis * (v * axis).sum(dim=-1, keepdim=True) * (1 - c) \
+        + torch.cross(axis, v, dim=-1) * s
+
+
+def rusinkiewicz(wo, wi):
+    """param_rusin2, utils.py:233-258 -> [cos(phi_d), cos(theta_h), cos(theta_d)].
+
+    Keeps the reference's ``sqrt(clamp(1 - cos_theta_h, 1e-6))`` (1-cos, not 1-cos^2).
+    """
+    wo = F.normalize(wo, dim=-1)
+    wi = F.normalize(wi, dim=-1)
+    ey = torch.tensor([0, 1, 0], dtype=torch.float).expand_as(wo)
+    ez = torch.tensor([0, 0, 1], dtype=torch.float).expand_as(wo)
+    h = F.normalize(wo + wi, dim=-1)
+    cos_th = h[..., 2]
+    r = nonzero_eps(h[..., 1]).hypot(nonzero_eps(h[..., 0])).clamp(min=1e-6)
+    c = (h[..., 0] / r).unsqueeze(-1)
+    s = -(h[..., 1] / r).unsqueeze(-1)
+    tmp = F.normalize(rodrigues(wi, ez, c, s), dim=-1)
+    c = h[..., 2].unsqueeze(-1)
+    s = -(1 - h[..., 2]).clamp(min=1e-6).sqrt().unsqueeze(-1)
+    diff = F.normalize(rodrigues(tmp, ey, c, s), dim=-1)
+    cos_td = diff[..., 2]
+    cos_pd = torch.atan2(nonzero_eps(diff[..., 1]), nonzero_eps(diff[..., 0])).cos()
+    return torch.stack([cos_pd, cos_th, cos_td], dim=-1)
+
+
+class NeuralBSDFRef(nn.Module):
+    """NeuralBSDF, bsdfs.py:613-637: ``act(MLP_6x96,F=64(param_rusin2(it.wi, wo)))``, pdf 1."""
+
+    def __init__(self, activation="sigmoid"):
+        super().__init__()
+        self.mlp = SkipMLP(in_size=3, out=3, num_layers=6, hidden_size=96, freqs=64)
+        self.act_name = activation
+
+    def act(self, x):
+        return {"sigmoid": torch.sigmoid, "softplus": F.softplus}[self.act_name](x)
+
+    def eval_and_pdf(self, it, wo, active=True):
+        f = self.act(self.mlp(rusinkiewicz(it.wi, wo)))
+        return f, torch.ones(f.shape[:-1])
+
+    def joint_eval_pdf(self, it, wo, active=True):
+        f, pdf = self.eval_and_pdf(it, wo, active)
+        return torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1)
+
+
+class DiffuseRef(nn.Module):
+    """Diffuse, bsdfs.py:78-118 (preprocess default x/pi)."""
+
+    def __init__(self, reflectance=(0.25, 0.2, 0.7), preprocess="div_pi"):
+        super().__init__()
+        self.reflectance = torch.tensor(list(reflectance))
+        self.preproc_name = preprocess
+
+    def preproc(self, x):
+        return {"div_pi": lambda v: v / math.pi, "sigmoid": torch.sigmoid,
+                "softplus": F.softplus, "identity": lambda v: v}[self.preproc_name](x)
+
+    def eval_and_pdf(self, it, wo, active=True):
+        spectrum = self.preproc(wo[..., 2].unsqueeze(-1) * self.reflectance)
+        return spectrum, wo[..., 2] / math.pi
+
+    def joint_eval_pdf(self, it, wo, active=True):
+        f, pdf = self.eval_and_pdf(it, wo, active)
+        return torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1)
+
+
+def fresnel_conductor(cos_t, eta_r: float, eta_i: float):
+    """bsdfs.py:327-341."""
+    ct2 = cos_t * cos_t
+    st2 = (1 - ct2).clamp(min=1e-10)
+    st4 = st2 * st2
+    tmp = eta_r * eta_r - eta_i * eta_i - st2
+    a2pb2 = (tmp * tmp + 4 * eta_i * eta_i * eta_r * eta_r).clamp(min=1e-10).sqrt()
+    a = (0.5 * (a2pb2 + tmp)).clamp(min=1e-10).sqrt()
+    t1 = a2pb2 + ct2
+    t2 = 2 * cos_t * a
+    rs = (t1 - t2) / (t1 + t2)
+    t3 = a2pb2 * ct2 + st4
+    t4 = t2 * st2
+    rp = rs * (t3 - t4) / (t3 + t4)
+    return 0.5 * (rs + rp)
+
+
+class ConductorRef(nn.Module):
+    """Conductor, bsdfs.py:345-388."""
+
+    def __init__(self, specular=(1.0, 1.0, 1.0), eta=1.3, k=1.0, activation="sigmoid"):
+        super().__init__()
+        self.eta = torch.tensor(eta)
+        self.k = torch.tensor(k)
+        self.specular = torch.tensor(list(specular))
+        self.act_name = activation
+
+    def act(self, x):
+        return {"sigmoid": torch.sigmoid, "softplus": F.softplus}[self.act_name](x)
+
+    def eval_and_pdf(self, it, wi_unused, active=True):
+        wo = wi_unused
+        refl = torch.cat([-it.wi[..., :1], -it.wi[..., 1:2], it.wi[..., 2:]], dim=-1)
+        thresh = (refl * wo).sum(dim=-1, keepdim=True) > 0.94
+        eta = F.softplus(self.eta).item()
+        fres = fresnel_conductor(it.wi[..., 2], eta, 0.0).reshape_as(thresh)
+        spectrum = torch.where(thresh, fres * self.act(self.specular),
+                               torch.zeros(it.p.shape))
+        pdf = torch.where(thresh.reshape(it.p.shape[:-1]), 1.0, 0.0)
+        if not isinstance(active, bool):
+            spectrum = torch.where(active.unsqueeze(-1), spectrum, torch.zeros_like(spectrum))
+        return spectrum, pdf
+
+    def joint_eval_pdf(self, it, wo, active=True):
+        f, pdf = self.eval_and_pdf(it, wo, active)
+        return torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1)
+
+
+class SpatialMixBSDF(nn.Module):
+    """ComposeSpatialVarying, bsdfs.py:482-536.
+
+    ``sp_var_fn = SkipMLP(16, 256, F=128, sigma=128, out=len(bsdfs), xavier)`` is built AFTER
+    the component BSDFs (they are constructed in the caller's argument list).
+    """
+
+    def __init__(self, bsdfs):
+        super().__init__()
+        self.bsdfs = nn.ModuleList(bsdfs)
+        self.sp_var_fn = SkipMLP(num_layers=16, hidden_size=256, freqs=128, sigma=2 << 6,
+                                 in_size=3, out=len(bsdfs), xavier_init=True)
+
+    def weights(self, p):
+        w = self.sp_var_fn(p).reshape(p.shape[:-1] + (len(self.bsdfs),))
+        return w.sigmoid()
+
+    def eval_and_pdf(self, it, wo, active=True):
+        k = self.weights(it.p)
+        parts = torch.stack([b.joint_eval_pdf(it, wo, active) for b in self.bsdfs], dim=-1)
+        it.normalized_weights = k
+        parts = torch.where(active[..., None, None], parts * k.unsqueeze(-2),
+                            torch.zeros_like(parts))
+        spectrum, pdf = parts.sum(dim=-1).split([3, 1], dim=-1)
+        return spectrum, pdf.squeeze(-1)
+
+
+# ---------------------------------------------------------------------------------------------
+# Lights  (lights/lights.py, scene.py:290-324)
+# ---------------------------------------------------------------------------------------------
+
+class LightSample:
+    def __init__(self, d, pdf, dist=None):
+        self.d = d
+        self.pdf = pdf
+        self.dist = dist
+
+
+class LightFieldRef(nn.Module):
+    """LightField, lights.py:155-195: direction/magnitude from a 10x256 MLP, colour sigmoid."""
+
+    def __init__(self):
+        super().__init__()
+        self.light_field_approx = SkipMLP(in_size=3, out=3, num_layers=10, hidden_size=256)
+        self.color = nn.Parameter(torch.zeros(3))
+
+    def sample_direction(self, it, active):
+        v = self.light_field_approx(it.p[active])
+        d = torch.zeros_like(it.p)
+        d[active] = F.normalize(v, eps=1e-6, dim=-1).clamp(min=1e-6, max=1)
+        le = torch.zeros_like(it.p)
+        le[active] = torch.linalg.norm(v, ord=2, dim=-1, keepdim=True) * self.color.sigmoid()
+        return LightSample(d, torch.ones(it.p.shape[:-1])), le
+
+
+class PointLightRef(nn.Module):
+    """PointLights, lights.py:40-110 (one light)."""
+
+    def __init__(self, intensity=(1.0, 1.0, 1.0), location=(0.0, 1.0, 0.0), const=1e-8,
+                 linear=1e-8, square=1.0, scale=1e2):
+        super().__init__()
+        self.scale = torch.tensor(float(scale))
+        self.intensity = torch.tensor([list(intensity)], dtype=torch.float)
+        self.location = torch.tensor(list(location), dtype=torch.float).reshape(-1, 3)
+        self.const = torch.tensor(float(const))
+        self.linear = torch.tensor(float(linear))
+        self.square = torch.tensor(float(square))
+
+    def sample_direction(self, it, active):
+        # the reference broadcasts location as [L,1,1,1,3] against p [N,W,H,B,3]
+        shape = (-1,) + (1,) * (it.p.dim() - 2) + (3,)
+        d = self.location.reshape(shape) - it.p
+        dist = torch.linalg.norm(d, dim=-1, keepdim=True)
+        d = F.normalize(d, eps=1e-6, dim=-1)
+        fall = self.const.clamp(min=1e-6) + self.linear.clamp(min=1e-6) * dist \
+            + self.square.clamp(min=1e-6) * dist.square()
+        color = self.intensity.reshape(shape)
+        le = self.scale * F.normalize(color, dim=-1) / fall.clamp(min=1e-6)
+        le = le.expand_as(it.p).clone() if le.shape != it.p.shape else le
+        le[~active] = 0
+        return LightSample(d, 1, dist), le
+
+
+def emitter_no_shadow(it, lights, active):
+    """sample_emitter_dir_wo_isect, scene.py:321-324."""
+    ds, le = lights.sample_direction(it, active)
+    le[~active] = 0
+    return ds, le
+
+
+def emitter_shadow_ray(it, shape, lights, active):
+    """sample_emitter_dir_w_isect, scene.py:290-298."""
+    ds, le = lights.sample_direction(it, active)
+    rays = torch.cat([it.p, ds.d], dim=-1)
+    visible = shape.intersect_test(rays, max_t=ds.dist.reshape_as(active)[..., None],
+                                   active=active)
+    le[~visible | ~active] = 0
+    return ds, le
+
+
+# ---------------------------------------------------------------------------------------------
+# Integrators  (integrators/integrators.py)
+# ---------------------------------------------------------------------------------------------
+
+class DirectRef:
+    """Direct, integrators.py:139-206 with emitter_samples=1, bsdf_samples=0.
+
+    ``primary`` is always True: ``Direct.__init__`` assigns ``training`` before
+    ``nn.Module.__init__`` resets it (:153-154), so the coarse scan always runs.
+    """
+
+    def dims(self):
+        return 3
+
+    def sample(self, shape, rays, bsdf, lights, w_isect=False, jitter=None):
+        result = torch.zeros(*rays.shape[:-1], 3)
+        it, active = shape.intersect(rays, primary=True, jitter=jitter)
+        if not active.any():
+            return result, active, it
+        if w_isect is True:
+            ds, le = emitter_shadow_ray(it, shape, lights, active)
+        else:
+            ds, le = emitter_no_shadow(it, lights, active)
+        ae = active & (torch.as_tensor(ds.pdf) > 0)
+        wo = it.to_local(ds.d)
+        f, pdf = bsdf.eval_and_pdf(it, wo, active=ae)
+        mis = torch.ones_like(pdf.reshape_as(ae))
+        val = mis[ae].unsqueeze(-1) * f[ae] * le[ae]
+        val = val / 1
+        result[ae] = result[ae] + val
+        return result, active, it
+
+
+class NeRFIntegratorRef:
+    """NeRFIntegrator, integrators.py:243-257: append sigmoid(throughput) as alpha."""
+
+    def __init__(self, sub):
+        self.sub = sub
+
+    def dims(self):
+        return self.sub.dims() + 1
+
+    def sample(self, shape, rays, bsdf, lights, w_isect=False, jitter=None):
+        rgb, _, it = self.sub.sample(shape, rays, bsdf, lights, w_isect=w_isect, jitter=jitter)
+        alpha = it.throughput.unsqueeze(-1)
+        if it.with_logits:
+            alpha = alpha.sigmoid()
+        return torch.cat([rgb, alpha], dim=-1), torch.tensor(True), it
+
+
+# ---------------------------------------------------------------------------------------------
+# Cameras  (cameras/cameras.py)
+# ---------------------------------------------------------------------------------------------
+
+class NeRFCameraRef:
+    """NeRFCamera.sample_positions, cameras.py:23-54."""
+
+    def __init__(self, cam_to_world, focal):
+        self.cam_to_world = cam_to_world
+        self.focal = focal
+
+    def __len__(self):
+        return self.cam_to_world.shape[0]
+
+    def sample_positions(self, pos, size, with_noise=0.0, noise=None):
+        u, v = pos.split(1, dim=-1)
+        if with_noise:
+            if noise is None:
+                nu, nv = torch.rand_like(u), torch.rand_like(v)
+            else:
+                nu, nv = noise
+            u = u + (nu - 0.5) * with_noise
+            v = v + (nv - 0.5) * with_noise
+        d = torch.stack([(u - size * 0.5) / self.focal, -(v - size * 0.5) / self.focal,
+                         -torch.ones_like(u)], dim=-1)
+        r_d = torch.sum(d[..., None, :] * self.cam_to_world[..., :3, :3], dim=-1)
+        r_d = F.normalize(r_d, dim=-1).permute(2, 0, 1, 3).unsqueeze(-2)
+        r_o = self.cam_to_world[..., :3, -1][:, None, None, None, :].expand_as(r_d)
+        return torch.cat([r_o, r_d], dim=-1)
+
+
+class DTUCameraRef:
+    """DTUCamera.sample_positions + lift, cameras.py:132-192 (with_noise ignored)."""
+
+    def __init__(self, pose, intrinsic):
+        self.pose = pose
+        self.intrinsic = intrinsic
+
+    def __len__(self):
+        return self.pose.shape[0]
+
+    def sample_positions(self, pos, size, bundle_size=1):
+        r_o = self.pose[:, :3, 3]
+        W, H, _ = pos.shape
+        N = len(self)
+        scale = torch.tensor([1600, 1200], dtype=torch.float) / size
+        u, v = (pos * scale).reshape(-1, 2).split(1, dim=-1)
+        u = u.reshape(1, -1).expand(N, -1)
+        v = v.reshape(1, -1).expand(N, -1)
+        K = self.intrinsic
+        shape = u.shape
+        fx = K[..., 0, 0, None].expand(shape)
+        fy = K[..., 1, 1, None].expand(shape)
+        cx = K[..., 0, 2, None].expand(shape)
+        cy = K[..., 1, 2, None].expand(shape)
+        sk = K[..., 0, 1, None].expand(shape)
+        z = torch.ones_like(u)
+        xl = (u - cx + cy * sk / fy - sk * v / fy) / fx * z
+        yl = (v - cy) / fy * z
+        pts = torch.stack([xl, yl, z, torch.ones_like(z)], dim=-1)
+        world = torch.bmm(self.pose, pts.permute(0, 2, 1)).permute(0, 2, 1)[..., :3]
+        r_o = r_o[:, None, :].expand_as(world)
+        r_d = F.normalize(world - r_o, dim=-1)
+        return torch.cat([r_o, r_d], dim=-1).reshape(N, W, H, 1, 6) \
+            .expand(N, W, H, bundle_size, 6)
+
+
+# ---------------------------------------------------------------------------------------------
+# Renderer  (main.py:13-179)
+# ---------------------------------------------------------------------------------------------
+
+def _tile_positions(x0, y0, chunk):
+    gx, gy = torch.meshgrid(torch.arange(x0, x0 + chunk, dtype=torch.float),
+                            torch.arange(y0, y0 + chunk, dtype=torch.float), indexing="ij")
+    return torch.stack([gy, gx], dim=-1)
+
+
+def render(shape, lights, camera, integrator, bsdf, size, chunk_size, background=1.0,
+           with_noise=0.0, crop=None, jitter=None, w_isect=False, camera_noise=None):
+    """pathtrace (main.py:13-93) / pathtrace_sample mode="crop" (main.py:97-179).
+
+    ``crop=(u, v, crop_size)`` renders the crop window; ``jitter`` fixes the coarse-scan
+    jitter (else ``random.random()`` is drawn per tile like the reference); ``camera_noise``
+    is an optional callable ``(u, v) -> (nu, nv)`` replacing the camera's ``rand_like``.
+    """
+    n_cam = len(camera)
+    dims = integrator.dims()
+    if crop is None:
+        u0, v0, extent = 0, 0, size
+    else:
+        u0, v0, extent = crop
+        u0 = max(min(u0, size - extent), 0)
+        v0 = max(min(v0, size - extent), 0)
+        chunk_size = min(chunk_size, extent)
+    assert size % chunk_size == 0
+    out = torch.full([n_cam, extent, extent, dims], float(background))
+    xs = list(range(u0, u0 + extent, chunk_size))
+    ys = list(range(v0, v0 + extent, chunk_size))
+    for ij in range(len(xs) * len(ys)):
+        i, j = divmod(ij, len(ys))
+        x0, y0 = xs[j], ys[i]
+        pos = _tile_positions(x0, y0, chunk_size)
+        if isinstance(camera, NeRFCameraRef):
+            noise = None if camera_noise is None else camera_noise(pos)
+            rays = camera.sample_positions(pos, size, with_noise, noise)
+        else:
+            rays = camera.sample_positions(pos, size)
+        vals, mask, _ = integrator.sample(shape, rays, bsdf, lights, w_isect=w_isect,
+                                          jitter=jitter)
+        valid = mask.any(dim=-1)
+        v = torch.mean(vals, dim=-2)
+        v[~valid] = background
+        out[:, x0 - u0:x0 - u0 + chunk_size, y0 - v0:y0 - v0 + chunk_size] = v
+    if n_cam == 1:
+        out = out.squeeze(0)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Volumetric NeRF baselines  (shapes/nerf.py:153-214)
+# ---------------------------------------------------------------------------------------------
+
+class NeRFLERef(nn.Module):
+    """NeRFLE (envmap=False, NeRF+PT), nerf.py:153-214.
+
+    Reproduces the reference's compositing quirks: ``alpha = 1-exp(-sigma * t)`` with the
+    absolute depth, and ``roll(cumprod, 1)`` with the LAST entry set to 1.
+    """
+
+    def __init__(self, steps=64):
+        super().__init__()
+        self.latent_size = 64
+        self.first = SkipMLP(num_layers=5, hidden_size=128, in_size=3, out=1 + self.latent_size)
+        self.second = SkipMLP(in_size=self.latent_size + 6, out=3)
+        self.steps = steps
+
+    def forward(self, rays, light_location, jitter=None):
+        r_o, r_d = rays.split([3, 3], dim=-1)
+        if jitter is None:
+            jitter = random.random()
+        ts = torch.linspace(0, 2 + jitter * 0.1, self.steps)
+        pts = r_o.unsqueeze(0) + torch.tensordot(ts, r_d, dims=0)
+        first = self.first(pts)
+        latent = first[..., 1:]
+        alpha = first[..., 0, None]
+        light = light_location[None, :, None, None, None, :].expand(latent.shape[:-1] + (3,))
+        rgb = self.second(torch.cat([latent, r_d[None, ...].expand(latent.shape[:-1] + (3,)),
+                                     light], dim=-1)).sigmoid()
+        sigma = F.relu(alpha).squeeze(-1)
+        alpha = 1 - torch.exp(-sigma * ts[:, None, None, None, None].expand_as(sigma))
+        cp = torch.cumprod((1 - alpha).clamp(min=1e-10), dim=0)
+        cp = torch.roll(cp, 1, 0)
+        cp[-1, ...] = 1
+        w = alpha * cp
+        return (w[..., None] * rgb).sum(dim=0)

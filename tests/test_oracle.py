@@ -1,0 +1,123 @@
+"""Oracle pins: the reference's one recorded output plus known-answer tests."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import pathtracer_ref as R
+from oracle import recipes
+
+
+def test_reference_checksum():
+    """the only run of the reference, reproduced bit for bit."""
+    torch.set_num_threads(8)
+    out = recipes.baseline_checksum_render()
+    assert out.shape == (64, 64, 4)
+    assert out.abs().sum().item() == recipes.BASELINE_ABS_SUM
+
+
+def test_unit_sphere_march_kat():
+    """KAT 1: SPHERE_SDF from z=1.5 along -z hits at t=0.5; normal = p_hat; p offset 5e-3."""
+    shape = R.MarchedSDF(sdf=R.unit_sphere_sdf, max_steps=16)
+    rays = torch.tensor([[0.0, 0.0, 1.5, 0.0, 0.0, -1.0],
+                         [0.3, 0.0, 1.5, 0.0, 0.0, -1.0],
+                         [0.0, 3.0, 1.5, 0.0, 0.0, -1.0]])
+    it, hit = shape.intersect(rays, primary=False)
+    assert hit.tolist() == [True, True, False]
+    assert abs(it.t[0].item() - 0.5) < 1e-6
+    n = it.n[1]
+    p_surface = torch.tensor([0.3, 0.0, math.sqrt(1 - 0.09)])
+    assert torch.allclose(n, p_surface, atol=1e-3)
+    assert torch.allclose(it.p[0], torch.tensor([0.0, 0.0, 1.0 + 5e-3]), atol=1e-5)
+
+
+def test_zero_init_mlp_is_zero():
+    """KAT 2: zero_init SkipConnMLP returns exactly 0; one-sphere blob reduces to |p|-r."""
+    torch.manual_seed(0)
+    m = R.SkipMLP(num_layers=8, hidden_size=128, in_size=3, out=1, freqs=32,
+                  activation="softplus", zero_init=True)
+    x = torch.randn(17, 3)
+    assert (m(x) == 0).all()
+    blob = R.SphereBlobSDF(n=1)
+    with torch.no_grad():
+        blob.centers.zero_()
+        blob.radii.fill_(0.5)
+    p = torch.randn(9, 3)
+    expect = -torch.log(torch.exp(-32 * (p.norm(dim=-1) - 0.5)).clamp(min=1e-4)) / 32
+    assert torch.allclose(blob(p), expect, atol=1e-6)
+
+
+def test_fourier_encode_kat():
+    """KAT 3: e_k through an identity basis gives analytic sin/cos."""
+    basis = torch.eye(3)
+    x = torch.eye(3)
+    enc = R.fourier_encode(x, basis)
+    assert torch.allclose(enc[:, 3:6], torch.eye(3) * math.sin(1.0))
+    assert torch.allclose(enc[:, 6:9], torch.ones(3, 3) - torch.eye(3) * (1 - math.cos(1.0)))
+
+
+def test_compositing_closed_form():
+    """KAT 4: NeRFLE rolled-cumprod weights with constant sigma (nerf.py:206-213)."""
+    S = 8
+    ts = torch.linspace(0, 2, S)
+    sigma = 0.7
+    alpha = 1 - torch.exp(-sigma * ts)
+    cp = torch.cumprod((1 - alpha).clamp(min=1e-10), 0)
+    cp = torch.roll(cp, 1, 0)
+    cp[-1] = 1
+    w = alpha * cp
+    trans_all = torch.prod(1 - alpha)
+    assert torch.isclose(w[0], alpha[0] * trans_all)
+    for k in range(1, S - 1):
+        assert torch.isclose(w[k], alpha[k] * torch.prod(1 - alpha[:k]))
+    assert torch.isclose(w[-1], alpha[-1])
+
+
+def test_frame_kat():
+    """KAT 5: coordinate_system(z) = diag(1,-1,1) (t = s x n flips y, interaction.py:25);
+    to_local(from_local(v)) = v_hat."""
+    f = R.shading_frame(torch.tensor([[0.0, 0.0, 1.0]]))
+    assert torch.allclose(f[0], torch.diag(torch.tensor([1.0, -1.0, 1.0])), atol=1e-6)
+    torch.manual_seed(1)
+    n = F.normalize(torch.randn(64, 3), dim=-1)
+    v = torch.randn(64, 3)
+    fr = R.shading_frame(n)
+    back = R.frame_to_local(fr, R.frame_from_local(fr, v))
+    assert torch.allclose(back, F.normalize(v, dim=-1), atol=1e-5)
+
+
+def test_rusinkiewicz_kat():
+    """KAT 6: param_rusin2(z, z): H = z, phi_d from nz(1e-7) pairs."""
+    z = torch.tensor([[0.0, 0.0, 1.0]])
+    out = R.rusinkiewicz(z, z)
+    # diff = rotate(z about y by c=1, s=-sqrt(1e-6)) = [s, 0, c] normalised -> [-1e-3, 0, 1]
+    s = -math.sqrt(1e-6)
+    dx = s / math.sqrt(1 + s * s)
+    expect_phi = math.cos(math.atan2(1e-7, dx))
+    assert abs(out[0, 1].item() - 1.0) < 1e-6
+    assert abs(out[0, 0].item() - expect_phi) < 1e-5
+    assert abs(out[0, 2].item() - 1 / math.sqrt(1 + s * s)) < 1e-6
+
+
+def test_point_light_falloff_kat():
+    """KAT 7: PointLights falloff scale*normalize(I)/(c + l d + q d^2)."""
+    light = R.PointLightRef(location=(0.0, 2.0, 0.0), scale=100.0)
+    it = R.Interaction(p=torch.zeros(1, 1, 1, 1, 3))
+    ds, le = light.sample_direction(it, torch.ones(1, 1, 1, 1, dtype=torch.bool))
+    fall = 1e-6 + 1e-6 * 2 + 1 * 4
+    assert torch.allclose(le.reshape(3), torch.full((3,), 100 / math.sqrt(3) / fall), rtol=1e-6)
+    assert torch.allclose(ds.d.reshape(3), torch.tensor([0.0, 1.0, 0.0]))
+
+
+def test_coarse_scan_argmin_kat():
+    """KAT 8: the scan's argmin on SPHERE_SDF with a fixed jitter."""
+    shape = R.MarchedSDF(sdf=R.unit_sphere_sdf)
+    o = torch.tensor([[0.0, 0.0, 2.0]])
+    d = torch.tensor([[0.0, 0.0, -1.0]])
+    thr, best = shape.coarse_scan(o, d, jitter=0.5)
+    step = (2.2 + 0.5 * 2 / 128) / 128
+    # |2 - t| - 1 is minimised at the sample closest to t = 2 (the centre)
+    k = round(2.0 / step)
+    assert abs(best[0, 2].item() - (2.0 - k * step)) < 1e-5
+    assert thr.item() < -0.99
