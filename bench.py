@@ -1,0 +1,344 @@
+#!/usr/bin/env python
+"""bench.py -- ray-samples/s of the MI355X ray-march render path (BASELINE.json metric).
+
+One step = one frame batch: N views (N = number of ranks) of an 800x800 NeRF-camera render of a
+learned SDF with the nerf_synthetic shading stack, rows dealt round-robin to the ranks in 10-row
+tiles (each rank renders 800x800 rays per step: weak scaling), then one RCCL all-gather of the
+row slabs at the end of the step.  Per frame the reference work is W*H*(S + 130) SDF-MLP
+evaluations (S = 64 march steps, 130 = coarse scan, sdfs.py:119-131, 232-249) plus shading on the
+hit rays; the headline unit is the metric's ray-sample = W*H*S per frame.
+
+Scene (synthetic, seeded): SphereSDF-style prior (one sphere r=0.25) + an 8x256
+SkipConnMLP shift (F=16, sigma=32, softplus, default torch init, output layer x0.1) -- the metric's
+"8x256 MLP", evaluated at every sample; ComposeSpatialVarying([NeuralBSDF(Softplus)] x 8) with its
+16x256 spatial MLP; LightField (10x256); NeRFIntegrator(Direct()).
+"""
+import argparse
+import json
+import math
+import os
+import random
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FLOP_SDF_8x256 = 1_120_864  # per evaluation (F=16, in 3, out 1)
+SCAN_EVALS = 130             # sdf(o) + 128 samples + sdf(best)
+PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=800)
+    ap.add_argument("--samples", type=int, default=64, help="march steps per ray (max_steps)")
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--tile-rows", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-crop", type=int, default=48, help="side of the CPU-baseline crop")
+    ap.add_argument("--no-fp32-check", action="store_true")
+    return ap.parse_args()
+
+
+def look_at(eye):
+    eye = torch.tensor(eye, dtype=torch.float)
+    fwd = F.normalize(-eye, dim=0)
+    right = F.normalize(torch.cross(fwd, torch.tensor([0.0, 1.0, 0.0]), dim=0), dim=0)
+    up = torch.cross(right, fwd, dim=0)
+    c2w = torch.zeros(3, 4)
+    c2w[:, 0], c2w[:, 1], c2w[:, 2], c2w[:, 3] = right, up, -fwd, eye
+    return c2w
+
+
+def view_c2w(i, n):
+    a = 2 * math.pi * i / max(n, 1) + 0.3
+    return look_at((math.sin(a) * math.cos(0.4), math.sin(0.4), math.cos(a) * math.cos(0.4)))
+
+
+def build_scene(device, samples, seed=0):
+    """Product objects of the bench scene (identical on every rank)."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, NeuralBSDF
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.lights import LightField
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    torch.manual_seed(seed)
+    random.seed(seed)
+    sphere = SphereSDF(n=1, device="cpu")
+    with torch.no_grad():
+        sphere.centers.zero_()
+        sphere.radii.fill_(0.25)
+    sphere.shift = SkipConnMLP(num_layers=8, hidden_size=256, in_size=3, out=1, freqs=16,
+                               activation=F.softplus, device="cpu")
+    with torch.no_grad():
+        sphere.shift.out.weight.mul_(0.1)
+        sphere.shift.out.bias.mul_(0.1)
+    shape = SDF(sdf=sphere.to(device), device=device, max_steps=samples)
+    bsdf = ComposeSpatialVarying([NeuralBSDF(activation=torch.nn.Softplus(), device="cpu")
+                                  for _ in range(8)], device="cpu")
+    for b in bsdf.bsdfs:
+        b.mlp.to(device)
+    bsdf.sp_var_fn.to(device)
+    lights = LightField(device="cpu").to(device)
+    return dict(shape=shape, bsdf=bsdf, lights=lights, integrator=NeRFIntegrator(Direct()),
+                pt=pt)
+
+
+def oracle_scene(scene):
+    """The same weights in the CPU oracle (cpu_baseline leg only)."""
+    from oracle import pathtracer_ref as R
+    blob = R.SphereBlobSDF(n=1, shift_hidden=256, shift_freqs=16, shift_zero_init=False)
+    src = scene["shape"].sdf
+    with torch.no_grad():
+        blob.centers.copy_(src.centers.cpu())
+        blob.radii.copy_(src.radii.cpu())
+        blob.tfs.copy_(src.tfs.cpu())
+    _copy_to_oracle(blob.shift, src.shift)
+    parts = [R.NeuralBSDFRef(activation="softplus") for _ in scene["bsdf"].bsdfs]
+    for o, p in zip(parts, scene["bsdf"].bsdfs):
+        _copy_to_oracle(o.mlp, p.mlp)
+    bsdf = R.SpatialMixBSDF(parts)
+    _copy_to_oracle(bsdf.sp_var_fn, scene["bsdf"].sp_var_fn)
+    lights = R.LightFieldRef()
+    _copy_to_oracle(lights.light_field_approx, scene["lights"].light_field_approx)
+    shape = R.MarchedSDF(sdf=blob, max_steps=scene["shape"].max_steps)
+    return dict(shape=shape, bsdf=bsdf, lights=lights,
+                integrator=R.NeRFIntegratorRef(R.DirectRef()))
+
+
+def _copy_to_oracle(dst, src):
+    with torch.no_grad():
+        dst.basis_p = src.basis_p.detach().cpu().clone()
+        for a, b in zip([dst.init, *dst.layers, dst.out], src._linears()):
+            a.weight.copy_(b.weight.cpu())
+            a.bias.copy_(b.bias.cpu())
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer.render import RowRenderer, row_shard
+    _lib.load(require_device=True)
+    nra.set_precision(args.precision)
+
+    size = args.size
+    scene = build_scene(device, args.samples)
+    pt = scene["pt"]
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    c2w = torch.stack([view_c2w(i, world) for i in range(world)]).to(device)
+    cameras = pt.cameras.NeRFCamera(cam_to_world=c2w, focal=focal, device=device)
+    rows = row_shard(size, rank, world, args.tile_rows)
+    rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
+                     size, rows, background=0.0, with_noise=1e-3, device=device)
+    max_rows = max(len(row_shard(size, r, world, args.tile_rows)) for r in range(world))
+    gather_buf = torch.zeros(world, world, max_rows, size, 4, device=device)
+    full = torch.zeros(world, size, size, 4, device=device)
+
+    def step():
+        img = rr.render()
+        if world > 1:
+            import torch.distributed as dist
+            slab = torch.zeros(world, max_rows, size, 4, device=device)
+            slab[:, :len(rows)] = img
+            dist.all_gather_into_tensor(gather_buf.view(world * world, max_rows, size, 4), slab)
+            for r in range(world):
+                rws = row_shard(size, r, world, args.tile_rows)
+                full[:, rws] = gather_buf[r, :, :len(rws)]
+        else:
+            full[:, rows] = img
+        return full
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        elapsed = time.perf_counter() - t0
+        _lib.profile_enable(False)
+        k_ms, k_n = _lib.profile_read("k_intersect")
+        if world > 1:
+            t = torch.tensor([elapsed], device=device)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            elapsed = t.item()
+
+    ms_step = 1000 * elapsed / args.steps
+    rays_per_rank = len(rows) * size * world  # this rank's rows of every view
+    rays_total = world * size * size * args.steps
+    value = rays_total * args.samples / elapsed
+    flop_launch = rays_per_rank * (args.samples + SCAN_EVALS) * FLOP_SDF_8x256
+    avg_kernel_ms = k_ms / max(k_n, 1)
+    achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_intersect.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("size") == size and pm.get("precision") == args.precision:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    extra = {}
+    if rank == 0 and world == 1:
+        with torch.no_grad():
+            hit_frac = float(rr_hit_fraction(rr))
+        extra["hit_fraction"] = round(hit_frac, 4)
+        if not args.no_fp32_check and args.precision == "fp16":
+            extra["psnr_fp16_vs_fp32"] = round(psnr_vs_fp32(scene, cameras, size), 2)
+        if not args.no_cpu_baseline:
+            extra.update(cpu_baseline(scene, size, args))
+
+    if rank == 0:
+        line = {
+            "metric": "ray-samples/sec/GPU (800x800x64, 8x256 MLP); PSNR vs ref",
+            "value": value,
+            "unit": "ray-samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (seeded random-init weights, SphereSDF prior + 8x256 shift MLP)",
+            "config": {
+                "workload": f"{size}x{size} NeRFCamera frame per GPU, {args.samples} march steps + "
+                            f"{SCAN_EVALS}-eval coarse scan per ray, SDF MLP 8x256 F16, "
+                            "8x NeuralBSDF(6x96) + 16x256 spatial MLP + LightField(10x256), "
+                            "NeRFIntegrator(Direct)",
+                "image": [size, size],
+                "samples_per_ray": args.samples,
+                "views_per_step": world,
+                "parallelism": f"row-tile shard x{world} ({args.tile_rows}-row tiles) + RCCL all-gather",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "kernel": "k_intersect",
+                "achieved": achieved,
+                "peak": peak,
+                "unit": "TFLOP/s",
+                "frac": achieved / peak,
+                "traffic": traffic,
+                "flop_per_launch": flop_launch,
+                "avg_kernel_ms": avg_kernel_ms,
+                "launches": k_n,
+            },
+            "sdf_evals_per_s": rays_total * (args.samples + SCAN_EVALS) / elapsed,
+        }
+        if "cpu_baseline" in extra:
+            line["cpu_baseline"] = extra.pop("cpu_baseline")
+        line.update(extra)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def rr_hit_fraction(rr):
+    from neural_raytracing_amd.pathtracer import render as R
+    for b in R._BUFS.values():
+        return b.hit.float().mean().item()
+    return 0.0
+
+
+def psnr_vs_fp32(scene, cameras, size, crop=200):
+    """PSNR of the fp16 render against the fp32 render of a central crop (no camera jitter)."""
+    import neural_raytracing_amd as nra
+    pt = scene["pt"]
+    c0 = (size - crop) // 2
+    imgs = {}
+    for prec in ("fp32", "fp16"):
+        nra.set_precision(prec)
+        random.seed(123)
+        img, _ = pt.pathtrace_sample(scene["shape"], scene["lights"], single_camera(cameras),
+                                     scene["integrator"], bsdf=scene["bsdf"], size=size,
+                                     chunk_size=size, bundle_size=1, crop_size=crop, uv=(c0, c0),
+                                     background=0, with_noise=0.0)
+        imgs[prec] = img.clamp(0, 1)
+    nra.set_precision("fp16")
+    mse = ((imgs["fp16"] - imgs["fp32"]) ** 2).mean().item()
+    return -10 * math.log10(max(mse, 1e-12))
+
+
+def single_camera(cameras):
+    return type(cameras)(cam_to_world=cameras.cam_to_world[:1], focal=cameras.focal,
+                         device=cameras.device)
+
+
+def cpu_baseline(scene, size, args):
+    """The CPU restatement (oracle/, 'port') on this host's cores over a bounded crop, plus the
+    PSNR of the GPU render of the same crop against it."""
+    import neural_raytracing_amd as nra
+    from oracle import pathtracer_ref as R
+    threads = torch.get_num_threads()
+    osc = oracle_scene(scene)
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    c2w = view_c2w(0, 1).unsqueeze(0)
+    ocam = R.NeRFCameraRef(c2w, focal)
+    crop = args.cpu_crop
+    c0 = (size - crop) // 2
+    random.seed(7)
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        want = R.render(osc["shape"], osc["lights"], ocam, osc["integrator"], osc["bsdf"], size=size,
+                        chunk_size=size, background=0.0, with_noise=0.0, crop=(c0, c0, crop))
+    cpu_s = time.perf_counter() - t0
+    rate = crop * crop * args.samples / cpu_s
+    pt = scene["pt"]
+    gcam = pt.cameras.NeRFCamera(cam_to_world=c2w.cuda(), focal=focal)
+    psnr = {}
+    for prec in ("fp32", args.precision):
+        nra.set_precision(prec)
+        random.seed(7)
+        with torch.no_grad():
+            got, _ = pt.pathtrace_sample(scene["shape"], scene["lights"], gcam, scene["integrator"],
+                                         bsdf=scene["bsdf"], size=size, chunk_size=size,
+                                         bundle_size=1, crop_size=crop, uv=(c0, c0), background=0,
+                                         with_noise=0.0)
+        got = got.cpu().clamp(0, 1)
+        mse = ((got - want.clamp(0, 1)) ** 2).mean().item()
+        psnr[prec] = -10 * math.log10(max(mse, 1e-12))
+        if prec == "fp32":
+            maxdiff = (got - want.clamp(0, 1)).abs().max().item()
+    nra.set_precision(args.precision)
+    return {
+        "cpu_baseline": {"value": rate, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+                         "sample": f"{crop}x{crop} crop of the same frame, {args.samples} march steps + "
+                                   f"coarse scan + shading, oracle/pathtracer_ref.py, {cpu_s:.1f} s"},
+        "psnr_vs_ref": round(psnr[args.precision], 2),
+        "fp32_maxabs_vs_ref": maxdiff,
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+/*
+ * nrt.h -- C ABI of libnrt_hip.so, the MI355X (gfx950) ray-march render path.
+ *
+ * The reference (prashantraina/neural_raytracing, pytorch3d/pathtracer) has no FFI: its hot path
+ * sits behind duck-typed Python objects.  Each entry point below replaces one of those Python
+ * call sites; the comment on each names the reference file:line it stands in for.  The Python
+ * host layer (neural_raytracing_amd/pathtracer) binds these with ctypes.
+ *
+ * Conventions
+ *   - All array pointers are DEVICE memory owned by the caller unless the name says host_.
+ *   - Every compute call is stream-ordered on the caller's hipStream_t (passed as void*);
+ *     nothing synchronises the device and nothing allocates device memory except the
+ *     *_create functions (weights are packed once) and nrt_workspace_* helpers.
+ *   - Rays are [P, 6] float32 = origin(3) || direction(3), P = N*W*H*B flattened in the
+ *     reference's [N, W, H, B] order.
+ *   - Return value: 0 on success, negative NRT_E* on error; nrt_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - precision: NRT_FP32 computes every MLP layer with exact-f32 MFMA (v_mfma_f32_32x32x2_f32)
+ *     and matches the CPU restatement to ~1e-6; NRT_FP16 uses v_mfma_f32_32x32x16_f16 with f32
+ *     accumulation (the throughput path, judged by PSNR against FP32).
+ */
+#ifndef NRT_H_
+#define NRT_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NRT_OK 0
+#define NRT_EINVAL (-1)
+#define NRT_EUNSUPPORTED (-2)
+#define NRT_EHIP (-3)
+#define NRT_ENOMEM (-4)
+
+#define NRT_FP32 0
+#define NRT_FP16 1
+
+/* activations (neural_blocks.py:26 leaky_relu default; sdfs.py:29 softplus) */
+#define NRT_ACT_LEAKY_RELU 0
+#define NRT_ACT_SOFTPLUS 1
+#define NRT_ACT_NONE 2
+#define NRT_ACT_SIGMOID 3
+#define NRT_ACT_RELU 4
+
+const char* nrt_last_error(void);
+int nrt_version(void);
+/* 1 when the library was built for gfx950 and a device is visible; 0 otherwise */
+int nrt_device_ok(void);
+
+/* ---------------------------------------------------------------------------------------
+ * SkipConnMLP (neural_blocks.py:12-86 + utils.py:33-40 fourier2)
+ * ------------------------------------------------------------------------------------- */
+typedef struct nrt_mlp nrt_mlp;
+
+typedef struct {
+  int32_t in_size;     /* input features (3 for points)                                   */
+  int32_t hidden;      /* hidden width, multiple of 32 (32..256)                          */
+  int32_t num_layers;  /* hidden Linear layers (skip-concat layers counted)               */
+  int32_t out;         /* output features (<= 96)                                         */
+  int32_t freqs;       /* Fourier features F: basis is [in_size, F]                       */
+  int32_t skip;        /* skip period: layer i concatenates the encoding iff              */
+                       /*   i != num_layers-1 && i % skip == 0   (neural_blocks.py:48,82) */
+  int32_t latent;      /* latent_size appended to the encoding                            */
+  int32_t activation;  /* NRT_ACT_*                                                       */
+} nrt_mlp_desc;
+
+/* Pack host float32 weights (torch layout).  host_basis: [in_size, F] (basis_p).
+ * host_weights[l], host_biases[l] for l = 0 (init: [hidden, dp]), 1..num_layers (layers[i]:
+ * [hidden, hidden (+dp if skip)]), num_layers+1 (out: [out, hidden]); dp = in+2F+latent.
+ * Replaces the per-call eager Linear chain (neural_blocks.py:75-86). */
+int nrt_mlp_create(const nrt_mlp_desc* desc, const float* host_basis,
+                   const float* const* host_weights, const float* const* host_biases,
+                   nrt_mlp** out);
+int nrt_mlp_destroy(nrt_mlp* mlp);
+
+/* y[M, out] = SkipConnMLP(x[M, in], latent[M, latent]) -- neural_blocks.py:75-86 */
+int nrt_mlp_forward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,
+                    float* y, int precision, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Signed distance fields (shapes/sdfs.py)
+ * ------------------------------------------------------------------------------------- */
+typedef struct nrt_sdf nrt_sdf;
+
+/* SPHERE_SDF = |p| - 1 (sdfs.py:13) */
+int nrt_sdf_create_unit_sphere(nrt_sdf** out);
+/* a bare SkipConnMLP with out=1 used as the SDF */
+int nrt_sdf_create_mlp(const nrt_mlp* mlp, nrt_sdf** out);
+/* SphereSDF (sdfs.py:16-44): smooth_min_k(|(I+tfs_i) p - c_i| - r_i) + shift(p).
+ * host_centers [n,3], host_radii [n], host_tfs [n,3,3]; shift may be NULL. */
+int nrt_sdf_create_sphere_blob(int32_t n, const float* host_centers, const float* host_radii,
+                               const float* host_tfs, float k, const nrt_mlp* shift,
+                               nrt_sdf** out);
+int nrt_sdf_destroy(nrt_sdf* sdf);
+
+/* out[M] = sdf(p[M,3]) */
+int nrt_sdf_eval(const nrt_sdf* sdf, const float* p, int64_t M, float* out, int precision,
+                 void* stream);
+/* out[M,3] = d sdf / d p  (SDF.autograd_diff, sdfs.py:184-197; f32 backward) */
+int nrt_sdf_grad(const nrt_sdf* sdf, const float* p, int64_t M, float* grad, void* stream);
+
+typedef struct {
+  int32_t max_steps;   /* SDF.max_steps (sdfs.py:96; scripts set 32/64/256)               */
+  float epsilon;       /* SDF.epsilon 1e-3                                                 */
+  float max_t;         /* intersect(max_t=10)                                              */
+  int32_t primary;     /* 1: run the 128-step coarse scan (SDF.throughput, sdfs.py:232)     */
+  double scan_max_t;   /* dist + random.random()*(2/128), computed by the caller           */
+  int32_t precision;   /* NRT_FP32 / NRT_FP16                                               */
+} nrt_march_params;
+
+/* SDF.intersect (sdfs.py:111-160) for P rays.  Outputs (each [P] or [P,3]):
+ *   t, hit (uint8), p (offset by 5*eps*n on hits), n (unit normal, 0 on misses),
+ *   raw_n (un-normalised gradient, 0 on misses; may be NULL), wi = to_local(-d) (NULL ok),
+ *   throughput (-1000*sdf(best scan point); untouched when primary == 0).
+ * hit_idx[P] / hit_count[1] (int32, optional): compacted indices of hit rays (any order).
+ * workspace: nrt_intersect_workspace_bytes(P) bytes of device memory. */
+size_t nrt_intersect_workspace_bytes(const nrt_sdf* sdf, int64_t P);
+int nrt_sdf_intersect(const nrt_sdf* sdf, const float* rays, int64_t P,
+                      const nrt_march_params* params, float* t, uint8_t* hit, float* p, float* n,
+                      float* raw_n, float* wi, float* throughput, int32_t* hit_idx,
+                      int32_t* hit_count, void* workspace, void* stream);
+
+/* SDF.intersect_test (sdfs.py:162-181): visible[P] = (t >= max_t[P]) | still-marching,
+ * march from t0 = 100*eps.  max_t is per ray (scene.py:296 passes the light distance). */
+int nrt_sdf_occlusion(const nrt_sdf* sdf, const float* rays, int64_t P, const float* max_t,
+                      int32_t max_steps, float epsilon, uint8_t* visible, int precision,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Lights (lights/lights.py) and BSDFs (bsdf/bsdfs.py)
+ * ------------------------------------------------------------------------------------- */
+typedef struct nrt_light nrt_light;
+typedef struct nrt_bsdf nrt_bsdf;
+
+/* LightField (lights.py:155-195): 10x256 MLP -> direction/magnitude, colour = sigmoid(c) */
+int nrt_light_create_field(const nrt_mlp* mlp, const float* host_color3, nrt_light** out);
+/* PointLights (lights.py:40-110), one light */
+int nrt_light_create_point(const float* host_location3, const float* host_intensity3,
+                           float constant, float linear, float square, float scale,
+                           nrt_light** out);
+int nrt_light_destroy(nrt_light* light);
+
+#define NRT_BSDF_NEURAL 0     /* NeuralBSDF (bsdfs.py:613-637): act(MLP(param_rusin2))     */
+#define NRT_BSDF_DIFFUSE 1    /* Diffuse (bsdfs.py:78-118)                                 */
+#define NRT_BSDF_CONDUCTOR 2  /* Conductor (bsdfs.py:345-388)                              */
+
+typedef struct {
+  int32_t kind;          /* NRT_BSDF_*                                                     */
+  const nrt_mlp* mlp;    /* NEURAL only                                                    */
+  int32_t activation;    /* NEURAL: act; DIFFUSE: preprocess (NONE = x/pi, SIGMOID, ...);  */
+                         /* CONDUCTOR: act on specular                                      */
+  float params[4];       /* DIFFUSE: reflectance rgb; CONDUCTOR: specular rgb, eta         */
+} nrt_bsdf_component;
+
+/* ComposeSpatialVarying (bsdfs.py:482-536): sum_j sigmoid(sp_var(p))_j * f_j.
+ * spatial may be NULL for a single component (weight 1, no sigmoid). */
+int nrt_bsdf_create(int32_t n, const nrt_bsdf_component* components, const nrt_mlp* spatial,
+                    nrt_bsdf** out);
+int nrt_bsdf_destroy(nrt_bsdf* bsdf);
+
+/* Direct.sample's emitter + BSDF block (integrators.py:173-189) for the hit rays listed in
+ * hit_idx[0 .. *hit_count): light sample at p, wo = to_local(frame(n), d_light),
+ * rgb[i] = (sum_j k_j f_j(wi, wo)) * Le.  rgb of rays not listed is left untouched.
+ * weights_out [P, n_components] (optional): the sigmoid spatial weights
+ * (it.normalized_weights, bsdfs.py:520). */
+int nrt_shade_direct(const nrt_bsdf* bsdf, const nrt_light* light, const float* p,
+                     const float* n, const float* wi, const int32_t* hit_idx,
+                     const int32_t* hit_count, int64_t P, float* rgb, float* weights_out,
+                     int precision, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Cameras (cameras/cameras.py) and the tile composite (main.py:85-90, integrators.py:251)
+ * ------------------------------------------------------------------------------------- */
+#define NRT_CAM_NERF 0   /* NeRFCamera.sample_positions (cameras.py:23-54)                   */
+#define NRT_CAM_DTU 1    /* DTUCamera.sample_positions + lift (cameras.py:132-192)           */
+#define NRT_CAM_FOV 2    /* FoVPerspectiveCameras.sample_positions (renderer/cameras.py:539)  */
+
+typedef struct {
+  int32_t kind;
+  int32_t size;            /* `size` argument of pathtrace                                  */
+  float focal;             /* NERF                                                          */
+  float mat[16];           /* NERF: c2w [3,4] row-major; DTU: pose [4,4];                   */
+                           /* FOV: inverse full-projection [4,4] (row-vector convention)    */
+  float intrinsic[16];     /* DTU: K [4,4]                                                  */
+  float origin[3];         /* FOV: camera centre                                            */
+} nrt_camera;
+
+/* rays[(n*W + x)*H + y][6] for tile rows x in [x0, x0+W), cols y in [y0, y0+H) of camera n.
+ * Pixel (x, y) uses u = y0+y, v = x0+x (main.py:71 stacks [gy, gx]) unless `positions`
+ * ([W, H, 2] device, (u, v) per pixel, the reference's position_samples) is given.
+ * noise (device, uniforms in [0,1), NULL = none; with_noise is the jitter amplitude):
+ *   NERF: [2, W, H] -- u plane then v plane (two rand_like draws, cameras.py:35-36);
+ *   FOV:  [W, H, 2] -- interleaved (one sampler draw, renderer/cameras.py:553-555);
+ *   DTU ignores it (cameras.py:156-192 never reads with_noise). */
+int nrt_raygen(const nrt_camera* host_cams, int32_t N, int32_t x0, int32_t y0, int32_t W,
+               int32_t H, float with_noise, const float* noise, const float* positions,
+               float* rays, void* stream);
+
+/* SurfaceInteraction.set_normals + to_local(-d) (interaction.py:73-78, sdfs.py:158-159):
+ * frame[P,9] = coordinate_system(n) as [s | t | n] columns (row-major 3x3, may be NULL) and
+ * wi[P,3] = to_local(frame, -d) (may be NULL). */
+int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi,
+               void* stream);
+
+/* image[n, X0+x, Y0+y, :] for the tile = rgb (3 ch) and, when alpha_from_throughput,
+ * sigmoid(throughput) as the 4th channel (NeRFIntegrator, integrators.py:249-257); pixels
+ * whose hit==0 take `background` when fill_misses (main.py:88-89).  img_w, img_h, channels
+ * describe the destination [N, img_w, img_h, channels] float32 image. */
+int nrt_composite(const float* rgb, const float* throughput, const uint8_t* hit, int32_t N,
+                  int32_t W, int32_t H, int32_t alpha_from_throughput, int32_t fill_misses,
+                  float background, float* image, int32_t img_w, int32_t img_h,
+                  int32_t channels, int32_t X0, int32_t Y0, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Kernel timing (bench / profiling aid; no reference counterpart)
+ * When enabled, the heavy launches (k_intersect, k_sdf_grad, k_shade_direct, k_mlp_forward)
+ * are bracketed by hipEvents on the stream they run on.  nrt_profile_read synchronises those
+ * events and returns the summed duration and launch count of kernel `name`.
+ * ------------------------------------------------------------------------------------- */
+void nrt_profile_enable(int on);
+void nrt_profile_reset(void);
+int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NRT_H_ */

@@ -1,0 +1,172 @@
+"""ctypes binding of libnrt_hip.so (include/nrt.h).
+
+The library is loaded lazily on first use, after torch (so the process has a single HIP
+runtime: torch's libamdhip64.so.7 satisfies the library's NEEDED entry).  There is no CPU
+fallback: any compute call without the library or without a gfx950 device raises.
+"""
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnrt_hip.so")
+
+NRT_FP32 = 0
+NRT_FP16 = 1
+
+ACT = {"leaky_relu": 0, "softplus": 1, "none": 2, "sigmoid": 3, "relu": 4}
+
+NRT_BSDF_NEURAL, NRT_BSDF_DIFFUSE, NRT_BSDF_CONDUCTOR = 0, 1, 2
+NRT_CAM_NERF, NRT_CAM_DTU, NRT_CAM_FOV = 0, 1, 2
+
+
+class NrtError(RuntimeError):
+    pass
+
+
+class MlpDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("in_size", "hidden", "num_layers", "out", "freqs", "skip", "latent", "activation")]
+
+
+class MarchParams(ctypes.Structure):
+    _fields_ = [("max_steps", ctypes.c_int32), ("epsilon", ctypes.c_float),
+                ("max_t", ctypes.c_float), ("primary", ctypes.c_int32),
+                ("scan_max_t", ctypes.c_double), ("precision", ctypes.c_int32)]
+
+
+class BsdfComponent(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("mlp", ctypes.c_void_p),
+                ("activation", ctypes.c_int32), ("params", ctypes.c_float * 4)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("size", ctypes.c_int32), ("focal", ctypes.c_float),
+                ("mat", ctypes.c_float * 16), ("intrinsic", ctypes.c_float * 16),
+                ("origin", ctypes.c_float * 3)]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+
+_SIGNATURES = {
+    "nrt_last_error": (ctypes.c_char_p, []),
+    "nrt_version": (_I32, []),
+    "nrt_device_ok": (_I32, []),
+    "nrt_mlp_create": (_I32, [ctypes.POINTER(MlpDesc), _P, _P, _P, ctypes.POINTER(_P)]),
+    "nrt_mlp_destroy": (_I32, [_P]),
+    "nrt_mlp_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P]),
+    "nrt_sdf_create_unit_sphere": (_I32, [ctypes.POINTER(_P)]),
+    "nrt_sdf_create_mlp": (_I32, [_P, ctypes.POINTER(_P)]),
+    "nrt_sdf_create_sphere_blob": (_I32, [_I32, _P, _P, _P, _F, _P, ctypes.POINTER(_P)]),
+    "nrt_sdf_destroy": (_I32, [_P]),
+    "nrt_sdf_eval": (_I32, [_P, _P, _I64, _P, _I32, _P]),
+    "nrt_sdf_grad": (_I32, [_P, _P, _I64, _P, _P]),
+    "nrt_intersect_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
+    "nrt_sdf_intersect": (_I32, [_P, _P, _I64, ctypes.POINTER(MarchParams), _P, _P, _P, _P, _P,
+                                 _P, _P, _P, _P, _P, _P]),
+    "nrt_sdf_occlusion": (_I32, [_P, _P, _I64, _P, _I32, _F, _P, _I32, _P]),
+    "nrt_light_create_field": (_I32, [_P, _P, ctypes.POINTER(_P)]),
+    "nrt_light_create_point": (_I32, [_P, _P, _F, _F, _F, _F, ctypes.POINTER(_P)]),
+    "nrt_light_destroy": (_I32, [_P]),
+    "nrt_bsdf_create": (_I32, [_I32, _P, _P, ctypes.POINTER(_P)]),
+    "nrt_bsdf_destroy": (_I32, [_P]),
+    "nrt_shade_direct": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I32, _P]),
+    "nrt_raygen": (_I32, [_P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P]),
+    "nrt_frames": (_I32, [_P, _P, _I64, _P, _P, _P]),
+    "nrt_profile_enable": (None, [_I32]),
+    "nrt_profile_reset": (None, []),
+    "nrt_profile_read": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(_I64)]),
+    "nrt_composite": (_I32, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _I32, _I32, _I32,
+                             _I32, _I32, _P]),
+}
+
+_lib = None
+
+
+def exported_symbols():
+    return list(_SIGNATURES)
+
+
+def load(require_device=False):
+    """Load the library (once).  Raises NrtError if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NrtError(f"{LIB_PATH} not built: run __graft_entry__.build() or "
+                           "python -m neural_raytracing_amd.build")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    if require_device and not torch.cuda.is_available():
+        raise NrtError("the HIP render path needs a gfx950 GPU (torch.cuda.is_available() is False)")
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = _lib.nrt_last_error().decode() if _lib is not None else ""
+        raise NrtError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name, *args):
+    lib = load(require_device=True)
+    check(getattr(lib, name)(*args), name)
+
+
+def ptr(t):
+    """Raw device pointer of a contiguous tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise NrtError("tensor passed to the HIP library must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+# ---------------------------------------------------------------------------------------------
+# precision
+# ---------------------------------------------------------------------------------------------
+_precision = {"value": NRT_FP16 if os.environ.get("NRT_PRECISION", "fp32") == "fp16" else NRT_FP32}
+
+
+def set_precision(p):
+    """'fp32' (exact-f32 MFMA, parity with the reference) or 'fp16' (f16 MFMA, f32 accumulate)."""
+    if p not in ("fp32", "fp16"):
+        raise ValueError("precision must be 'fp32' or 'fp16'")
+    _precision["value"] = NRT_FP16 if p == "fp16" else NRT_FP32
+
+
+def get_precision():
+    return "fp16" if _precision["value"] == NRT_FP16 else "fp32"
+
+
+def precision_code():
+    return _precision["value"]
+
+
+def profile_enable(on=True):
+    load().nrt_profile_enable(1 if on else 0)
+
+
+def profile_reset():
+    load().nrt_profile_reset()
+
+
+def profile_read(name):
+    """(total_ms, launches) of kernel `name` since the last reset (synchronises its events)."""
+    tot = ctypes.c_double()
+    n = ctypes.c_int64()
+    check(load().nrt_profile_read(name.encode(), ctypes.byref(tot), ctypes.byref(n)),
+          "nrt_profile_read")
+    return tot.value, n.value

@@ -1,0 +1,252 @@
+// nrt_api_sdf.hip -- SDF handles, evaluation, gradient, intersect and occlusion launchers
+#include "nrt_launch.h"
+
+using namespace nrt;
+
+extern "C" {
+static int sdf_finish(std::unique_ptr<nrt_sdf>& s, nrt_sdf** out) {
+  NRT_HIP(hipMalloc(&s->dev, sizeof(SdfDev)));
+  NRT_HIP(hipMemcpy(s->dev, &s->host_dev, sizeof(SdfDev), hipMemcpyHostToDevice));
+  *out = s.release();
+  return NRT_OK;
+}
+
+int nrt_sdf_create_unit_sphere(nrt_sdf** out) {
+  if (!out) return NRT_EINVAL;
+  std::unique_ptr<nrt_sdf> s(new nrt_sdf());
+  std::memset(&s->host_dev, 0, sizeof(SdfDev));
+  s->host_dev.kind = 0;
+  return sdf_finish(s, out);
+}
+
+int nrt_sdf_create_mlp(const nrt_mlp* mlp, nrt_sdf** out) {
+  if (!mlp || !out) { set_error("nrt_sdf_create_mlp: null"); return NRT_EINVAL; }
+  if (mlp->desc.out < 1 || mlp->desc.in_size != 3) {
+    set_error("nrt_sdf_create_mlp: SDF MLP must map 3 -> >=1 (output 0 is the distance)");
+    return NRT_EINVAL;
+  }
+  std::unique_ptr<nrt_sdf> s(new nrt_sdf());
+  std::memset(&s->host_dev, 0, sizeof(SdfDev));
+  s->host_dev.kind = 1;
+  s->host_dev.mlp = mlp->dev;
+  s->host_dev.nb = mlp->desc.hidden / 32;
+  s->mlp = mlp;
+  return sdf_finish(s, out);
+}
+
+int nrt_sdf_create_sphere_blob(int32_t n, const float* centers, const float* radii,
+                               const float* tfs, float k, const nrt_mlp* shift, nrt_sdf** out) {
+  if (n < 1 || !centers || !radii || !tfs || !out) { set_error("nrt_sdf_create_sphere_blob: bad argument"); return NRT_EINVAL; }
+  if (shift && (shift->desc.in_size != 3 || shift->desc.out < 1)) {
+    set_error("nrt_sdf_create_sphere_blob: shift MLP must map 3 -> 1");
+    return NRT_EINVAL;
+  }
+  std::unique_ptr<nrt_sdf> s(new nrt_sdf());
+  std::memset(&s->host_dev, 0, sizeof(SdfDev));
+  std::vector<float> packed((size_t)n * 16, 0.f);
+  for (int i = 0; i < n; ++i) {
+    float* d = &packed[(size_t)i * 16];
+    // (tfs + I): sdfs.py:38
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) d[3 * a + b] = tfs[(size_t)i * 9 + 3 * a + b] + (a == b ? 1.f : 0.f);
+    d[9] = centers[i * 3]; d[10] = centers[i * 3 + 1]; d[11] = centers[i * 3 + 2];
+    d[12] = radii[i];
+  }
+  NRT_HIP(hipMalloc(&s->spheres, packed.size() * sizeof(float)));
+  NRT_HIP(hipMemcpy(s->spheres, packed.data(), packed.size() * sizeof(float), hipMemcpyHostToDevice));
+  s->host_dev.kind = 2;
+  s->host_dev.n_spheres = n;
+  s->host_dev.k = k;
+  s->host_dev.spheres = s->spheres;
+  s->host_dev.mlp = shift ? shift->dev : nullptr;
+  s->host_dev.nb = shift ? shift->desc.hidden / 32 : 0;
+  s->mlp = shift;
+  return sdf_finish(s, out);
+}
+
+int nrt_sdf_destroy(nrt_sdf* s) {
+  if (!s) return NRT_OK;
+  if (s->spheres) (void)hipFree(s->spheres);
+  if (s->dev) (void)hipFree(s->dev);
+  delete s;
+  return NRT_OK;
+}
+
+int nrt_sdf_eval(const nrt_sdf* s, const float* p, int64_t M, float* out, int precision, void* stream) {
+  if (!s || M < 0) { set_error("nrt_sdf_eval: bad argument"); return NRT_EINVAL; }
+  if (M == 0) return NRT_OK;
+  if (!p || !out) { set_error("nrt_sdf_eval: null p / out"); return NRT_EINVAL; }
+  const bool f16 = precision == NRT_FP16;
+  int hidden, ke;
+  sdf_dims(s, hidden, ke);
+  LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
+  dim3 grid(ceil_div64(ceil_div64(M, 32), lp.waves)), block(64 * lp.waves);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = NRT_OK;
+  NRT_NB_SWITCH(s->host_dev.nb, {
+    if (f16) {
+      if (!(rc = set_lds(k_sdf_eval<true, NB>, lp.bytes)))
+        k_sdf_eval<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, p, M, out, lp.RS, lp.per_wave);
+    } else {
+      if (!(rc = set_lds(k_sdf_eval<false, NB>, lp.bytes)))
+        k_sdf_eval<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, p, M, out, lp.RS, lp.per_wave);
+    }
+  });
+  if (rc) return rc;
+  return check_launch("k_sdf_eval");
+}
+
+// gradient launch shared by nrt_sdf_grad and the normal pass of nrt_sdf_intersect
+static const int kGradBlocks = 512;
+
+static size_t grad_scratch_floats_per_wave(const nrt_sdf* s) {
+  if (!s->mlp) return 0;
+  return (size_t)(s->mlp->desc.num_layers + 1) * 32 * s->mlp->desc.hidden;
+}
+
+static LdsPlan grad_plan(const nrt_sdf* s) {
+  int hidden, ke;
+  sdf_dims(s, hidden, ke);
+  return plan_lds(hidden, ke, 1, false, true);
+}
+
+static size_t grad_workspace_bytes(const nrt_sdf* s) {
+  LdsPlan lp = grad_plan(s);
+  return (size_t)kGradBlocks * lp.waves * grad_scratch_floats_per_wave(s) * sizeof(float);
+}
+
+static int launch_grad(const nrt_sdf* s, const float* p, const int32_t* index, const int32_t* count,
+                       int64_t M, float* grad, float* n_out, float* p_io, float eps, void* ws,
+                       hipStream_t st) {
+  LdsPlan lp = grad_plan(s);
+  const int64_t waves_needed = ceil_div64(M, 32);
+  int blocks = (int)std::min<int64_t>(kGradBlocks, ceil_div64(waves_needed, lp.waves));
+  blocks = std::max(blocks, 1);
+  int rc = NRT_OK;
+  ProfScope prof("k_sdf_grad", st);
+  NRT_NB_SWITCH(s->host_dev.nb, {
+    if (!(rc = set_lds(k_sdf_grad<NB>, lp.bytes)))
+      k_sdf_grad<NB><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
+          s->dev, p, index, count, M, grad, n_out, p_io, eps, s->mlp ? (float*)ws : nullptr, lp.RS,
+          lp.per_wave, (int64_t)grad_scratch_floats_per_wave(s));
+  });
+  if (rc) return rc;
+  return check_launch("k_sdf_grad");
+}
+
+int nrt_sdf_grad(const nrt_sdf* s, const float* p, int64_t M, float* grad, void* stream) {
+  if (!s || M < 0) { set_error("nrt_sdf_grad: bad argument"); return NRT_EINVAL; }
+  if (M == 0) return NRT_OK;
+  if (!p || !grad) { set_error("nrt_sdf_grad: null p / grad"); return NRT_EINVAL; }
+  void* ws = nullptr;
+  size_t bytes = grad_workspace_bytes(s);
+  if (bytes) NRT_HIP(hipMallocAsync(&ws, bytes, (hipStream_t)stream));
+  int rc = launch_grad(s, p, nullptr, nullptr, M, grad, nullptr, nullptr, 0.f, ws, (hipStream_t)stream);
+  if (ws) (void)hipFreeAsync(ws, (hipStream_t)stream);
+  return rc;
+}
+
+size_t nrt_intersect_workspace_bytes(const nrt_sdf* s, int64_t P) {
+  (void)P;
+  return s ? grad_workspace_bytes(s) + 256 : 0;
+}
+
+int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_march_params* a,
+                      float* t, uint8_t* hit, float* p, float* n, float* raw_n, float* wi,
+                      float* throughput, int32_t* hit_idx, int32_t* hit_count, void* workspace,
+                      void* stream) {
+  if (!s || !a || P < 0) { set_error("nrt_sdf_intersect: bad argument"); return NRT_EINVAL; }
+  if (P == 0) return NRT_OK;
+  if (!rays || !t || !hit || !p || !n) { set_error("nrt_sdf_intersect: null output"); return NRT_EINVAL; }
+  if (a->primary && !throughput) { set_error("nrt_sdf_intersect: throughput required when primary"); return NRT_EINVAL; }
+  if ((hit_idx == nullptr) != (hit_count == nullptr)) { set_error("nrt_sdf_intersect: hit_idx and hit_count go together"); return NRT_EINVAL; }
+  if (s->mlp && !workspace) { set_error("nrt_sdf_intersect: workspace required"); return NRT_EINVAL; }
+  if (P == 0) return NRT_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const bool f16 = a->precision == NRT_FP16;
+  int hidden, ke;
+  sdf_dims(s, hidden, ke);
+  MarchArgs ma;
+  ma.max_steps = a->max_steps;
+  ma.eps = a->epsilon;
+  ma.max_t = a->max_t;
+  ma.primary = a->primary;
+  ma.step = a->scan_max_t / 128.0;
+  // the normal pass needs the list of hit rays; use the caller's or a workspace-backed one
+  int32_t* idx = hit_idx;
+  int32_t* cnt = hit_count;
+  char* ws = (char*)workspace;
+  std::unique_ptr<char, void (*)(char*)> own(nullptr, [](char* q) { if (q) (void)hipFree(q); });
+  if (!idx) {
+    char* tmp = nullptr;
+    NRT_HIP(hipMallocAsync((void**)&tmp, (size_t)P * 4 + 256, st));
+    own.reset(tmp);
+    cnt = (int32_t*)tmp;
+    idx = (int32_t*)(tmp + 256);
+  }
+  NRT_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), st));
+  LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
+  dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
+  int rc0 = NRT_OK;
+  {
+  ProfScope prof("k_intersect", st);
+  NRT_NB_SWITCH(s->host_dev.nb, {
+    if (f16) {
+      if (!(rc0 = set_lds(k_intersect<true, NB>, lp.bytes)))
+        k_intersect<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
+                                                             throughput, idx, cnt, lp.RS, lp.per_wave);
+    } else {
+      if (!(rc0 = set_lds(k_intersect<false, NB>, lp.bytes)))
+        k_intersect<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
+                                                              throughput, idx, cnt, lp.RS, lp.per_wave);
+    }
+  });
+  }
+  if (rc0) return rc0;
+  if (int rc = check_launch("k_intersect")) return rc;
+  // normals on hit rays (f32 backward): raw gradient, unit normal, p += 5 eps n
+  if (int rc = launch_grad(s, p, idx, cnt, P, raw_n, n, p, a->epsilon, ws, st)) return rc;
+  if (wi) {
+    k_frame_wi<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, st>>>(rays, n, P, nullptr, wi);
+    if (int rc = check_launch("k_frame_wi")) return rc;
+  }
+  if (own) {
+    // keep the temporary list alive until the stream has consumed it
+    (void)hipFreeAsync(own.release(), st);
+  }
+  return NRT_OK;
+}
+
+int nrt_sdf_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const float* max_t,
+                      int32_t max_steps, float eps, uint8_t* visible, int precision, void* stream) {
+  if (!s || P < 0) { set_error("nrt_sdf_occlusion: bad argument"); return NRT_EINVAL; }
+  if (P == 0) return NRT_OK;
+  if (!rays || !max_t || !visible) { set_error("nrt_sdf_occlusion: null argument"); return NRT_EINVAL; }
+  const bool f16 = precision == NRT_FP16;
+  int hidden, ke;
+  sdf_dims(s, hidden, ke);
+  LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
+  dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
+  hipStream_t st = (hipStream_t)stream;
+  int rc = NRT_OK;
+  NRT_NB_SWITCH(s->host_dev.nb, {
+    if (f16) {
+      if (!(rc = set_lds(k_occlusion<true, NB>, lp.bytes)))
+        k_occlusion<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
+    } else {
+      if (!(rc = set_lds(k_occlusion<false, NB>, lp.bytes)))
+        k_occlusion<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
+    }
+  });
+  if (rc) return rc;
+  return check_launch("k_occlusion");
+}
+
+int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi, void* stream) {
+  if (!n || (wi && !rays) || P < 0) { set_error("nrt_frames: bad argument"); return NRT_EINVAL; }
+  if (P == 0 || (!frame && !wi)) return NRT_OK;
+  k_frame_wi<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, (hipStream_t)stream>>>(rays, n, P, frame, wi);
+  return check_launch("k_frame_wi");
+}
+
+}  // extern "C"

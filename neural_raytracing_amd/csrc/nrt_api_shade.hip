@@ -1,0 +1,127 @@
+// nrt_api_shade.hip -- light / BSDF handles and the fused direct-shading launcher
+#include "nrt_launch.h"
+
+using namespace nrt;
+
+extern "C" {
+static float sigm(float x) { return 1.f / (1.f + std::exp(-x)); }
+
+int nrt_light_create_field(const nrt_mlp* mlp, const float* color3, nrt_light** out) {
+  if (!mlp || !color3 || !out) { set_error("nrt_light_create_field: null"); return NRT_EINVAL; }
+  if (mlp->desc.in_size != 3 || mlp->desc.out != 3) { set_error("nrt_light_create_field: MLP must map 3 -> 3"); return NRT_EINVAL; }
+  std::unique_ptr<nrt_light> l(new nrt_light());
+  std::memset(&l->host_dev, 0, sizeof(LightDev));
+  l->host_dev.kind = 0;
+  l->host_dev.mlp = mlp->dev;
+  for (int i = 0; i < 3; ++i) l->host_dev.color_sig[i] = sigm(color3[i]);
+  l->mlp = mlp;
+  NRT_HIP(hipMalloc(&l->dev, sizeof(LightDev)));
+  NRT_HIP(hipMemcpy(l->dev, &l->host_dev, sizeof(LightDev), hipMemcpyHostToDevice));
+  *out = l.release();
+  return NRT_OK;
+}
+
+int nrt_light_create_point(const float* loc, const float* inten, float c, float lin, float q,
+                           float scale, nrt_light** out) {
+  if (!loc || !inten || !out) { set_error("nrt_light_create_point: null"); return NRT_EINVAL; }
+  std::unique_ptr<nrt_light> l(new nrt_light());
+  std::memset(&l->host_dev, 0, sizeof(LightDev));
+  l->host_dev.kind = 1;
+  float nrm = std::sqrt(inten[0] * inten[0] + inten[1] * inten[1] + inten[2] * inten[2]);
+  nrm = std::max(nrm, 1e-12f);
+  for (int i = 0; i < 3; ++i) {
+    l->host_dev.loc[i] = loc[i];
+    l->host_dev.scaled_dir[i] = scale * (inten[i] / nrm);
+  }
+  l->host_dev.c = std::max(c, 1e-6f);
+  l->host_dev.l = std::max(lin, 1e-6f);
+  l->host_dev.q = std::max(q, 1e-6f);
+  NRT_HIP(hipMalloc(&l->dev, sizeof(LightDev)));
+  NRT_HIP(hipMemcpy(l->dev, &l->host_dev, sizeof(LightDev), hipMemcpyHostToDevice));
+  *out = l.release();
+  return NRT_OK;
+}
+
+int nrt_light_destroy(nrt_light* l) {
+  if (!l) return NRT_OK;
+  if (l->dev) (void)hipFree(l->dev);
+  delete l;
+  return NRT_OK;
+}
+int nrt_bsdf_create(int32_t n, const nrt_bsdf_component* comps, const nrt_mlp* spatial, nrt_bsdf** out) {
+  if (n < 1 || n > kMaxComponents || !comps || !out) { set_error("nrt_bsdf_create: 1..32 components required"); return NRT_EINVAL; }
+  if (spatial && (spatial->desc.in_size != 3 || spatial->desc.out < n)) {
+    set_error("nrt_bsdf_create: spatial MLP must map 3 -> n_components");
+    return NRT_EINVAL;
+  }
+  std::unique_ptr<nrt_bsdf> b(new nrt_bsdf());
+  std::memset(&b->host_dev, 0, sizeof(BsdfDev));
+  b->host_dev.n = n;
+  b->host_dev.spatial = spatial ? spatial->dev : nullptr;
+  b->spatial = spatial;
+  for (int j = 0; j < n; ++j) {
+    const nrt_bsdf_component& c = comps[j];
+    BsdfCompDev& d = b->host_dev.comp[j];
+    d.kind = c.kind;
+    d.act = c.activation;
+    std::memcpy(d.params, c.params, sizeof(d.params));
+    if (c.kind == NRT_BSDF_NEURAL) {
+      if (!c.mlp || c.mlp->desc.in_size != 3 || c.mlp->desc.out != 3) {
+        set_error("nrt_bsdf_create: NeuralBSDF MLP must map 3 -> 3");
+        return NRT_EINVAL;
+      }
+      d.mlp = c.mlp->dev;
+      b->mlps.push_back(c.mlp);
+    } else if (c.kind != NRT_BSDF_DIFFUSE && c.kind != NRT_BSDF_CONDUCTOR) {
+      set_error("nrt_bsdf_create: unknown component kind");
+      return NRT_EINVAL;
+    }
+  }
+  NRT_HIP(hipMalloc(&b->dev, sizeof(BsdfDev)));
+  NRT_HIP(hipMemcpy(b->dev, &b->host_dev, sizeof(BsdfDev), hipMemcpyHostToDevice));
+  *out = b.release();
+  return NRT_OK;
+}
+
+int nrt_bsdf_destroy(nrt_bsdf* b) {
+  if (!b) return NRT_OK;
+  if (b->dev) (void)hipFree(b->dev);
+  delete b;
+  return NRT_OK;
+}
+
+int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
+                     const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+                     float* rgb, float* weights_out, int precision, void* stream) {
+  if (!b || !l || !p || !n || !wi || !hit_idx || !hit_count || !rgb || P < 0) {
+    set_error("nrt_shade_direct: bad argument");
+    return NRT_EINVAL;
+  }
+  if (P == 0) return NRT_OK;
+  const bool f16 = precision == NRT_FP16;
+  int hidden = 32, ke = 16;
+  auto upd = [&](const nrt_mlp* m) {
+    if (!m) return;
+    hidden = std::max(hidden, m->desc.hidden);
+    ke = std::max(ke, m->host_dev.ke);
+  };
+  upd(l->mlp);
+  upd(b->spatial);
+  for (auto* m : b->mlps) upd(m);
+  LdsPlan lp = plan_lds(hidden, ke, 64, f16, false);
+  int blocks = std::max(1, std::min(ceil_div64(ceil_div64(P, 32), lp.waves), 2048));
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof("k_shade_direct", st);
+  if (f16) {
+    if (int rc = set_lds(k_shade_direct<true>, lp.bytes)) return rc;
+    k_shade_direct<true><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, rgb, weights_out, lp.RS, lp.per_wave);
+  } else {
+    if (int rc = set_lds(k_shade_direct<false>, lp.bytes)) return rc;
+    k_shade_direct<false><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, rgb, weights_out, lp.RS, lp.per_wave);
+  }
+  return check_launch("k_shade_direct");
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// nrt_common.hip -- error state and library identity
+#include "nrt_launch.h"
+
+#include <vector>
+
+namespace nrt {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string& msg) { g_err = msg; }
+
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return NRT_EHIP;
+}
+
+int max_hidden(const nrt_mlp* m) { return m ? m->desc.hidden : 0; }
+
+struct ProfRec {
+  std::string name;
+  hipEvent_t a, b;
+};
+static bool g_prof = false;
+static std::vector<ProfRec> g_recs;
+
+ProfScope::ProfScope(const char* n, hipStream_t s) : name(n), stream(s) {
+  if (!g_prof) return;
+  if (hipEventCreate(&start) != hipSuccess) { start = nullptr; return; }
+  (void)hipEventRecord(start, stream);
+}
+
+ProfScope::~ProfScope() {
+  if (!start) return;
+  hipEvent_t stop;
+  if (hipEventCreate(&stop) != hipSuccess) return;
+  (void)hipEventRecord(stop, stream);
+  g_recs.push_back({name, start, stop});
+}
+
+}  // namespace nrt
+
+using namespace nrt;
+
+extern "C" {
+
+void nrt_profile_enable(int on) { nrt::g_prof = on != 0; }
+
+void nrt_profile_reset(void) {
+  for (auto& r : nrt::g_recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  nrt::g_recs.clear();
+}
+
+int nrt_profile_read(const char* name, double* total_ms, int64_t* launches) {
+  double tot = 0.0;
+  int64_t n = 0;
+  for (auto& r : nrt::g_recs) {
+    if (name && r.name != name) continue;
+    if (hipEventSynchronize(r.b) != hipSuccess) { set_error("nrt_profile_read: event sync failed"); return NRT_EHIP; }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) { set_error("nrt_profile_read: elapsed failed"); return NRT_EHIP; }
+    tot += ms;
+    ++n;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = n;
+  return NRT_OK;
+}
+
+const char* nrt_last_error(void) { return nrt::g_err.c_str(); }
+int nrt_version(void) { return 1; }
+
+int nrt_device_ok(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n < 1) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return 0;
+  return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,471 @@
+// nrt_device.h -- device-side building blocks of the gfx950 ray-march path.
+//
+// Work unit: one wavefront owns 32 rays.  Lane l serves ray r = l & 31 and lane-half h = l >> 5;
+// both halves carry the same ray state, and the MFMA fragment layout splits the K dimension
+// between them.  Every MLP layer is one GEMM  Z^T[N_out, 32 rays] = W[N_out, K] . U^T[K, 32 rays]
+// computed with 32x32 MFMA tiles: W is the A operand (pre-packed per lane on the host, read from
+// L2), the layer input U^T is the B operand.
+//
+//  * FP16 path ("register path"): v_mfma_f32_32x32x16_f16.  A layer's f32 accumulator tile has
+//    the ray on the lane and the output feature in the 16 registers, which is exactly the B
+//    fragment layout of the next layer; activations never leave registers (the k order inside
+//    a fragment is permuted, and the host packer permutes W's columns to match).
+//  * FP32 path ("LDS path"): v_mfma_f32_32x32x2_f32 (exact f32 fma chain).  Two 16-register
+//    tiles per input do not fit, so each wave keeps its 32 rays' activations in an LDS slab
+//    X[32][RS] and the B operand is one ds_read_b32 per k-step.
+//
+// Reference semantics restated here: SkipConnMLP.forward (neural_blocks.py:75-86) with the
+// fourier2 encoding (utils.py:37-40).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nrt {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxLin = 20;  // init + up to 18 hidden + out
+
+enum { ACT_LEAKY = 0, ACT_SOFTPLUS = 1, ACT_NONE = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
+
+// Device descriptor of a packed SkipConnMLP (built by nrt_mlp_create, lives in device memory).
+//
+// Encoding slot order (both paths): slot 2q / 2q+1 = sin / cos of projection q (q < F), then the
+// raw inputs x_0..x_{in-1}, then the latent, then zero padding up to `ke` (multiple of 16).
+// The packer maps slots back to the reference's column order [x, sin(xB), cos(xB), latent].
+struct MlpDev {
+  int in_size, hidden, n_hidden, out, freqs, skip, latent, act;
+  int dp;   // in + 2F + latent (reference encoding width)
+  int ke;   // encoding slots, padded to 16
+  int nb;   // hidden / 32
+  int ob;   // ceil(out / 32)
+  const float* basis;              // [in][F]
+  const h8* w16[kMaxLin];          // FP16 A fragments  [kstep][rowblock][64 lanes]
+  const float* w32[kMaxLin];       // FP32 A fragments  [kstep][rowblock][64 lanes]
+  const float* wt32[kMaxLin];      // FP32 A fragments of W^T (backward)
+  const float* bias[kMaxLin];      // [rowblocks*32]
+  const float* wout_row0;          // out.weight[0, :]  (gradient seed of an SDF head)
+  int nbt[kMaxLin];                // row blocks of W^T (input positions / 32, rounded up)
+};
+
+struct SdfDev {
+  int kind;         // 0 unit sphere, 1 MLP, 2 sphere blob (+ optional shift MLP)
+  int n_spheres;
+  float k;          // smooth-min sharpness (32)
+  const float* spheres;  // [n][16]: (I+tfs) row-major (9), centre (3), radius (1), pad (3)
+  const MlpDev* mlp;     // MLP or shift MLP (nullptr if none)
+  int nb;
+};
+
+// ------------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+// compiler-only fence: keeps LDS writes and the following cross-lane reads of one wave in
+// program order (a wave's DS instructions execute in order in hardware)
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// torch semantics: F.leaky_relu (slope 0.01), F.softplus (beta 1, threshold 20), sigmoid, relu
+template <bool FAST>
+__device__ __forceinline__ float act_fwd(float x, int act) {
+  switch (act) {
+    case ACT_LEAKY: return x > 0.f ? x : x * 0.01f;
+    case ACT_SOFTPLUS:
+      if (FAST) return x > 20.f ? x : __logf(1.f + __expf(x));
+      return x > 20.f ? x : log1pf(expf(x));
+    case ACT_SIGMOID:
+      return FAST ? 1.f / (1.f + __expf(-x)) : 1.f / (1.f + expf(-x));
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    default: return x;
+  }
+}
+
+// derivative of act at pre-activation x (torch backward formulas)
+__device__ __forceinline__ float act_bwd(float x, int act) {
+  switch (act) {
+    case ACT_LEAKY: return x > 0.f ? 1.f : 0.01f;
+    case ACT_SOFTPLUS: {
+      if (x > 20.f) return 1.f;
+      float z = expf(x);
+      return z / (z + 1.f);
+    }
+    case ACT_SIGMOID: {
+      float s = 1.f / (1.f + expf(-x));
+      return s * (1.f - s);
+    }
+    case ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + expf(-x)); }
+
+// F.normalize(v, eps): v / max(|v|, eps)
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z, float eps) {
+  float n = sqrtf(x * x + y * y + z * z);
+  n = fmaxf(n, eps);
+  x = x / n; y = y / n; z = z / n;
+}
+
+// ------------------------------------------------------------------------------------------
+// Encoding
+// ------------------------------------------------------------------------------------------
+// Input of one MLP evaluation for this lane's ray: up to 4 inputs in registers, or a pointer to
+// a row in global memory (inputs wider than 4, e.g. NeRFLE's second MLP).
+struct EncIn {
+  float x[4];
+  const float* xg;   // row pointer when in_size > 4, else nullptr
+  const float* lat;  // latent row or nullptr
+};
+
+template <bool FAST>
+__device__ __forceinline__ float proj(const MlpDev& m, const EncIn& e, int q) {
+  const float* B = m.basis;
+  const int F = m.freqs;
+  float s = 0.f;
+  if (e.xg == nullptr) {
+    // x @ B for in_size <= 4 (utils.py:39); same k order as a BLAS dot of length in
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (i < m.in_size) s = (i == 0) ? e.x[0] * B[q] : fmaf(e.x[i], B[i * F + q], s);
+  } else {
+    for (int i = 0; i < m.in_size; ++i) s = (i == 0) ? e.xg[0] * B[q] : fmaf(e.xg[i], B[i * F + q], s);
+  }
+  return s;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void sincos_(float a, float& s, float& c) {
+  if (FAST) { s = __sinf(a); c = __cosf(a); }
+  else sincosf(a, &s, &c);
+}
+
+// value of the raw (non-sin/cos) encoding slot: inputs, latent, zero padding
+__device__ __forceinline__ float enc_plain(const MlpDev& m, const EncIn& e, int slot) {
+  int i = slot - 2 * m.freqs;
+  if (i < m.in_size) {
+    if (e.xg) return e.xg[i];
+    float v = e.x[0];
+    v = (i == 1) ? e.x[1] : v;
+    v = (i == 2) ? e.x[2] : v;
+    v = (i == 3) ? e.x[3] : v;
+    return v;
+  }
+  i -= m.in_size;
+  if (i < m.latent && e.lat) return e.lat[i];
+  return 0.f;
+}
+
+// two adjacent slots (2q, 2q+1) starting at an even slot
+template <bool FAST>
+__device__ __forceinline__ void enc_pair(const MlpDev& m, const EncIn& e, int slot, float& a,
+                                         float& b) {
+  if (slot < 2 * m.freqs) {
+    sincos_<FAST>(proj<FAST>(m, e, slot >> 1), a, b);
+  } else {
+    a = enc_plain(m, e, slot);
+    b = enc_plain(m, e, slot + 1);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// FP16 register path
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f16v mfma16(h8 a, h8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// acc[reg] = bias[32*blk + (reg&3) + 8*(reg>>2) + 4*h]
+__device__ __forceinline__ f16v bias_tile(const float* __restrict__ bias, int blk, int h) {
+  f16v v;
+  const float* b = bias + 32 * blk + 4 * h;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float4 q = *reinterpret_cast<const float4*>(b + 8 * g);
+    v[4 * g + 0] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+  }
+  return v;
+}
+
+// B fragment of encoding k-step s (slots 16s + 8h + j), optionally through the activation
+template <bool FAST>
+__device__ __forceinline__ h8 enc_frag16(const MlpDev& m, const EncIn& e, int s, int h, int act) {
+  h8 f;
+  const int base = 16 * s + 8 * h;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    float a, b;
+    enc_pair<FAST>(m, e, base + 2 * jj, a, b);
+    if (act >= 0) { a = act_fwd<FAST>(a, act); b = act_fwd<FAST>(b, act); }
+    f[2 * jj] = (_Float16)a;
+    f[2 * jj + 1] = (_Float16)b;
+  }
+  return f;
+}
+
+template <int NB>
+__device__ __forceinline__ void act_to_frags(const f16v (&acc)[NB], h8 (&hb)[2 * NB], int act) {
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      h8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (_Float16)act_fwd<true>(acc[ib][8 * s2 + j], act);
+      hb[2 * ib + s2] = f;
+    }
+}
+
+// Full SkipConnMLP forward for the wave's 32 rays.  Output rows < m.out are written to
+// y[r * ystride + row] (LDS or global, f32).
+template <int NB>
+__device__ __forceinline__ void mlp16_forward(const MlpDev& m, const EncIn& e, float* __restrict__ y, int ystride) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const int neb = m.ke >> 4;
+  f16v acc[NB];
+  h8 hb[2 * NB];
+
+  // init layer: raw encoding in, no activation (neural_blocks.py:80)
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) acc[ib] = bias_tile(m.bias[0], ib, h);
+  {
+    const h8* __restrict__ A = m.w16[0] + lane;
+    for (int s = 0; s < neb; ++s) {
+      h8 b = enc_frag16<true>(m, e, s, h, -1);
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(s * NB + ib) * 64], b, acc[ib]);
+    }
+  }
+  // hidden layers: x = layer(act(cat[x, enc] if skip else x))   (neural_blocks.py:81-84)
+  for (int i = 0; i < m.n_hidden; ++i) {
+    act_to_frags<NB>(acc, hb, m.act);
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) acc[ib] = bias_tile(m.bias[1 + i], ib, h);
+    const h8* __restrict__ A = m.w16[1 + i] + lane;
+#pragma unroll
+    for (int s = 0; s < 2 * NB; ++s)
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(s * NB + ib) * 64], hb[s], acc[ib]);
+    if (i != m.n_hidden - 1 && (i % m.skip) == 0) {
+      A += 2 * NB * NB * 64;
+      for (int s = 0; s < neb; ++s) {
+        h8 b = enc_frag16<true>(m, e, s, h, m.act);
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(s * NB + ib) * 64], b, acc[ib]);
+      }
+    }
+  }
+  act_to_frags<NB>(acc, hb, m.act);
+  // out layer (neural_blocks.py:86)
+  const float* __restrict__ bo = m.bias[m.n_hidden + 1];
+  const h8* __restrict__ A = m.w16[m.n_hidden + 1] + lane;
+  for (int ob = 0; ob < m.ob; ++ob) {
+    f16v o = bias_tile(bo, ob, h);
+#pragma unroll
+    for (int s = 0; s < 2 * NB; ++s) o = mfma16(A[(s * m.ob + ob) * 64], hb[s], o);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int row = 32 * ob + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < m.out) y[r * ystride + row] = o[reg];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// FP32 LDS path
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// LDS row stride (floats) of the per-wave activation slab: hidden | enc | [enc grad]
+__host__ __device__ inline int slab_stride(int hidden, int ke, bool with_grad) {
+  int rs = hidden + ke + (with_grad ? ke : 0);
+  return rs | 1;  // odd stride: 32 lanes of a ds_read_b32 hit 32 different banks
+}
+
+template <bool FAST>
+__device__ __forceinline__ void write_enc_slab(const MlpDev& m, const EncIn& e, float* X, int RS) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  float* row = X + r * RS + m.hidden;
+  // the two lane halves share the pairs: half h takes pairs 2h, 2h+4, ...  (slots multiple of 4)
+  for (int slot = 2 * h; slot < m.ke; slot += 4) {
+    float a, b;
+    enc_pair<FAST>(m, e, slot, a, b);
+    row[slot] = a;
+    row[slot + 1] = b;
+  }
+}
+
+// One FP32 GEMM over `nks` k-steps of the slab starting at column kcol; accumulates into acc.
+// act_in >= 0 applies the activation to B on the fly (skip-concat of the encoding).
+template <int NB>
+__device__ __forceinline__ void gemm32(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
+                                       int rb0, int nks, const float* X, int RS, int kcol,
+                                       int act_in) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const float* xr = X + r * RS + kcol + h;
+  for (int s = 0; s < nks; ++s) {
+    float b = xr[2 * s];
+    if (act_in >= 0) b = act_fwd<false>(b, act_in);
+    const float* As = A + (s * nrb + rb0) * 64 + lane;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+      if (rb0 + ib < nrb) acc[ib] = mfma32(As[ib * 64], b, acc[ib]);
+  }
+}
+
+template <int NB>
+__device__ __forceinline__ void bias32(f16v (&acc)[NB], const float* bias, int rb0, int nrb, int h) {
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib)
+    if (rb0 + ib < nrb) acc[ib] = bias_tile(bias, rb0 + ib, h);
+}
+
+// Forward through the FP32 slab.  If zs != nullptr the pre-activations of the init layer and
+// of every hidden layer are stored to zs[(layer*32 + r)*hidden + row] for the backward pass.
+template <int NB>
+__device__ __forceinline__ void mlp32_forward(const MlpDev& m, const EncIn& e, float* X, int RS,
+                              float* __restrict__ y, int ystride, float* __restrict__ zs) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const int H = m.hidden;
+  write_enc_slab<false>(m, e, X, RS);
+  wave_lds_fence();
+  f16v acc[NB];
+  for (int l = 0; l <= m.n_hidden; ++l) {
+    bias32<NB>(acc, m.bias[l], 0, NB, h);
+    if (l == 0) {
+      gemm32<NB>(acc, m.w32[0], NB, 0, m.ke >> 1, X, RS, H, -1);
+    } else {
+      const int i = l - 1;
+      gemm32<NB>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
+      if (i != m.n_hidden - 1 && (i % m.skip) == 0)
+        gemm32<NB>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, m.ke >> 1, X, RS, H, m.act);
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        int row = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        float z = acc[ib][reg];
+        if (zs) zs[(l * 32 + r) * H + row] = z;
+        X[r * RS + row] = act_fwd<false>(z, m.act);
+      }
+    wave_lds_fence();
+  }
+  // out layer
+  const float* Ao = m.w32[m.n_hidden + 1];
+  for (int ob = 0; ob < m.ob; ++ob) {
+    f16v o[1];
+    o[0] = bias_tile(m.bias[m.n_hidden + 1], ob, h);
+    // k-steps over hidden; A is [s][ob][64]
+    const float* xr = X + r * RS + h;
+    for (int s = 0; s < (H >> 1); ++s) o[0] = mfma32(Ao[(s * m.ob + ob) * 64 + lane], xr[2 * s], o[0]);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      int row = 32 * ob + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (row < m.out) y[r * ystride + row] = o[0][reg];
+    }
+  }
+  wave_lds_fence();
+}
+
+// d out[0] / d x for the wave's rays, after mlp32_forward(..., zs) on the same slab.
+// Returns the gradient with respect to the first min(in_size, 3) inputs in g[0..2].
+template <int NB>
+__device__ __forceinline__ void mlp32_backward_out0(const MlpDev& m, const EncIn& e, float* X, int RS,
+                                    const float* __restrict__ zs, float g[3]) {
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const int H = m.hidden;
+  const int ke = m.ke;
+  float* row = X + r * RS;
+  float* egrad = row + H + ke;
+  for (int s = h; s < ke; s += 2) egrad[s] = 0.f;
+  // seed: dy/dh_last = W_out[0,:] * act'(z_last)
+  const float* zl = zs + (m.n_hidden * 32 + r) * H;
+  for (int k = h; k < H; k += 2) row[k] = m.wout_row0[k] * act_bwd(zl[k], m.act);
+  wave_lds_fence();
+  f16v acc[NB];
+  for (int l = m.n_hidden; l >= 0; --l) {
+    const float* At = m.wt32[l];
+    const int nrb = m.nbt[l];
+    const bool has_hidden_in = (l != 0);
+    const bool has_enc_in = (l == 0) || ((l - 1) != m.n_hidden - 1 && ((l - 1) % m.skip) == 0);
+    const int hid_rb = has_hidden_in ? NB : 0;
+    // encoding positions first (they only accumulate), hidden block group last (in place)
+    if (has_enc_in) {
+      const int enc_pos0 = has_hidden_in ? H : 0;
+      for (int rb0 = hid_rb; rb0 < nrb; rb0 += NB) {
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+        gemm32<NB>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+          if (rb0 + ib >= nrb) continue;
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            int slot = pos - enc_pos0;
+            if (slot >= 0 && slot < ke) {
+              float v = acc[ib][reg];
+              // skip inputs are act(enc) (neural_blocks.py:84); the init input is raw enc
+              if (l != 0) v *= act_bwd(row[H + slot], m.act);
+              egrad[slot] += v;
+            }
+          }
+        }
+      }
+      wave_lds_fence();
+    }
+    if (has_hidden_in) {
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+      gemm32<NB>(acc, At, nrb, 0, H >> 1, X, RS, 0, -1);
+      wave_lds_fence();
+      const float* zp = zs + ((l - 1) * 32 + r) * H;
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          int pos = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          row[pos] = acc[ib][reg] * act_bwd(zp[pos], m.act);
+        }
+      wave_lds_fence();
+    }
+  }
+  // encoding -> input:  d sin(xB_q) = cos(xB_q) B_q,  d cos(xB_q) = -sin(xB_q) B_q,  d x_i = e_i
+  float gx[3] = {0.f, 0.f, 0.f};
+  const int F = m.freqs;
+  for (int q = h; q < F; q += 2) {
+    float s, c;
+    sincosf(proj<false>(m, e, q), &s, &c);
+    float w = egrad[2 * q] * c - egrad[2 * q + 1] * s;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (i < m.in_size) gx[i] = fmaf(w, m.basis[i * F + q], gx[i]);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (i < m.in_size) gx[i] += egrad[2 * F + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) g[i] = gx[i] + __shfl_xor(gx[i], 32);
+  wave_lds_fence();
+}
+
+}  // namespace nrt

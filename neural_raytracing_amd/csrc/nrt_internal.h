@@ -1,0 +1,85 @@
+// nrt_internal.h -- host-side objects behind the opaque C handles of include/nrt.h
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/nrt.h"
+#include "nrt_device.h"
+
+struct nrt_mlp {
+  nrt_mlp_desc desc;
+  nrt::MlpDev host_dev;          // host copy of the device descriptor
+  nrt::MlpDev* dev = nullptr;    // device copy
+  void* blob = nullptr;          // all packed arrays
+  size_t blob_bytes = 0;
+};
+
+struct nrt_sdf {
+  nrt::SdfDev host_dev;
+  nrt::SdfDev* dev = nullptr;
+  float* spheres = nullptr;
+  const nrt_mlp* mlp = nullptr;
+};
+
+namespace nrt {
+
+struct LightDev {
+  int kind;                 // 0 field, 1 point
+  const MlpDev* mlp;
+  float color_sig[3];       // sigmoid(color)
+  float loc[3];
+  float scaled_dir[3];      // scale * normalize(intensity)
+  float c, l, q;            // clamped falloff coefficients
+};
+
+constexpr int kMaxComponents = 32;
+
+struct BsdfCompDev {
+  int kind;
+  const MlpDev* mlp;
+  int act;
+  float params[4];
+};
+
+struct BsdfDev {
+  int n;
+  const MlpDev* spatial;
+  BsdfCompDev comp[kMaxComponents];
+};
+
+}  // namespace nrt
+
+struct nrt_light {
+  nrt::LightDev host_dev;
+  nrt::LightDev* dev = nullptr;
+  const nrt_mlp* mlp = nullptr;
+};
+
+struct nrt_bsdf {
+  nrt::BsdfDev host_dev;
+  nrt::BsdfDev* dev = nullptr;
+  std::vector<const nrt_mlp*> mlps;
+  const nrt_mlp* spatial = nullptr;
+};
+
+namespace nrt {
+// launch timing registry (nrt_profile_*); begin/end are no-ops unless enabled
+struct ProfScope {
+  const char* name;
+  hipStream_t stream;
+  hipEvent_t start = nullptr;
+  ProfScope(const char* n, hipStream_t s);
+  ~ProfScope();
+};
+void set_error(const std::string& msg);
+int hip_fail(hipError_t e, const char* what);
+int max_hidden(const nrt_mlp* m);
+}  // namespace nrt
+
+#define NRT_HIP(call)                                         \
+  do {                                                        \
+    hipError_t _e = (call);                                   \
+    if (_e != hipSuccess) return nrt::hip_fail(_e, #call);    \
+  } while (0)

@@ -1,0 +1,661 @@
+// nrt_kernels.h -- gfx950 kernels of the ray-march render path and their launchers.
+//
+//   k_mlp_forward   SkipConnMLP on a flat batch                 neural_blocks.py:75-86
+//   k_sdf_eval      SDF callable on a flat batch                sdfs.py:13, 40-44
+//   k_sdf_grad      autograd normal (f32 backward)              sdfs.py:184-197
+//   k_intersect     sphere trace + 128-step coarse scan         sdfs.py:111-137, 232-249
+//   k_normals       normals + 5*eps offset of the hit rays      sdfs.py:152-158
+//   k_frame_wi      shading frame and wi = to_local(-d)         interaction.py:9-41, sdfs.py:158-159
+//   k_occlusion     shadow-ray march                            sdfs.py:162-181
+//   k_shade_direct  light sample + spatially varying BSDF       integrators.py:173-189, bsdfs.py:515-536
+//   k_raygen        NeRF / DTU / FoV primary rays               cameras.py:23-54, 132-192
+//   k_composite     NeRFIntegrator alpha + background + tile    integrators.py:249-257, main.py:85-90
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "nrt_internal.h"
+
+namespace nrt {
+
+constexpr int kLdsBytes = 160 * 1024;
+
+// ------------------------------------------------------------------------------------------
+// generic MLP evaluation with runtime hidden-size dispatch
+// ------------------------------------------------------------------------------------------
+template <bool F16, int NB>
+__device__ __forceinline__ void mlp_eval(const MlpDev& m, const EncIn& e, float* X, int RS,
+                                         float* Y, int ys, float* zs) {
+  if (F16) mlp16_forward<NB>(m, e, Y, ys);
+  else mlp32_forward<NB>(m, e, X, RS, Y, ys, zs);
+  wave_lds_fence();
+}
+
+// runtime hidden-size dispatch (one inlined copy per supported width)
+template <bool F16>
+__device__ __forceinline__ void mlp_eval_any(const MlpDev& m, const EncIn& e, float* X, int RS,
+                                          float* Y, int ys) {
+  switch (m.nb) {
+    case 1: mlp_eval<F16, 1>(m, e, X, RS, Y, ys, nullptr); break;
+    case 2: mlp_eval<F16, 2>(m, e, X, RS, Y, ys, nullptr); break;
+    case 3: mlp_eval<F16, 3>(m, e, X, RS, Y, ys, nullptr); break;
+    case 4: mlp_eval<F16, 4>(m, e, X, RS, Y, ys, nullptr); break;
+    default: mlp_eval<F16, 8>(m, e, X, RS, Y, ys, nullptr); break;
+  }
+}
+
+// per-wave LDS carve: FP32 slab X[32][RS] followed by Y[32][ys]
+struct WaveLds {
+  float* X;
+  float* Y;
+};
+
+__device__ __forceinline__ WaveLds wave_lds(float* smem, int per_wave_floats, int RS, bool f16) {
+  const int w = threadIdx.x >> 6;
+  float* base = smem + (size_t)w * per_wave_floats;
+  WaveLds l;
+  l.X = base;
+  l.Y = f16 ? base : base + 32 * RS;
+  return l;
+}
+
+__host__ __device__ inline int wave_lds_floats(int RS, int ys, bool f16) {
+  return (f16 ? 0 : 32 * RS) + 32 * ys;
+}
+
+// ------------------------------------------------------------------------------------------
+// SDF
+// ------------------------------------------------------------------------------------------
+template <bool FAST>
+__device__ __forceinline__ float spheres_value(const SdfDev& s, float x, float y, float z) {
+  // smooth_min(|(I+T_i) p - c_i| - r_i, k)   (sdfs.py:37-43, utils.py:386-387)
+  float acc = 0.f;
+  const float* sp = s.spheres;
+  for (int i = 0; i < s.n_spheres; ++i, sp += 16) {
+    float qx = fmaf(sp[2], z, fmaf(sp[1], y, sp[0] * x)) - sp[9];
+    float qy = fmaf(sp[5], z, fmaf(sp[4], y, sp[3] * x)) - sp[10];
+    float qz = fmaf(sp[8], z, fmaf(sp[7], y, sp[6] * x)) - sp[11];
+    float d = sqrtf(qx * qx + qy * qy + qz * qz) - sp[12];
+    acc += FAST ? __expf(-s.k * d) : expf(-s.k * d);
+  }
+  return -logf(fmaxf(acc, 1e-4f)) / s.k;
+}
+
+__device__ __forceinline__ void spheres_grad(const SdfDev& s, float x, float y, float z, float g[3]) {
+  float acc = 0.f, gx = 0.f, gy = 0.f, gz = 0.f;
+  const float* sp = s.spheres;
+  for (int i = 0; i < s.n_spheres; ++i, sp += 16) {
+    float qx = fmaf(sp[2], z, fmaf(sp[1], y, sp[0] * x)) - sp[9];
+    float qy = fmaf(sp[5], z, fmaf(sp[4], y, sp[3] * x)) - sp[10];
+    float qz = fmaf(sp[8], z, fmaf(sp[7], y, sp[6] * x)) - sp[11];
+    float nq = sqrtf(qx * qx + qy * qy + qz * qz);
+    float w = expf(-s.k * (nq - sp[12]));
+    acc += w;
+    float inv = nq > 0.f ? w / nq : 0.f;
+    float ux = qx * inv, uy = qy * inv, uz = qz * inv;  // w * q/|q|
+    gx += sp[0] * ux + sp[3] * uy + sp[6] * uz;       // (I+T)^T (w q/|q|)
+    gy += sp[1] * ux + sp[4] * uy + sp[7] * uz;
+    gz += sp[2] * ux + sp[5] * uy + sp[8] * uz;
+  }
+  // d/dp -log(max(S,1e-4))/k = (1/S) sum w_i dd_i/dp   (zero where the clamp is active)
+  float sc = acc >= 1e-4f ? 1.f / acc : 0.f;
+  g[0] = gx * sc; g[1] = gy * sc; g[2] = gz * sc;
+}
+
+// SDF value of this lane's point; every lane of the wave must call it (MFMA is wave-wide).
+template <bool F16, int NB>
+__device__ __forceinline__ float sdf_value(const SdfDev& s, float x, float y, float z,
+                                           const WaveLds& l, int RS, float* zs) {
+  if (s.kind == 0) return sqrtf(x * x + y * y + z * z) - 1.f;
+  float v = 0.f;
+  if (s.kind == 2) v = spheres_value<F16>(s, x, y, z);
+  if (s.mlp) {
+    EncIn e;
+    e.x[0] = x; e.x[1] = y; e.x[2] = z; e.x[3] = 0.f;
+    e.xg = nullptr; e.lat = nullptr;
+    mlp_eval<F16, NB>(*s.mlp, e, l.X, RS, l.Y, 1, zs);
+    float m = l.Y[lane_id() & 31];
+    wave_lds_fence();
+    v = (s.kind == 2) ? v + m : m;
+  }
+  return v;
+}
+
+// d sdf / dp (FP32 slab path), every lane of the wave must call it
+template <int NB>
+__device__ __forceinline__ void sdf_gradient(const SdfDev& s, float x, float y, float z,
+                                             const WaveLds& l, int RS, float* zs, float g[3]) {
+  g[0] = g[1] = g[2] = 0.f;
+  if (s.kind == 0) {
+    float n = sqrtf(x * x + y * y + z * z);
+    if (n > 0.f) { g[0] = x / n; g[1] = y / n; g[2] = z / n; }
+    return;
+  }
+  if (s.kind == 2) spheres_grad(s, x, y, z, g);
+  if (s.mlp) {
+    EncIn e;
+    e.x[0] = x; e.x[1] = y; e.x[2] = z; e.x[3] = 0.f;
+    e.xg = nullptr; e.lat = nullptr;
+    float gm[3];
+    mlp32_forward<NB>(*s.mlp, e, l.X, RS, l.Y, 1, zs);
+    mlp32_backward_out0<NB>(*s.mlp, e, l.X, RS, zs, gm);
+    g[0] += gm[0]; g[1] += gm[1]; g[2] += gm[2];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// flat-batch kernels (one wave = 32 rows)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t wave_global() {
+  return (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+}
+
+template <bool F16, int NB>
+__global__ void __launch_bounds__(256, F16 ? 2 : 1) k_mlp_forward(const MlpDev* __restrict__ mp,
+                                                      const float* __restrict__ x,
+                                                      const float* __restrict__ lat, int64_t M,
+                                                      float* __restrict__ y, int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const MlpDev& m = *mp;
+  WaveLds l = wave_lds(smem, per_wave, RS, F16);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t row0 = wave_global() * 32;
+  if (row0 >= M) return;  // whole wave exits together
+  const int64_t row = row0 + r;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  EncIn e;
+  const int in = m.in_size;
+  if (in <= 4) {
+    for (int i = 0; i < 4; ++i) e.x[i] = (i < in) ? x[rr * in + i] : 0.f;
+    e.xg = nullptr;
+  } else {
+    e.x[0] = e.x[1] = e.x[2] = e.x[3] = 0.f;
+    e.xg = x + rr * in;
+  }
+  e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
+  mlp_eval<F16, NB>(m, e, l.X, RS, l.Y, m.out, nullptr);
+  if (valid)
+    for (int o = (lane >> 5); o < m.out; o += 2) y[row * m.out + o] = l.Y[r * m.out + o];
+}
+
+template <bool F16, int NB>
+__global__ void __launch_bounds__(256, F16 ? 2 : 1) k_sdf_eval(const SdfDev* __restrict__ sp,
+                                                   const float* __restrict__ p, int64_t M,
+                                                   float* __restrict__ out, int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const SdfDev& s = *sp;
+  WaveLds l = wave_lds(smem, per_wave, RS, F16);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t row0 = wave_global() * 32;
+  if (row0 >= M) return;
+  const int64_t row = row0 + r;
+  const int64_t rr = row < M ? row : M - 1;
+  float v = sdf_value<F16, NB>(s, p[rr * 3], p[rr * 3 + 1], p[rr * 3 + 2], l, RS, nullptr);
+  if (row < M && lane < 32) out[row] = v;
+}
+
+// gradient over a flat batch (optionally through an index list with a device-side count);
+// grid-stride over waves with a per-resident-wave pre-activation scratch
+template <int NB>
+__global__ void __launch_bounds__(256) k_sdf_grad(
+    const SdfDev* __restrict__ sp, const float* __restrict__ p, const int32_t* __restrict__ index,
+    const int32_t* __restrict__ count, int64_t M, float* __restrict__ grad,
+    float* __restrict__ n_out, float* __restrict__ p_io, float offset_eps,
+    float* __restrict__ zscr, int RS, int per_wave, int64_t zs_per_wave) {
+  extern __shared__ float smem[];
+  const SdfDev& s = *sp;
+  WaveLds l = wave_lds(smem, per_wave, RS, false);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t gw = wave_global();
+  float* zs = zscr ? zscr + gw * zs_per_wave : nullptr;
+  const int64_t total = count ? (int64_t)(*count) : M;
+  for (int64_t w = gw; w * 32 < total; w += nw) {
+    const int64_t i = w * 32 + r;
+    const bool valid = i < total;
+    const int64_t ii = valid ? i : total - 1;
+    const int64_t idx = index ? (int64_t)index[ii] : ii;
+    const float* pp = p_io ? p_io : p;
+    const float x = pp[idx * 3], y = pp[idx * 3 + 1], z = pp[idx * 3 + 2];
+    float g[3];
+    sdf_gradient<NB>(s, x, y, z, l, RS, zs, g);
+    if (valid && lane < 32) {
+      if (grad) { grad[idx * 3] = g[0]; grad[idx * 3 + 1] = g[1]; grad[idx * 3 + 2] = g[2]; }
+      if (n_out) {
+        // normals[hit] = normalize(raw, eps=1e-6); p[hit] += normals * eps * 5  (sdfs.py:156-157)
+        float nx = g[0], ny = g[1], nz = g[2];
+        normalize3(nx, ny, nz, 1e-6f);
+        n_out[idx * 3] = nx; n_out[idx * 3 + 1] = ny; n_out[idx * 3 + 2] = nz;
+        if (p_io) {
+          p_io[idx * 3] = x + (nx * offset_eps) * 5.f;
+          p_io[idx * 3 + 1] = y + (ny * offset_eps) * 5.f;
+          p_io[idx * 3 + 2] = z + (nz * offset_eps) * 5.f;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// sphere tracing + coarse scan: one fused loop with a single SDF call site
+// ------------------------------------------------------------------------------------------
+struct MarchArgs {
+  int max_steps;
+  float eps;
+  float max_t;
+  int primary;
+  double step;  // scan step = scan_max_t / 128 (python float)
+};
+
+template <bool F16, int NB>
+__global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
+    const SdfDev* __restrict__ sp, const float* __restrict__ rays, int64_t P, MarchArgs a,
+    float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
+    float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,
+    int32_t* __restrict__ hit_idx, int32_t* __restrict__ hit_count, int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const SdfDev& s = *sp;
+  WaveLds l = wave_lds(smem, per_wave, RS, F16);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t ray0 = wave_global() * 32;
+  if (ray0 >= P) return;
+  const int64_t ray = ray0 + r;
+  const bool valid = ray < P;
+  const int64_t rr = valid ? ray : P - 1;
+  const float ox = rays[rr * 6], oy = rays[rr * 6 + 1], oz = rays[rr * 6 + 2];
+  const float dx = rays[rr * 6 + 3], dy = rays[rr * 6 + 4], dz = rays[rr * 6 + 5];
+
+  // Phase 1 (sdfs.py:119-131): sphere tracing.  The reference evaluates every ray at every step;
+  // a ray that stopped marching never changes again, so the wave leaves the phase as soon as none
+  // of its rays is marching (identical results, fewer evaluations).
+  // Phase 2 (sdfs.py:238-249): sdf(o), 128 samples at fl32(step*(i+1)), then sdf(best_pos).
+  float t = 0.f;
+  bool live = valid, hit = false;
+  int i = 0;            // march step
+  int j = -2;           // scan sample: -1 = origin, 0..127 = samples, 128 = best point
+  float best = 0.f, thr = 0.f;
+  int idx = 0;
+  for (;;) {
+    if (j == -2) {
+      if (i >= a.max_steps || !wave_any(live)) {
+        if (!a.primary) break;
+        j = -1;
+      } else {
+        live = live && (t < a.max_t);
+      }
+    }
+    float px, py, pz;
+    if (j == -2) {
+      px = __fadd_rn(ox, __fmul_rn(dx, t));
+      py = __fadd_rn(oy, __fmul_rn(dy, t));
+      pz = __fadd_rn(oz, __fmul_rn(dz, t));
+    } else if (j == -1) {
+      px = ox; py = oy; pz = oz;
+    } else {
+      float ts = (j < 128) ? (float)(a.step * (double)(j + 1)) : __fmul_rn((float)idx, (float)a.step);
+      px = __fadd_rn(ox, __fmul_rn(ts, dx));
+      py = __fadd_rn(oy, __fmul_rn(ts, dy));
+      pz = __fadd_rn(oz, __fmul_rn(ts, dz));
+    }
+    const float d = sdf_value<F16, NB>(s, px, py, pz, l, RS, nullptr);
+    if (j == -2) {
+      const bool now = live && (d <= a.eps);
+      hit = hit || now;
+      live = live && !now;
+      if (live) t = t + d;
+      ++i;
+    } else if (j == -1) {
+      best = d;
+      ++j;
+    } else if (j < 128) {
+      if (d < best) idx = j + 1;
+      best = fminf(best, d);
+      ++j;
+    } else {
+      thr = -1000.f * d;
+      break;
+    }
+  }
+  if (valid && lane < 32) {
+    t_out[ray] = t;
+    hit_out[ray] = hit ? 1 : 0;
+    p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
+    p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
+    p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
+    n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
+    if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+    if (a.primary) thr_out[ray] = thr;
+  }
+  if (hit_idx) {
+    // wave-aggregated append of the hit rays (order is irrelevant downstream)
+    const uint64_t m = __ballot(valid && hit && lane < 32);
+    const int cnt = __popcll(m);
+    int base = 0;
+    if (lane == 0 && cnt) base = atomicAdd(hit_count, cnt);
+    base = __shfl(base, 0);
+    if (valid && hit && lane < 32) {
+      const int off = __popcll(m & ((1ull << lane) - 1ull));
+      hit_idx[base + off] = (int32_t)ray;
+    }
+  }
+}
+
+// shading frame of n (0 on misses) and wi = to_local(frame, -d)
+__device__ __forceinline__ void make_frame(float nx, float ny, float nz, float f[9]) {
+  // coordinate_system, interaction.py:9-27; f = [s | t | n] as columns: f[3*row + col]
+  normalize3(nx, ny, nz, 1e-7f);
+  float sign = nz >= 0.f ? 1.f : -1.f;
+  float sz = sign + nz;
+  float a = -(1.f / (fabsf(sz) < 1e-6f ? 1e-6f : sz));
+  float b = nx * ny * a;
+  float sx = (nx * nx * a * sign) + 1.f, sy = b * sign, szz = nx * -sign;
+  normalize3(sx, sy, szz, 1e-7f);
+  float tx = sy * nz - szz * ny, ty = szz * nx - sx * nz, tz = sx * ny - sy * nx;  // s x n
+  normalize3(tx, ty, tz, 1e-7f);
+  float s2x = ny * tz - nz * ty, s2y = nz * tx - nx * tz, s2z = nx * ty - ny * tx;  // n x t
+  normalize3(s2x, s2y, s2z, 1e-7f);
+  f[0] = s2x; f[3] = s2y; f[6] = s2z;
+  f[1] = tx;  f[4] = ty;  f[7] = tz;
+  f[2] = nx;  f[5] = ny;  f[8] = nz;
+}
+
+// to_local (interaction.py:37-41): normalize(mean_j frame[j][c] * w[j])
+__device__ __forceinline__ void to_local(const float f[9], float wx, float wy, float wz,
+                                         float o[3]) {
+  for (int c = 0; c < 3; ++c) o[c] = ((f[c] * wx + f[3 + c] * wy) + f[6 + c] * wz) / 3.f;
+  normalize3(o[0], o[1], o[2], 1e-7f);
+}
+
+template <int = 0>
+__global__ void k_frame_wi(const float* __restrict__ rays, const float* __restrict__ n, int64_t P,
+                           float* __restrict__ frame, float* __restrict__ wi) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  float f[9];
+  make_frame(n[i * 3], n[i * 3 + 1], n[i * 3 + 2], f);
+  if (frame)
+    for (int q = 0; q < 9; ++q) frame[i * 9 + q] = f[q];
+  if (wi) {
+    float o[3];
+    to_local(f, -rays[i * 6 + 3], -rays[i * 6 + 4], -rays[i * 6 + 5], o);
+    wi[i * 3] = o[0]; wi[i * 3 + 1] = o[1]; wi[i * 3 + 2] = o[2];
+  }
+}
+
+// shadow-ray march (intersect_test, sdfs.py:162-181)
+template <bool F16, int NB>
+__global__ void __launch_bounds__(256, F16 ? 2 : 1) k_occlusion(const SdfDev* __restrict__ sp,
+                                                    const float* __restrict__ rays, int64_t P,
+                                                    const float* __restrict__ max_t, int max_steps,
+                                                    float eps, uint8_t* __restrict__ visible,
+                                                    int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const SdfDev& s = *sp;
+  WaveLds l = wave_lds(smem, per_wave, RS, F16);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t ray0 = wave_global() * 32;
+  if (ray0 >= P) return;
+  const int64_t ray = ray0 + r;
+  const bool valid = ray < P;
+  const int64_t rr = valid ? ray : P - 1;
+  const float ox = rays[rr * 6], oy = rays[rr * 6 + 1], oz = rays[rr * 6 + 2];
+  const float dx = rays[rr * 6 + 3], dy = rays[rr * 6 + 4], dz = rays[rr * 6 + 5];
+  float t = 0.f + 1e2f * eps;
+  bool live = valid;
+  for (int i = 0; i < max_steps; ++i) {
+    if (!wave_any(live)) break;
+    const float px = __fadd_rn(ox, __fmul_rn(dx, t));
+    const float py = __fadd_rn(oy, __fmul_rn(dy, t));
+    const float pz = __fadd_rn(oz, __fmul_rn(dz, t));
+    const float d = sdf_value<F16, NB>(s, px, py, pz, l, RS, nullptr);
+    const bool now = live && (d < eps);
+    if (live) t = t + d;
+    live = live && !now;
+  }
+  if (valid && lane < 32) visible[ray] = ((t >= max_t[ray]) || live) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// shading
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float nz_eps(float v) { return fabsf(v) < 1e-7f ? 1e-7f : v; }
+
+// param_rusin2(wo, wi), utils.py:233-258 (wo, wi already local)
+__device__ __forceinline__ void rusin2(float ax, float ay, float az, float bx, float by, float bz,
+                                       float out[3]) {
+  normalize3(ax, ay, az, 1e-12f);  // wo
+  normalize3(bx, by, bz, 1e-12f);  // wi
+  float hx = ax + bx, hy = ay + by, hz = az + bz;
+  normalize3(hx, hy, hz, 1e-12f);
+  float r = fmaxf(hypotf(nz_eps(hy), nz_eps(hx)), 1e-6f);
+  float c = hx / r, s = -(hy / r);
+  // rotate wi about z: v*c + z*(v.z)*(1-c) + (z x v)*s, z x v = (-vy, vx, 0)
+  float tx = bx * c + 0.f * bz * (1.f - c) + (0.f * bz - 1.f * by) * s;
+  float ty = by * c + 0.f * bz * (1.f - c) + (1.f * bx - 0.f * bz) * s;
+  float tz = bz * c + 1.f * bz * (1.f - c) + (0.f * by - 0.f * bx) * s;
+  normalize3(tx, ty, tz, 1e-12f);
+  float c2 = hz, s2 = -sqrtf(fmaxf(1.f - hz, 1e-6f));
+  // rotate tmp about y: y x v = (vz, 0, -vx)
+  float dx = tx * c2 + 0.f * ty * (1.f - c2) + (1.f * tz - 0.f * ty) * s2;
+  float dy = ty * c2 + 1.f * ty * (1.f - c2) + (0.f * tx - 0.f * tz) * s2;
+  float dz = tz * c2 + 0.f * ty * (1.f - c2) + (0.f * ty - 1.f * tx) * s2;
+  normalize3(dx, dy, dz, 1e-12f);
+  out[0] = cosf(atan2f(nz_eps(dy), nz_eps(dx)));
+  out[1] = hz;
+  out[2] = dz;
+}
+
+__device__ __forceinline__ float fresnel_conductor(float cos_t, float eta_r) {
+  // bsdfs.py:327-341 with eta_i = 0
+  float ct2 = cos_t * cos_t;
+  float st2 = fmaxf(1.f - ct2, 1e-10f);
+  float st4 = st2 * st2;
+  float tmp = (float)((double)eta_r * (double)eta_r) - st2;
+  float a2pb2 = sqrtf(fmaxf(tmp * tmp + 0.f, 1e-10f));
+  float a = sqrtf(fmaxf(0.5f * (a2pb2 + tmp), 1e-10f));
+  float t1 = a2pb2 + ct2;
+  float t2 = 2.f * cos_t * a;
+  float rs = (t1 - t2) / (t1 + t2);
+  float t3 = a2pb2 * ct2 + st4;
+  float t4 = t2 * st2;
+  float rp = rs * (t3 - t4) / (t3 + t4);
+  return 0.5f * (rs + rp);
+}
+
+// One wave shades 32 hit rays.  The MLP evaluations of the light, the spatial weights and each
+// NeuralBSDF run through ONE call site (a job loop) so every hidden width is inlined once.
+template <bool F16>
+__global__ void __launch_bounds__(256) k_shade_direct(
+    const BsdfDev* __restrict__ bp, const LightDev* __restrict__ lp, const float* __restrict__ P_,
+    const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
+    const int32_t* __restrict__ hit_count, float* __restrict__ rgb, float* __restrict__ wout,
+    int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const BsdfDev& bs = *bp;
+  const LightDev& lt = *lp;
+  WaveLds l = wave_lds(smem, per_wave, RS, F16);
+  // per-wave scratch after Y: spatial weights K[32][kMaxComponents]
+  float* Kw = l.Y + 32 * 32;
+  const int lane = lane_id(), r = lane & 31;
+  const int ys = 32;
+  const int nc = bs.n;
+  const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t total = *hit_count;
+  for (int64_t w = wave_global(); w * 32 < total; w += nw) {
+    const int64_t i = w * 32 + r;
+    const bool valid = i < total;
+    const int64_t idx = hit_idx[valid ? i : total - 1];
+    const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
+    float fr[9];
+    make_frame(N_[idx * 3], N_[idx * 3 + 1], N_[idx * 3 + 2], fr);
+    const float wix = WI[idx * 3], wiy = WI[idx * 3 + 1], wiz = WI[idx * 3 + 2];
+
+    float ldx = 0.f, ldy = 0.f, ldz = 0.f, le[3] = {0.f, 0.f, 0.f}, wo[3] = {0.f, 0.f, 0.f};
+    float feat[3] = {0.f, 0.f, 0.f};
+    float f[3] = {0.f, 0.f, 0.f};
+    if (lt.kind == 1) {
+      // PointLights.sample_direction (lights.py:89-110)
+      float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
+      float dist = sqrtf(vx * vx + vy * vy + vz * vz);
+      ldx = vx; ldy = vy; ldz = vz;
+      normalize3(ldx, ldy, ldz, 1e-6f);
+      float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
+      le[0] = lt.scaled_dir[0] / fall; le[1] = lt.scaled_dir[1] / fall; le[2] = lt.scaled_dir[2] / fall;
+      to_local(fr, ldx, ldy, ldz, wo);
+      rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
+    }
+    if (!bs.spatial)
+      for (int j = lane >> 5; j < nc; j += 2) Kw[r * kMaxComponents + j] = 1.f;
+    // job list: -2 light field, -1 spatial weights, 0..nc-1 components
+    for (int job = -2; job < nc; ++job) {
+      const MlpDev* m = nullptr;
+      if (job == -2) m = (lt.kind == 0) ? lt.mlp : nullptr;
+      else if (job == -1) m = bs.spatial;
+      else m = (bs.comp[job].kind == 0) ? bs.comp[job].mlp : nullptr;
+      if (m) {
+        EncIn e;
+        e.xg = nullptr; e.lat = nullptr; e.x[3] = 0.f;
+        if (job < 0) { e.x[0] = px; e.x[1] = py; e.x[2] = pz; }
+        else { e.x[0] = feat[0]; e.x[1] = feat[1]; e.x[2] = feat[2]; }
+        mlp_eval_any<F16>(*m, e, l.X, RS, l.Y, ys);
+      }
+      if (job == -2) {
+        if (lt.kind == 0) {
+          // LightField.sample_direction (lights.py:175-195)
+          float vx = l.Y[r * ys], vy = l.Y[r * ys + 1], vz = l.Y[r * ys + 2];
+          float mag = sqrtf(vx * vx + vy * vy + vz * vz);
+          ldx = vx; ldy = vy; ldz = vz;
+          normalize3(ldx, ldy, ldz, 1e-6f);
+          ldx = fminf(fmaxf(ldx, 1e-6f), 1.f);
+          ldy = fminf(fmaxf(ldy, 1e-6f), 1.f);
+          ldz = fminf(fmaxf(ldz, 1e-6f), 1.f);
+          le[0] = mag * lt.color_sig[0]; le[1] = mag * lt.color_sig[1]; le[2] = mag * lt.color_sig[2];
+          to_local(fr, ldx, ldy, ldz, wo);
+          rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
+        }
+      } else if (job == -1) {
+        if (m)
+          for (int j = lane >> 5; j < nc; j += 2) Kw[r * kMaxComponents + j] = sigmoidf_(l.Y[r * ys + j]);
+      } else {
+        const BsdfCompDev& c = bs.comp[job];
+        float v[3];
+        if (c.kind == 0) {
+          for (int q = 0; q < 3; ++q) v[q] = act_fwd<false>(l.Y[r * ys + q], c.act);
+        } else if (c.kind == 1) {
+          // Diffuse.eval_and_pdf (bsdfs.py:108-118)
+          for (int q = 0; q < 3; ++q) {
+            float x = wo[2] * c.params[q];
+            v[q] = (c.act == ACT_NONE) ? x / (float)M_PI : act_fwd<false>(x, c.act);
+          }
+        } else {
+          // Conductor.eval_and_pdf (bsdfs.py:364-388)
+          float rx = -wix, ry = -wiy, rz = wiz;
+          bool th = ((rx * wo[0] + ry * wo[1]) + rz * wo[2]) > 0.94f;
+          float fres = fresnel_conductor(wiz, c.params[3]);
+          for (int q = 0; q < 3; ++q) v[q] = th ? fres * act_fwd<false>(c.params[q], c.act) : 0.f;
+        }
+        wave_lds_fence();
+        const float kj = Kw[r * kMaxComponents + job];
+        f[0] += v[0] * kj; f[1] += v[1] * kj; f[2] += v[2] * kj;
+      }
+      wave_lds_fence();
+    }
+    if (valid && lane < 32) {
+      // integrators.py:186-189: mis(=1) * bsdf_val * emitter_val, / emitter_samples(=1)
+      rgb[idx * 3] = (1.f * f[0]) * le[0];
+      rgb[idx * 3 + 1] = (1.f * f[1]) * le[1];
+      rgb[idx * 3 + 2] = (1.f * f[2]) * le[2];
+      if (wout)
+        for (int j = 0; j < nc; ++j) wout[idx * nc + j] = Kw[r * kMaxComponents + j];
+    }
+    wave_lds_fence();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// cameras + composite
+// ------------------------------------------------------------------------------------------
+template <int = 0>
+__global__ void k_raygen(const nrt_camera* __restrict__ cams, int N, int x0, int y0, int W, int H,
+                         float with_noise, const float* __restrict__ noise,
+                         const float* __restrict__ positions, float* __restrict__ rays) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)N * W * H;
+  if (i >= total) return;
+  const int yy = (int)(i % H);
+  const int xx = (int)((i / H) % W);
+  const int n = (int)(i / ((int64_t)W * H));
+  const nrt_camera& c = cams[n];
+  // positions = stack([gy, gx]) -> u = column (y), v = row (x)   (main.py:66-71)
+  const int64_t pix = (int64_t)xx * H + yy;
+  float u = (float)(y0 + yy), v = (float)(x0 + xx);
+  if (positions) { u = positions[pix * 2]; v = positions[pix * 2 + 1]; }
+  float o[3], d[3];
+  if (c.kind == NRT_CAM_NERF) {
+    if (with_noise != 0.f && noise) {
+      u = u + (noise[pix] - 0.5f) * with_noise;
+      v = v + (noise[(int64_t)W * H + pix] - 0.5f) * with_noise;
+    }
+    const float half = (float)((double)c.size * 0.5);
+    float a0 = (u - half) / c.focal, a1 = -((v - half) / c.focal), a2 = -1.f;
+    const float* M = c.mat;  // [3][4]
+    for (int j = 0; j < 3; ++j) d[j] = (a0 * M[4 * j] + a1 * M[4 * j + 1]) + a2 * M[4 * j + 2];
+    normalize3(d[0], d[1], d[2], 1e-12f);
+    o[0] = M[3]; o[1] = M[7]; o[2] = M[11];
+  } else if (c.kind == NRT_CAM_DTU) {
+    const float su = 1600.f / (float)c.size, sv = 1200.f / (float)c.size;
+    float uu = u * su, vv = v * sv;
+    const float* K = c.intrinsic;
+    float fx = K[0], fy = K[5], cx = K[2], cy = K[6], sk = K[1];
+    float xl = ((((uu - cx) + cy * sk / fy) - sk * vv / fy) / fx) * 1.f;
+    float yl = ((vv - cy) / fy) * 1.f;
+    float pt[4] = {xl, yl, 1.f, 1.f};
+    const float* Pm = c.mat;  // pose [4][4]
+    float wv[3];
+    for (int j = 0; j < 3; ++j)
+      wv[j] = ((Pm[4 * j] * pt[0] + Pm[4 * j + 1] * pt[1]) + Pm[4 * j + 2] * pt[2]) + Pm[4 * j + 3] * pt[3];
+    o[0] = Pm[3]; o[1] = Pm[7]; o[2] = Pm[11];
+    d[0] = wv[0] - o[0]; d[1] = wv[1] - o[1]; d[2] = wv[2] - o[2];
+    normalize3(d[0], d[1], d[2], 1e-12f);
+  } else {
+    // FoV (renderer/cameras.py:539-575): jitter, NDC, inverse projection, normalize(point)
+    if (with_noise != 0.f && noise) {
+      u = u + (with_noise * noise[pix * 2] - with_noise / 2.f);
+      v = v + (with_noise * noise[pix * 2 + 1] - with_noise / 2.f);
+    }
+    float px = -2.f * (u / (float)c.size) + 1.f;
+    float py = -2.f * (v / (float)c.size) + 1.f;
+    float pt[4] = {px, py, 1.f, 1.f};
+    const float* Mi = c.mat;  // row-vector convention: out = pt @ Mi
+    float q[4];
+    for (int j = 0; j < 4; ++j)
+      q[j] = ((pt[0] * Mi[j] + pt[1] * Mi[4 + j]) + pt[2] * Mi[8 + j]) + pt[3] * Mi[12 + j];
+    d[0] = q[0] / q[3]; d[1] = q[1] / q[3]; d[2] = q[2] / q[3];
+    normalize3(d[0], d[1], d[2], 1e-12f);
+    o[0] = c.origin[0]; o[1] = c.origin[1]; o[2] = c.origin[2];
+  }
+  float* rr = rays + i * 6;
+  rr[0] = o[0]; rr[1] = o[1]; rr[2] = o[2]; rr[3] = d[0]; rr[4] = d[1]; rr[5] = d[2];
+}
+
+template <int = 0>
+__global__ void k_composite(const float* __restrict__ rgb, const float* __restrict__ thr,
+                            const uint8_t* __restrict__ hit, int N, int W, int H, int alpha,
+                            int fill, float bg, float* __restrict__ img, int IW, int IH, int C,
+                            int X0, int Y0) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)N * W * H;
+  if (i >= total) return;
+  const int yy = (int)(i % H);
+  const int xx = (int)((i / H) % W);
+  const int n = (int)(i / ((int64_t)W * H));
+  float* o = img + (((int64_t)n * IW + (X0 + xx)) * IH + (Y0 + yy)) * C;
+  const bool miss = fill && hit && !hit[i];
+  for (int c = 0; c < 3 && c < C; ++c) o[c] = miss ? bg : rgb[i * 3 + c];
+  if (alpha && C > 3) o[3] = miss ? bg : 1.f / (1.f + expf(-thr[i]));
+}
+
+}  // namespace nrt

@@ -1,0 +1,80 @@
+// nrt_launch.h -- host-side launch helpers shared by the nrt_api_*.hip translation units
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "nrt_internal.h"
+#include "nrt_kernels.h"
+
+namespace nrt {
+
+
+
+// compile-time hidden-block count for a runtime MLP width (32, 64, 96, 128, 256)
+#define NRT_NB_SWITCH(nbv, ...)                               \
+  switch (nbv) {                                              \
+    case 2: { constexpr int NB = 2; __VA_ARGS__; } break;     \
+    case 3: { constexpr int NB = 3; __VA_ARGS__; } break;     \
+    case 4: { constexpr int NB = 4; __VA_ARGS__; } break;     \
+    case 8: { constexpr int NB = 8; __VA_ARGS__; } break;     \
+    default: { constexpr int NB = 1; __VA_ARGS__; } break;    \
+  }
+
+static inline int ceil_div64(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+
+// LDS layout of one launch: per-wave floats and waves per 64-thread-multiple block
+struct LdsPlan {
+  int RS = 1;         // FP32 slab stride
+  int ys = 1;         // Y stride
+  int per_wave = 0;   // floats
+  int waves = 4;      // waves per block
+  size_t bytes = 0;
+};
+
+static inline int env_max_waves() {
+  const char* s = std::getenv("NRT_MAX_WAVES");
+  int v = s ? std::atoi(s) : 4;
+  return v >= 1 && v <= 4 ? v : 4;
+}
+
+static inline LdsPlan plan_lds(int hidden, int ke, int ys, bool f16, bool with_grad, int max_waves = 4) {
+  LdsPlan p;
+  max_waves = std::min(max_waves, env_max_waves());
+  p.ys = std::max(ys, 1);
+  p.RS = f16 ? 1 : slab_stride(std::max(hidden, 32), std::max(ke, 16), with_grad);
+  p.per_wave = wave_lds_floats(p.RS, p.ys, f16);
+  int per_wave_bytes = p.per_wave * 4;
+  p.waves = std::max(1, std::min(max_waves, kLdsBytes / std::max(per_wave_bytes, 1)));
+  p.bytes = (size_t)p.waves * per_wave_bytes;
+  return p;
+}
+
+template <typename K>
+static inline int set_lds(K kernel, size_t bytes) {
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
+  }
+  return NRT_OK;
+}
+
+static inline int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, what);
+  return NRT_OK;
+}
+
+static inline int sdf_dims(const nrt_sdf* s, int& hidden, int& ke) {
+  hidden = 32; ke = 16;
+  if (s->mlp) { hidden = s->mlp->desc.hidden; ke = s->mlp->host_dev.ke; }
+  return NRT_OK;
+}
+
+}  // namespace nrt

@@ -1,0 +1,203 @@
+// nrt_pack.hip -- host packer: torch-layout SkipConnMLP weights -> per-lane MFMA A fragments.
+//
+// Layer l input positions (neural_blocks.py:46-55, 80-86):
+//   l = 0 (init)          : encoding slots                       (reference columns: enc cols)
+//   l = 1..L (layers[l-1]): hidden 0..H-1, then slots if skip    (columns: h, then H + enc col)
+//   l = L+1 (out)         : hidden 0..H-1
+// Fragment (kstep s, rowblock ib) holds, for lane (i = l&31, half hf = l>>5), the values of
+// W[32 ib + i][column] that the MFMA consumes at that lane:
+//   FP16 hidden k-steps use the accumulator-as-operand order (k = 16*(s&1) + 8*(j>>2) + 4hf + (j&3)
+//   inside 32-row block s>>1); FP16 encoding k-steps use slot 16s + 8hf + j; FP32 k-steps use
+//   position 2s + hf.  W^T fragments (FP32 backward) swap the roles of rows and positions.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "nrt_internal.h"
+
+namespace {
+
+struct Layer {
+  const float* W;  // [R][C]
+  const float* b;  // [R]
+  int R, C;
+  bool hidden_in;  // has the H hidden inputs
+  bool enc_in;     // has the encoding slots
+};
+
+struct Blob {
+  std::vector<char> bytes;
+  size_t add(const void* p, size_t n) {
+    size_t off = (bytes.size() + 255) & ~size_t(255);
+    bytes.resize(off + n);
+    std::memcpy(bytes.data() + off, p, n);
+    return off;
+  }
+};
+
+}  // namespace
+
+extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
+                              const float* const* weights, const float* const* biases,
+                              nrt_mlp** out) {
+  using namespace nrt;
+  if (!d || !basis || !weights || !biases || !out) {
+    set_error("nrt_mlp_create: null argument");
+    return NRT_EINVAL;
+  }
+  const int in = d->in_size, H = d->hidden, L = d->num_layers, O = d->out, F = d->freqs;
+  const int lat = d->latent;
+  if (in < 1 || H < 32 || H % 32 || H > 256 || L < 1 || L + 2 > kMaxLin || O < 1 || O > 96 ||
+      F < 0 || d->skip < 1 || lat < 0) {
+    set_error("nrt_mlp_create: unsupported shape (hidden must be 32..256 step 32, out <= 96, "
+              "layers <= 18)");
+    return NRT_EUNSUPPORTED;
+  }
+  const int NB = H / 32;
+  if (NB != 1 && NB != 2 && NB != 3 && NB != 4 && NB != 8) {
+    set_error("nrt_mlp_create: hidden must be one of 32, 64, 96, 128, 256");
+    return NRT_EUNSUPPORTED;
+  }
+  const int dp = in + 2 * F + lat;
+  const int ke = (dp + 15) / 16 * 16;
+  const int OB = (O + 31) / 32;
+
+  // encoding slot -> reference encoding column ([x, sin, cos, latent]); -1 = padding
+  std::vector<int> slot_col(ke, -1);
+  for (int s = 0; s < ke; ++s) {
+    if (s < 2 * F) slot_col[s] = (s & 1) ? in + F + (s >> 1) : in + (s >> 1);
+    else if (s < 2 * F + in) slot_col[s] = s - 2 * F;
+    else if (s < 2 * F + in + lat) slot_col[s] = in + 2 * F + (s - 2 * F - in);
+  }
+
+  std::vector<Layer> layers;
+  layers.push_back({weights[0], biases[0], H, dp, false, true});
+  for (int i = 0; i < L; ++i) {
+    bool skip = (i != L - 1) && (i % d->skip == 0);
+    layers.push_back({weights[1 + i], biases[1 + i], H, skip ? H + dp : H, true, skip});
+  }
+  layers.push_back({weights[L + 1], biases[L + 1], O, H, true, false});
+
+  auto col_of_hidden = [](int k) { return k; };
+  auto col_of_slot = [&](const Layer& ly, int slot) {
+    int c = slot_col[slot];
+    if (c < 0) return -1;
+    return ly.hidden_in ? H + c : c;
+  };
+  auto wval = [](const Layer& ly, int row, int col) -> float {
+    if (row < 0 || row >= ly.R || col < 0 || col >= ly.C) return 0.f;
+    return ly.W[(size_t)row * ly.C + col];
+  };
+
+  Blob blob;
+  MlpDev md;
+  std::memset(&md, 0, sizeof(md));
+  md.in_size = in; md.hidden = H; md.n_hidden = L; md.out = O; md.freqs = F;
+  md.skip = d->skip; md.latent = lat; md.act = d->activation;
+  md.dp = dp; md.ke = ke; md.nb = NB; md.ob = OB;
+
+  size_t off_basis = blob.add(basis, sizeof(float) * (size_t)in * (F > 0 ? F : 1));
+  std::vector<size_t> off16(layers.size()), off32(layers.size()), offt(layers.size()),
+      offb(layers.size());
+
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& ly = layers[l];
+    const int nrb = (ly.R + 31) / 32;
+    // ---- FP16 fragments
+    {
+      std::vector<_Float16> f;
+      const int ks_h = ly.hidden_in ? 2 * NB : 0;
+      const int ks_e = ly.enc_in ? ke / 16 : 0;
+      f.resize((size_t)(ks_h + ks_e) * nrb * 64 * 8);
+      for (int s = 0; s < ks_h + ks_e; ++s)
+        for (int ib = 0; ib < nrb; ++ib)
+          for (int lane = 0; lane < 64; ++lane) {
+            int i = lane & 31, hf = lane >> 5;
+            for (int j = 0; j < 8; ++j) {
+              int col;
+              if (s < ks_h) {
+                int k = 32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * hf + (j & 3);
+                col = col_of_hidden(k);
+              } else {
+                col = col_of_slot(ly, 16 * (s - ks_h) + 8 * hf + j);
+              }
+              f[(((size_t)s * nrb + ib) * 64 + lane) * 8 + j] = (_Float16)wval(ly, 32 * ib + i, col);
+            }
+          }
+      off16[l] = blob.add(f.data(), f.size() * sizeof(_Float16));
+    }
+    // ---- FP32 fragments (natural k order over the slab: hidden then slots)
+    {
+      const int ks_h = ly.hidden_in ? H / 2 : 0;
+      const int ks_e = ly.enc_in ? ke / 2 : 0;
+      std::vector<float> f((size_t)(ks_h + ks_e) * nrb * 64);
+      for (int s = 0; s < ks_h + ks_e; ++s)
+        for (int ib = 0; ib < nrb; ++ib)
+          for (int lane = 0; lane < 64; ++lane) {
+            int i = lane & 31, hf = lane >> 5;
+            int col = (s < ks_h) ? col_of_hidden(2 * s + hf) : col_of_slot(ly, 2 * (s - ks_h) + hf);
+            f[((size_t)s * nrb + ib) * 64 + lane] = wval(ly, 32 * ib + i, col);
+          }
+      off32[l] = blob.add(f.data(), f.size() * sizeof(float));
+    }
+    // ---- FP32 W^T fragments (backward) for init and hidden layers
+    if (l + 1 < layers.size()) {
+      const int npos = (ly.hidden_in ? H : 0) + (ly.enc_in ? ke : 0);
+      const int nrbt = (npos + 31) / 32;
+      md.nbt[l] = nrbt;
+      const int ks = H / 2;  // k over the layer's H output rows
+      std::vector<float> f((size_t)ks * nrbt * 64);
+      for (int s = 0; s < ks; ++s)
+        for (int ib = 0; ib < nrbt; ++ib)
+          for (int lane = 0; lane < 64; ++lane) {
+            int i = lane & 31, hf = lane >> 5;
+            int pos = 32 * ib + i;
+            int col = -1;
+            if (pos < npos) {
+              if (ly.hidden_in && pos < H) col = col_of_hidden(pos);
+              else col = col_of_slot(ly, pos - (ly.hidden_in ? H : 0));
+            }
+            f[((size_t)s * nrbt + ib) * 64 + lane] = wval(ly, 2 * s + hf, col);
+          }
+      offt[l] = blob.add(f.data(), f.size() * sizeof(float));
+    }
+    // ---- bias padded to row blocks
+    {
+      std::vector<float> b((size_t)nrb * 32, 0.f);
+      for (int r = 0; r < ly.R; ++r) b[r] = ly.b[r];
+      offb[l] = blob.add(b.data(), b.size() * sizeof(float));
+    }
+  }
+  size_t off_w0 = blob.add(layers.back().W, sizeof(float) * H);  // out.weight[0, :]
+
+  std::unique_ptr<nrt_mlp> m(new nrt_mlp());
+  m->desc = *d;
+  m->blob_bytes = blob.bytes.size();
+  NRT_HIP(hipMalloc(&m->blob, m->blob_bytes));
+  NRT_HIP(hipMemcpy(m->blob, blob.bytes.data(), m->blob_bytes, hipMemcpyHostToDevice));
+  char* base = static_cast<char*>(m->blob);
+  md.basis = reinterpret_cast<const float*>(base + off_basis);
+  for (size_t l = 0; l < layers.size(); ++l) {
+    md.w16[l] = reinterpret_cast<const h8*>(base + off16[l]);
+    md.w32[l] = reinterpret_cast<const float*>(base + off32[l]);
+    md.wt32[l] = (l + 1 < layers.size()) ? reinterpret_cast<const float*>(base + offt[l]) : nullptr;
+    md.bias[l] = reinterpret_cast<const float*>(base + offb[l]);
+  }
+  md.wout_row0 = reinterpret_cast<const float*>(base + off_w0);
+  m->host_dev = md;
+  NRT_HIP(hipMalloc(&m->dev, sizeof(MlpDev)));
+  NRT_HIP(hipMemcpy(m->dev, &md, sizeof(MlpDev), hipMemcpyHostToDevice));
+  *out = m.release();
+  return NRT_OK;
+}
+
+extern "C" int nrt_mlp_destroy(nrt_mlp* m) {
+  if (!m) return NRT_OK;
+  if (m->blob) (void)hipFree(m->blob);
+  if (m->dev) (void)hipFree(m->dev);
+  delete m;
+  return NRT_OK;
+}

@@ -1,0 +1,1 @@
+from .integrators import Debug, Depth, Direct, Integrator, Mask, NeRFIntegrator  # noqa: F401

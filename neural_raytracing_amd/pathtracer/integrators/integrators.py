@@ -1,0 +1,156 @@
+"""Integrators (integrators/integrators.py).  ``Direct`` runs the fused HIP path:
+nrt_sdf_intersect (march + coarse scan + normals) then nrt_shade_direct (light sample +
+spatially varying BSDF) over the compacted hit list."""
+import torch
+import torch.nn as nn
+
+from ... import _lib
+
+
+class Integrator(nn.Module):
+    def __init__(self, max_depth=2, russian_roulette_depth=5, sampler=None, lights=None):
+        super().__init__()
+        self.max_depth = max_depth
+        self.rr_depth = russian_roulette_depth
+        self.sampler = sampler
+        self.lights = lights
+
+    def dims(self):
+        raise NotImplementedError()
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        raise NotImplementedError()
+
+
+class Debug(Integrator):
+    """Normals as colour (integrators.py:25-35)."""
+
+    def dims(self):
+        return 3
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        si, active = shapes.intersect(rays)
+        result = torch.where(active.unsqueeze(-1), (si.n + 1) / 2,
+                             torch.tensor(0., device=active.device))
+        return result, active, si
+
+
+class Mask(Integrator):
+    """Adds the hit mask as a channel (integrators.py:45-54)."""
+
+    def __init__(self, sub_integrator, **kwargs):
+        super().__init__(**kwargs)
+        self.sub_integrator = sub_integrator
+
+    def dims(self):
+        return self.sub_integrator.dims() + 1
+
+    def sample(self, density_field, rays, bsdf, **kwargs):
+        result, active, si = self.sub_integrator.sample(density_field, rays, bsdf, **kwargs)
+        mask = torch.where(active, 1., 0.)
+        return torch.cat([result, mask.unsqueeze(-1)], dim=-1), torch.ones_like(active), si
+
+
+class Depth(Integrator):
+    """Ray depths (integrators.py:57-67)."""
+
+    def __init__(self, scale=False, empty_val=-1, **kwargs):
+        super().__init__(**kwargs)
+        self.empty_val = empty_val
+        self.scale = scale
+
+    def dims(self):
+        return 1
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        it, active = shapes.intersect(rays)
+        results = torch.where(active, it.t, torch.full_like(it.t, self.empty_val))
+        if self.scale:
+            results[results != 0] /= results[results != 0].max()
+        return results.unsqueeze(-1), active, it
+
+
+def _light_handle(lights):
+    nrt = getattr(lights, "nrt", None)
+    if nrt is None:
+        raise _lib.NrtError(f"light {type(lights).__name__} has no HIP implementation "
+                            "(supported: LightField, PointLights)")
+    return nrt()
+
+
+def _bsdf_handle(bsdf):
+    nrt = getattr(bsdf, "nrt", None)
+    if nrt is None:
+        from ..bsdf import ComposeSpatialVarying
+        comp = getattr(bsdf, "_component", None)
+        if comp is None:
+            raise _lib.NrtError(f"BSDF {type(bsdf).__name__} has no HIP implementation")
+        wrapper = getattr(bsdf, "_nrt_single", None)
+        if wrapper is None:
+            wrapper = ComposeSpatialVarying.__new__(ComposeSpatialVarying)
+            nn.Module.__init__(wrapper)
+            wrapper.bsdfs = [bsdf]
+            wrapper.sp_var_fn = None
+            object.__setattr__(bsdf, "_nrt_single", wrapper)
+        return wrapper.nrt()
+    return nrt()
+
+
+class Direct(Integrator):
+    """Direct lighting, one emitter sample, no BSDF sampling (integrators.py:139-206).
+
+    ``training`` is set before ``nn.Module.__init__`` resets it to True (integrators.py:153-154),
+    so the coarse scan always runs; that quirk is kept.
+    """
+    DEFAULT_EMITTER_SAMPLES = 1
+    DEFAULT_BSDF_SAMPLES = 0
+
+    def dims(self):
+        return 3
+
+    def __init__(self, emitter_samples=DEFAULT_EMITTER_SAMPLES, bsdf_samples=DEFAULT_BSDF_SAMPLES,
+                 training=True, **kwargs):
+        self.emitter_samples = emitter_samples
+        self.bsdf_samples = bsdf_samples
+        self.training = training
+        super().__init__(**kwargs)
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        lights = kwargs.get("lights", self.lights)
+        w_isect = kwargs.get("w_isect")
+        if w_isect not in (None, False):
+            raise _lib.NrtError("Direct(w_isect=...) shadow rays are not on the HIP path yet")
+        if self.emitter_samples != 1 or self.bsdf_samples != 0:
+            raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
+        result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
+        it, active = shapes.intersect(rays, primary=self.training)
+        hit_idx, hit_count, flat = it._nrt_hits
+        P = flat.shape[0]
+        rgb = result.reshape(P, 3)
+        nb = len(getattr(bsdf, "bsdfs", [bsdf]))
+        weights = torch.zeros(P, nb, device=rays.device)
+        _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights),
+                  _lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
+                  _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
+                  _lib.ptr(rgb), _lib.ptr(weights), _lib.precision_code(), _lib.stream())
+        setattr(it, "normalized_weights", weights.reshape(rays.shape[:-1] + (nb,)))
+        return result, active, it
+
+
+class NeRFIntegrator(Integrator):
+    """Appends sigmoid(throughput) as alpha (integrators.py:243-257)."""
+
+    def __init__(self, sub_integrator, **kwargs):
+        super().__init__(**kwargs)
+        self.sub_integrator = sub_integrator
+
+    def dims(self):
+        return self.sub_integrator.dims() + 1
+
+    def sample(self, density_field, rays, bsdf, **kwargs):
+        result, active, mi = self.sub_integrator.sample(density_field, rays, bsdf, **kwargs)
+        alpha = mi.throughput.unsqueeze(-1)
+        if mi.with_logits:
+            alpha = alpha.sigmoid()
+        result = torch.cat([result, alpha], dim=-1)
+        return result, torch.tensor(True, device=result.device), mi

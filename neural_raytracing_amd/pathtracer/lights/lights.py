@@ -1,0 +1,100 @@
+"""Lights (lights/lights.py).  Sampling at the hit points runs inside ``nrt_shade_direct``;
+the handles below pack the parameters."""
+import ctypes
+from itertools import chain
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ... import _lib
+from .._handles import _Handle, _host, mlp_handle
+from ..interaction import DirectionSample
+from ..neural_blocks import SkipConnMLP
+
+
+class Light(nn.Module):
+    def __init__(self):
+        super().__init__()
+
+    def sample_direction(self, it, sampler, active=True):
+        raise NotImplementedError()
+
+    def intersect(self, _rays):
+        return None, False
+
+
+class PointLights(Light):
+    """Point light with constant/linear/quadratic falloff (lights.py:40-110)."""
+
+    def __init__(self, intensity=[1., 1., 1.], location=[0, 1, 0], const=1e-8, linear=1e-8,
+                 square=1, scale=1e2, device="cuda"):
+        super().__init__()
+        self.device = device
+        self.scale = torch.tensor(scale, dtype=torch.float, requires_grad=True)
+        if type(intensity) is torch.Tensor:
+            self.intensity = intensity
+        else:
+            self.intensity = torch.tensor([intensity], device=device, requires_grad=True, dtype=torch.float)
+        if type(location) is torch.Tensor:
+            self.location = location
+        else:
+            self.location = torch.tensor(location, device=device, requires_grad=True, dtype=torch.float)
+            if len(self.location.shape) == 1:
+                self.location = self.location.unsqueeze(0).detach()
+        self.const = torch.tensor(const, dtype=torch.float, requires_grad=True)
+        self.linear = torch.tensor(linear, dtype=torch.float, requires_grad=True)
+        self.square = torch.tensor(square, dtype=torch.float, requires_grad=True)
+
+    def parameters(self):
+        return chain(self.location_parameters(), self.spectrum_parameters())
+
+    def location_parameters(self):
+        return [self.location]
+
+    def spectrum_parameters(self):
+        return [self.scale, self.intensity, self.const, self.linear, self.square]
+
+    def nrt(self):
+        loc = _host(self.location.reshape(-1, 3)[0])
+        inten = _host(self.intensity.reshape(-1, 3)[0])
+        out = ctypes.c_void_p()
+        _lib.check(_lib.load().nrt_light_create_point(
+            loc.data_ptr(), inten.data_ptr(), float(self.const), float(self.linear),
+            float(self.square), float(self.scale), ctypes.byref(out)), "nrt_light_create_point")
+        h = _Handle(out, "nrt_light_destroy")
+        object.__setattr__(self, "_nrt_light", h)
+        return h.value
+
+    def envmap(self, p):
+        d = p[None, ...] - self.location[:, None, None, :]
+        dist = torch.linalg.norm(d, dim=-1, keepdim=True)
+        spectrum = self.const.clamp(min=1e-6) + self.linear.clamp(min=1e-6) * dist + \
+            self.square.clamp(min=1e-6) * dist.square()
+        return self.scale * F.normalize(self.intensity, dim=-1) / spectrum.clamp(min=1e-6)
+
+
+class LightField(nn.Module):
+    """Learned light f(p) -> direction * magnitude, colour sigmoid(c) (lights.py:155-195)."""
+
+    def __init__(self, device="cuda"):
+        super().__init__()
+        self.light_field_approx = SkipConnMLP(in_size=3, out=3, num_layers=10, hidden_size=256,
+                                              device=device).to(device)
+        self.color = nn.Parameter(torch.tensor([0., 0., 0.], requires_grad=True, dtype=torch.float,
+                                               device=device), requires_grad=True)
+        self.device = device
+
+    def nrt(self):
+        mh = mlp_handle(self.light_field_approx)
+        color = _host(self.color)
+        key = (id(mh), tuple(color.tolist()))
+        cached = getattr(self, "_nrt_light", None)
+        if cached is not None and cached[0] == key:
+            return cached[1].value
+        out = ctypes.c_void_p()
+        _lib.check(_lib.load().nrt_light_create_field(mh.value, color.data_ptr(), ctypes.byref(out)),
+                   "nrt_light_create_field")
+        h = _Handle(out, "nrt_light_destroy", [mh])
+        object.__setattr__(self, "_nrt_light", (key, h))
+        return h.value

@@ -1,0 +1,120 @@
+"""Renderer entry points (main.py:13-179) on the HIP path.
+
+The tile loop, crop logic, background fill and the ``addition`` hook follow the reference;
+each tile's rays come from ``nrt_raygen`` (cameras with ``rays_tile``) and the integrator runs
+its HIP kernels.  Positions follow main.py:66-71: pixel (row x, col y) has u = y, v = x.
+"""
+import random
+
+import torch
+
+from .render import fused_integrator, render_tile
+from .samplers import Sampler
+
+
+def nothing(_):
+    return None
+
+
+def rand_uv(w, h, size):
+    return random.randint(0, w - size), random.randint(0, h - size)
+
+
+def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, with_noise, device):
+    if hasattr(cameras, "rays_tile"):
+        return cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise)
+    gx, gy = torch.meshgrid(torch.arange(x0, x0 + chunk, device=device, dtype=torch.float),
+                            torch.arange(y0, y0 + chunk, device=device, dtype=torch.float),
+                            indexing="ij")
+    positions = torch.stack([gy, gx], dim=-1)
+    return cameras.sample_positions(positions, sampler, bundle_size, size=size, N=batch_dims,
+                                    with_noise=with_noise)
+
+
+def _composite(out, values, mask, background, xs, ys, chunk):
+    valid = mask.any(dim=-1)
+    v = torch.mean(values, dim=-2)
+    v[~valid] = background
+    out[:, xs:xs + chunk, ys:ys + chunk, :] = v
+
+
+def _fused(integrator, cameras, w_isect, addition):
+    """Direct / NeRFIntegrator(Direct) tiles go through the fused kernels when nothing needs the
+    interaction record (addition is the default `nothing`)."""
+    if addition is not nothing or w_isect not in (None, False) or not hasattr(cameras, "rays_tile"):
+        return None
+    return fused_integrator(integrator)
+
+
+def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=None, height=None,
+              chunk_size=32, bundle_size=4, background=1, addition=nothing, sampler=Sampler(),
+              silent=False, trim=0, device="cuda", squeeze_first=True, w_isect=False,
+              with_noise=1e-3):
+    """main.py:13-93."""
+    if trim != 0:
+        raise NotImplementedError("pathtrace(trim != 0) is not supported on the HIP path")
+    batch_dims = len(cameras)
+    if width is None:
+        width = size
+    if height is None:
+        height = size
+    out = torch.full([batch_dims, width, height, integrator.dims()], background, device=device,
+                     dtype=torch.float)
+    assert (size % chunk_size) == 0, \
+        f"Can only specify chunk sizes which evenly divide size, {size} % {chunk_size}"
+    xs = list(range(0, width, chunk_size))
+    ys = list(range(0, height, chunk_size))
+    it = None
+    fused = _fused(integrator, cameras, w_isect, addition)
+    for ij in range(len(xs) * len(ys)):
+        i, j = divmod(ij, len(ys))
+        x0, y0 = xs[j], ys[i]
+        if fused is not None:
+            render_tile(fused, shapes, lights, cameras, bsdf, out, x0, y0, chunk_size, size,
+                        with_noise, background)
+            continue
+        rays = _tile_rays(cameras, x0, y0, chunk_size, size, sampler, bundle_size, batch_dims,
+                          with_noise, device)
+        values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
+                                             sampler=sampler, w_isect=w_isect)
+        _composite(out, values, mask, background, x0, y0, chunk_size)
+    if squeeze_first and batch_dims == 1:
+        out = out.squeeze(0)
+    return out, addition(it)
+
+
+def pathtrace_sample(shapes, lights, cameras, integrator, bsdf=None, size=512, chunk_size=32,
+                     bundle_size=4, crop_size=128, uv=None, background=1, sampler=Sampler(),
+                     addition=nothing, silent=False, mode="crop", device="cuda",
+                     squeeze_first=True, w_isect=False, with_noise=1e-2):
+    """main.py:97-179."""
+    if uv is None:
+        uv = rand_uv(size, size, crop_size)
+    batch_dims = len(cameras)
+    img = [batch_dims, size, size, integrator.dims()]
+    if mode == "crop":
+        img = [batch_dims, crop_size, crop_size, integrator.dims()]
+    out = torch.full(img, background, device=device, dtype=torch.float)
+    assert (size % chunk_size) == 0, \
+        f"Can only specify chunk sizes which evenly divide size, {size} % {chunk_size}"
+    chunk_size = min(chunk_size, crop_size)
+    u = max(min(uv[0], size - crop_size), 0)
+    v = max(min(uv[1], size - crop_size), 0)
+    xs = list(range(u, u + crop_size, chunk_size))
+    ys = list(range(v, v + crop_size, chunk_size))
+    it = None
+    for ij in range(len(xs) * len(ys)):
+        i, j = divmod(ij, len(ys))
+        x0, y0 = xs[j], ys[i]
+        rays = _tile_rays(cameras, x0, y0, chunk_size, size, sampler, bundle_size, batch_dims,
+                          with_noise, device)
+        values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
+                                             sampler=sampler, w_isect=w_isect)
+        if mode == "crop":
+            _composite(out, values, mask, background, x0 - u, y0 - v, chunk_size)
+        else:
+            _composite(out, values, mask, background, x0, y0, chunk_size)
+    if squeeze_first and batch_dims == 1:
+        out = out.squeeze(0)
+    setattr(it, "crop_uv", uv)
+    return out, addition(it)

@@ -1,0 +1,149 @@
+"""Fused render path: one tile = nrt_raygen -> nrt_sdf_intersect -> nrt_shade_direct ->
+nrt_composite, all stream-ordered on torch's current stream, with buffers reused across calls.
+
+``pathtrace`` / ``pathtrace_sample`` (main.py) route ``Direct`` and ``NeRFIntegrator(Direct)``
+tiles here; ``render_rows`` renders an arbitrary set of image rows (the multi-GPU row shard,
+SURVEY §8e).  Semantics are the reference's Direct.sample (integrators.py:156-206) +
+NeRFIntegrator (integrators.py:249-257) + the tile composite (main.py:85-90) for bundle_size 1.
+"""
+import ctypes
+import random
+
+import torch
+
+from .. import _lib
+from .integrators import Direct, NeRFIntegrator
+from .integrators.integrators import _bsdf_handle, _light_handle
+from .shapes.sdfs import sdf_handle
+
+
+def fused_integrator(integrator):
+    """(direct, with_alpha) if the integrator is Direct or NeRFIntegrator(Direct), else None."""
+    if isinstance(integrator, NeRFIntegrator) and type(integrator.sub_integrator) is Direct:
+        return integrator.sub_integrator, True
+    if type(integrator) is Direct:
+        return integrator, False
+    return None
+
+
+class _Buffers:
+    def __init__(self, P, nb, device):
+        f = dict(device=device)
+        self.P = P
+        self.t = torch.empty(P, **f)
+        self.hit = torch.empty(P, dtype=torch.uint8, **f)
+        self.p = torch.empty(P, 3, **f)
+        self.n = torch.empty(P, 3, **f)
+        self.raw = torch.empty(P, 3, **f)
+        self.wi = torch.empty(P, 3, **f)
+        self.thr = torch.empty(P, **f)
+        self.rgb = torch.empty(P, 3, **f)
+        self.weights = torch.empty(P, max(nb, 1), **f)
+        self.hit_idx = torch.empty(max(P, 1), dtype=torch.int32, **f)
+        self.hit_count = torch.zeros(1, dtype=torch.int32, **f)
+        self.ws = None
+
+
+_BUFS = {}
+
+
+def _buffers(P, nb, device):
+    key = (P, nb, str(device))
+    b = _BUFS.get(key)
+    if b is None:
+        _BUFS.clear()  # keep one set alive
+        b = _BUFS[key] = _Buffers(P, nb, device)
+    return b
+
+
+def direct_kernels(direct, shapes, rays_flat, bsdf, lights):
+    """Run intersect + shade on flat rays [P,6]; returns the buffer set (rgb zero on misses)."""
+    P = rays_flat.shape[0]
+    dev = rays_flat.device
+    nb = len(getattr(bsdf, "bsdfs", [bsdf]))
+    b = _buffers(P, nb, dev)
+    lib = _lib.load(require_device=True)
+    sh = sdf_handle(shapes.sdf)
+    ws_bytes = lib.nrt_intersect_workspace_bytes(sh, P)
+    if b.ws is None or b.ws.numel() < ws_bytes:
+        b.ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    primary = bool(direct.training)
+    scan_max_t = 0.0
+    if primary:
+        scan_max_t = getattr(shapes, "dist", 2.2) + random.random() * (2 / 128)
+    mp = _lib.MarchParams(int(shapes.max_steps), float(shapes.epsilon), 10.0, int(primary),
+                          float(scan_max_t), _lib.precision_code())
+    s = _lib.stream()
+    _lib.call("nrt_sdf_intersect", sh, _lib.ptr(rays_flat), P, ctypes.byref(mp), _lib.ptr(b.t),
+              _lib.ptr(b.hit), _lib.ptr(b.p), _lib.ptr(b.n), _lib.ptr(b.raw), _lib.ptr(b.wi),
+              _lib.ptr(b.thr) if primary else None, _lib.ptr(b.hit_idx), _lib.ptr(b.hit_count),
+              _lib.ptr(b.ws), s)
+    if not primary:
+        b.thr.zero_()
+    b.rgb.zero_()
+    _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), _lib.ptr(b.p),
+              _lib.ptr(b.n), _lib.ptr(b.wi), _lib.ptr(b.hit_idx), _lib.ptr(b.hit_count), P,
+              _lib.ptr(b.rgb), None, _lib.precision_code(), s)
+    return b
+
+
+def composite(b, N, W, H, with_alpha, background, out, X0, Y0):
+    """Write the tile into out[N, IW, IH, C] (main.py:85-90): Direct fills misses with the
+    background, NeRFIntegrator appends sigmoid(throughput) and never fills."""
+    _lib.call("nrt_composite", _lib.ptr(b.rgb), _lib.ptr(b.thr), _lib.ptr(b.hit), N, W, H,
+              int(with_alpha), int(not with_alpha), float(background), _lib.ptr(out),
+              out.shape[1], out.shape[2], out.shape[3], int(X0), int(Y0), _lib.stream())
+
+
+def render_tile(fused, shapes, lights, cameras, bsdf, out, x0, y0, chunk, size, with_noise,
+                background, ox=0, oy=0):
+    direct, with_alpha = fused
+    rays = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise)
+    N = rays.shape[0]
+    b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights)
+    composite(b, N, chunk, chunk, with_alpha, background, out, x0 - ox, y0 - oy)
+    return b
+
+
+def row_shard(size, rank, world, tile_rows=16):
+    """Image rows of `rank` when tiles of `tile_rows` rows are dealt round-robin."""
+    rows = []
+    for t0 in range(rank * tile_rows, size, world * tile_rows):
+        rows.extend(range(t0, min(t0 + tile_rows, size)))
+    return rows
+
+
+class RowRenderer:
+    """Renders a fixed set of rows of every camera of a NeRF/DTU camera batch.
+
+    ``positions`` ([R, size, 2], u = column, v = row) are built once; each ``render`` call is
+    raygen + intersect + shade + composite into ``self.image`` [N, R, size, C].
+    """
+
+    def __init__(self, shapes, lights, cameras, integrator, bsdf, size, rows, background=0.0,
+                 with_noise=1e-3, device="cuda"):
+        fused = fused_integrator(integrator)
+        if fused is None:
+            raise _lib.NrtError("RowRenderer supports Direct and NeRFIntegrator(Direct)")
+        self.fused = fused
+        self.shapes, self.lights, self.cameras, self.bsdf = shapes, lights, cameras, bsdf
+        self.size = size
+        self.rows = list(rows)
+        self.background = background
+        self.with_noise = with_noise
+        R = len(self.rows)
+        v = torch.tensor(self.rows, dtype=torch.float32, device=device)[:, None].expand(R, size)
+        u = torch.arange(size, dtype=torch.float32, device=device)[None, :].expand(R, size)
+        self.positions = torch.stack([u, v], dim=-1).contiguous()
+        dims = 4 if fused[1] else 3
+        self.image = torch.empty(len(cameras), R, size, dims, device=device)
+
+    def render(self):
+        direct, with_alpha = self.fused
+        R = len(self.rows)
+        rays = self.cameras.rays_tile(0, 0, R, self.size, self.size, self.with_noise,
+                                      positions=self.positions)
+        N = rays.shape[0]
+        b = direct_kernels(direct, self.shapes, rays.reshape(-1, 6), self.bsdf, self.lights)
+        composite(b, N, R, self.size, with_alpha, self.background, self.image, 0, 0)
+        return self.image

@@ -1,0 +1,188 @@
+"""SDF shapes (shapes/sdfs.py): the sphere-tracing march, the 128-step coarse scan and the
+normals run in ``nrt_sdf_intersect``; ``SphereSDF`` / ``SkipConnMLP`` SDFs evaluate in
+``nrt_sdf_eval``.  SDF callables the library does not recognise raise ``NrtError``."""
+import ctypes
+import random
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ... import _lib
+from .._handles import _Handle, _cache, _host, mlp_handle
+from ..interaction import MixedInteraction
+from ..neural_blocks import SkipConnMLP
+
+
+def SPHERE_SDF(p):
+    """Default unit sphere SDF (sdfs.py:13)."""
+    return torch.norm(p, dim=-1) - 1
+
+
+class SphereSDF(nn.Module):
+    """Spheres smooth-min-ed together plus a residual MLP (sdfs.py:16-44)."""
+
+    def __init__(self, n=2 << 6, device="cuda"):
+        super().__init__()
+        self.centers = nn.Parameter(0.3 * torch.rand(n, 3, device=device, requires_grad=True) - 0.15)
+        self.radii = nn.Parameter(0.2 * torch.rand(n, device=device, requires_grad=True) - 0.1)
+        self.tfs = nn.Parameter(torch.zeros(n, 3, 3, device=device, requires_grad=True))
+        self.shift = SkipConnMLP(num_layers=8, hidden_size=128, in_size=3, out=1, device=device,
+                                 freqs=32, activation=F.softplus, zero_init=True).to(device)
+
+    def set_center(self, at):
+        self.centers = nn.Parameter(at.expand_as(self.centers).clone().detach())
+
+    def transform(self, p):
+        tfs = self.tfs + torch.eye(3, device=p.device).unsqueeze(0)
+        return torch.einsum("ijk,ibk->ibj", tfs, p.expand(tfs.shape[0], -1, -1))
+
+    def forward(self, p):
+        return sdf_eval(self, p)
+
+
+_UNIT = {}
+
+
+def sdf_handle(sdf):
+    """nrt_sdf for a recognised SDF callable."""
+    if sdf is SPHERE_SDF:
+        if "h" not in _UNIT:
+            lib = _lib.load()
+            out = ctypes.c_void_p()
+            _lib.check(lib.nrt_sdf_create_unit_sphere(ctypes.byref(out)), "nrt_sdf_create_unit_sphere")
+            _UNIT["h"] = _Handle(out, "nrt_sdf_destroy")
+        return _UNIT["h"].value
+    if isinstance(sdf, SkipConnMLP):
+        mh = mlp_handle(sdf)
+        params = [sdf.basis_p] + list(sdf.parameters())
+
+        def build():
+            out = ctypes.c_void_p()
+            _lib.check(_lib.load().nrt_sdf_create_mlp(mh.value, ctypes.byref(out)), "nrt_sdf_create_mlp")
+            return _Handle(out, "nrt_sdf_destroy", [mh])
+        return _cache(sdf, [*params, torch.empty(0)], build).value
+    if isinstance(sdf, SphereSDF) or _looks_like_sphere_sdf(sdf):
+        shift = getattr(sdf, "shift", None)
+        mh = mlp_handle(shift) if shift is not None else None
+        params = [sdf.centers, sdf.radii, sdf.tfs] + ([shift.basis_p] + list(shift.parameters()) if shift is not None else [])
+
+        def build():
+            c, r, t = _host(sdf.centers), _host(sdf.radii), _host(sdf.tfs)
+            out = ctypes.c_void_p()
+            _lib.check(_lib.load().nrt_sdf_create_sphere_blob(
+                c.shape[0], c.data_ptr(), r.data_ptr(), t.data_ptr(), 32.0,
+                mh.value if mh is not None else None, ctypes.byref(out)), "nrt_sdf_create_sphere_blob")
+            return _Handle(out, "nrt_sdf_destroy", [mh] if mh is not None else [])
+        return _cache(sdf, params, build).value
+    raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP implementation "
+                        "(supported: SPHERE_SDF, SphereSDF, SkipConnMLP)")
+
+
+def _looks_like_sphere_sdf(m):
+    return all(hasattr(m, a) for a in ("centers", "radii", "tfs", "shift"))
+
+
+def sdf_eval(sdf, p):
+    flat = p.reshape(-1, 3).float().contiguous()
+    out = torch.empty(flat.shape[0], device=p.device)
+    _lib.call("nrt_sdf_eval", sdf_handle(sdf), _lib.ptr(flat), flat.shape[0], _lib.ptr(out),
+              _lib.precision_code(), _lib.stream())
+    return out.reshape(p.shape[:-1])
+
+
+class HipInteraction(MixedInteraction):
+    """MixedInteraction produced by nrt_sdf_intersect.  ``raw_normals`` (the un-normalised
+    gradients of the hit points, in hit-mask order, sdfs.py:154-155) is materialised on
+    first access; it is None when nothing was hit, like the reference's missing attribute."""
+
+    @property
+    def raw_normals(self):
+        if not hasattr(self, "_nrt_raw"):
+            return None
+        hit = self._nrt_hit_mask.reshape(-1)
+        if not bool(hit.any()):
+            return None
+        return self._nrt_raw[hit]
+
+
+class SDF:
+    """A general SDF shape with sphere-tracing intersection (sdfs.py:89-277)."""
+
+    def __init__(self, device="cuda", sdf=SPHERE_SDF, epsilon=1e-3, max_steps=32, dist=2.2,
+                 **kwargs):
+        self.device = torch.device(device)
+        self.sdf = sdf
+        self.epsilon = epsilon
+        self.max_steps = max_steps
+        self.dist = dist
+
+    def __len__(self):
+        return 1
+
+    def parameters(self):
+        return self.sdf.parameters()
+
+    def intersect(self, rays, max_t=10, active=True, primary: bool = True):
+        """sdfs.py:111-160 on the HIP path.  ``primary`` draws ``random.random()`` for the
+        coarse-scan jitter exactly like SDF.throughput (sdfs.py:236)."""
+        dev = rays.device
+        lead = rays.shape[:-1]
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        h = sdf_handle(self.sdf)
+        t = torch.empty(P, device=dev)
+        hit = torch.empty(P, dtype=torch.uint8, device=dev)
+        p = torch.empty(P, 3, device=dev)
+        n = torch.empty(P, 3, device=dev)
+        raw = torch.empty(P, 3, device=dev)
+        wi = torch.empty(P, 3, device=dev)
+        thr = torch.empty(P, device=dev) if primary else None
+        hit_idx = torch.empty(max(P, 1), dtype=torch.int32, device=dev)
+        hit_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        lib = _lib.load(require_device=True)
+        ws_bytes = lib.nrt_intersect_workspace_bytes(h, P)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        scan_max_t = 0.0
+        if primary:
+            dist = getattr(self, "dist", 2.2)
+            scan_max_t = dist + random.random() * (2 / 128)
+        mp = _lib.MarchParams(int(self.max_steps), float(self.epsilon), float(max_t), int(bool(primary)),
+                              float(scan_max_t), _lib.precision_code())
+        _lib.call("nrt_sdf_intersect", h, _lib.ptr(flat), P, ctypes.byref(mp), _lib.ptr(t),
+                  _lib.ptr(hit), _lib.ptr(p), _lib.ptr(n), _lib.ptr(raw), _lib.ptr(wi),
+                  _lib.ptr(thr), _lib.ptr(hit_idx), _lib.ptr(hit_count), _lib.ptr(ws), _lib.stream())
+        hit_b = hit.bool().reshape(lead)
+        throughput = thr.reshape(lead) if primary else 0
+        si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead).squeeze(), obj=self,
+                            throughput=throughput)
+        si.n = n.reshape(lead + (3,))
+        frame = torch.empty(P, 9, device=dev)
+        _lib.call("nrt_frames", None, _lib.ptr(n), P, _lib.ptr(frame), None, _lib.stream())
+        si.frame = frame.reshape(lead + (3, 3))
+        si.wi = wi.reshape(lead + (3,))
+        si._nrt_hits = (hit_idx, hit_count, flat)
+        si._nrt_raw = raw
+        si._nrt_hit_mask = hit_b
+        return si, hit_b
+
+    def intersect_test(self, rays, max_t=10, active=True):
+        """sdfs.py:162-181 via nrt_sdf_occlusion."""
+        lead = rays.shape[:-1]
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        mt = torch.as_tensor(max_t, dtype=torch.float32, device=rays.device)
+        mt = mt.expand(lead + (1,)).reshape(P).contiguous() if mt.dim() > 0 else mt.expand(P).contiguous()
+        vis = torch.empty(P, dtype=torch.uint8, device=rays.device)
+        _lib.call("nrt_sdf_occlusion", sdf_handle(self.sdf), _lib.ptr(flat), P, _lib.ptr(mt),
+                  int(self.max_steps), float(self.epsilon), _lib.ptr(vis), _lib.precision_code(),
+                  _lib.stream())
+        return vis.bool().reshape(lead)
+
+    def autograd_diff(self, p):
+        """Normal direction d sdf / dp (sdfs.py:184-197) from the f32 backward kernel."""
+        flat = p.reshape(-1, 3).float().contiguous()
+        g = torch.empty_like(flat)
+        _lib.call("nrt_sdf_grad", sdf_handle(self.sdf), _lib.ptr(flat), flat.shape[0], _lib.ptr(g),
+                  _lib.stream())
+        return g.reshape(p.shape)

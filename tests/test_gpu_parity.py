@@ -1,0 +1,288 @@
+"""HIP path vs the CPU oracle (FP32 parity bar 1e-4 abs; FP16 judged by relative error/PSNR)."""
+import math
+import random
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import pathtracer_ref as R
+from oracle import recipes
+from tests.helpers import copy_mlp, product_mlp_like, seeded
+
+pytestmark = pytest.mark.gpu
+
+MLP_CASES = [
+    # name, ctor kwargs, activation, init
+    ("sdf_8x256_softplus", dict(num_layers=8, hidden_size=256, out=1, freqs=16), "softplus", None),
+    ("neural_bsdf_6x96", dict(num_layers=6, hidden_size=96, out=3, freqs=64), "leaky_relu", None),
+    ("light_field_10x256", dict(num_layers=10, hidden_size=256, out=3, freqs=16), "leaky_relu", None),
+    ("sp_var_16x256", dict(num_layers=16, hidden_size=256, out=8, freqs=128, sigma=128,
+                           xavier_init=True), "leaky_relu", None),
+    ("shift_8x128", dict(num_layers=8, hidden_size=128, out=1, freqs=32), "softplus", None),
+    ("nerfle_first_5x128", dict(num_layers=5, hidden_size=128, out=65, freqs=16), "leaky_relu", None),
+    ("default_8x64", dict(num_layers=8, hidden_size=64, out=3, freqs=16), "leaky_relu", None),
+    ("plain_nerf_latent", dict(num_layers=5, hidden_size=32, out=33, latent_size=32), "leaky_relu", None),
+]
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    yield
+    set_precision("fp32")
+
+
+@pytest.mark.parametrize("name,kw,act,_", MLP_CASES, ids=[c[0] for c in MLP_CASES])
+@pytest.mark.parametrize("M", [1, 31, 1000])
+def test_mlp_forward_fp32(name, kw, act, _, M):
+    seeded(1)
+    ref = R.SkipMLP(activation=act, **kw)
+    mine = product_mlp_like(ref, act)
+    x = torch.rand(M, 3) * 2 - 1
+    lat = torch.randn(M, kw["latent_size"]) if kw.get("latent_size") else None
+    with torch.no_grad():
+        want = ref(x, lat)
+        got = mine(x.cuda(), None if lat is None else lat.cuda()).cpu()
+    scale = max(1.0, want.abs().max().item())
+    assert (got - want).abs().max().item() <= 1e-4 * scale, (got - want).abs().max()
+
+
+@pytest.mark.parametrize("name,kw,act,_", MLP_CASES[:5], ids=[c[0] for c in MLP_CASES[:5]])
+def test_mlp_forward_fp16_close(name, kw, act, _):
+    from neural_raytracing_amd import set_precision
+    seeded(2)
+    ref = R.SkipMLP(activation=act, **kw)
+    mine = product_mlp_like(ref, act)
+    x = (torch.rand(4096, 3) * 2 - 1)
+    with torch.no_grad():
+        want = ref(x)
+        set_precision("fp16")
+        got = mine(x.cuda()).cpu()
+    err = (got - want).abs().max().item()
+    assert err <= 2e-2 * max(1.0, want.abs().max().item()), err
+
+
+def _blob_pair(n=32, shift_hidden=128, nonzero_shift=True):
+    from neural_raytracing_amd.pathtracer.shapes import SphereSDF
+    seeded(3)
+    ref = R.SphereBlobSDF(n=n, shift_hidden=shift_hidden, shift_zero_init=not nonzero_shift)
+    if nonzero_shift:
+        with torch.no_grad():
+            ref.shift.out.weight.mul_(0.05)
+    mine = SphereSDF(n=n, device="cpu")
+    if shift_hidden != 128:
+        raise ValueError
+    with torch.no_grad():
+        mine.centers.copy_(ref.centers)
+        mine.radii.copy_(ref.radii)
+        mine.tfs.copy_(ref.tfs + 0.05 * torch.randn_like(ref.tfs))
+        ref.tfs.copy_(mine.tfs)
+    copy_mlp(mine.shift, ref.shift)
+    return ref, mine.cuda()
+
+
+def test_sphere_sdf_eval_and_grad_fp32():
+    ref, mine = _blob_pair()
+    p = torch.rand(777, 3) - 0.5
+    with torch.no_grad():
+        want = ref(p)
+        got = mine(p.cuda()).cpu()
+    assert (got - want).abs().max().item() < 1e-5
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    g_ref = R.MarchedSDF(sdf=ref).gradient(p)
+    with torch.no_grad():
+        g = SDF(sdf=mine).autograd_diff(p.cuda()).cpu()
+    assert (g - g_ref).abs().max().item() < 1e-4
+
+
+def test_mlp_sdf_grad_fp32():
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    seeded(4)
+    ref = R.SkipMLP(num_layers=8, hidden_size=256, out=1, freqs=16, activation="softplus")
+    mine = product_mlp_like(ref, "softplus")
+    p = torch.rand(300, 3) - 0.5
+    g_ref = R.MarchedSDF(sdf=ref).gradient(p)
+    with torch.no_grad():
+        g = SDF(sdf=mine).autograd_diff(p.cuda()).cpu()
+    assert (g - g_ref).abs().max().item() < 1e-4 * max(1.0, g_ref.abs().max().item())
+
+
+def test_unit_sphere_intersect_kat():
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SPHERE_SDF
+    rays = torch.tensor([[0.0, 0.0, 1.5, 0.0, 0.0, -1.0],
+                         [0.3, 0.0, 1.5, 0.0, 0.0, -1.0],
+                         [0.0, 3.0, 1.5, 0.0, 0.0, -1.0]])
+    shape = SDF(sdf=SPHERE_SDF, max_steps=16)
+    with torch.no_grad():
+        it, hit = shape.intersect(rays.cuda(), primary=False)
+    ref_it, ref_hit = R.MarchedSDF(max_steps=16).intersect(rays, primary=False)
+    assert hit.cpu().tolist() == ref_hit.tolist() == [True, True, False]
+    assert torch.allclose(it.t.cpu(), ref_it.t, atol=1e-6)
+    assert torch.allclose(it.n.cpu(), ref_it.n, atol=1e-6)
+    assert torch.allclose(it.p.cpu(), ref_it.p, atol=1e-6)
+    assert torch.allclose(it.wi.cpu(), ref_it.wi, atol=1e-6)
+    assert torch.allclose(it.frame.cpu(), ref_it.frame, atol=1e-6)
+
+
+def test_blob_intersect_matches_oracle():
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    ref, mine = _blob_pair()
+    seeded(5)
+    o = torch.tensor([0.0, 0.0, 1.0]).expand(1, 48, 48, 1, 3)
+    d = F.normalize(torch.cat([torch.rand(1, 48, 48, 1, 2) * 0.6 - 0.3,
+                               -torch.ones(1, 48, 48, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    with torch.no_grad():
+        it, hit = SDF(sdf=mine, max_steps=32).intersect(rays.cuda(), primary=True)
+        rit, rhit = R.MarchedSDF(sdf=ref, max_steps=32).intersect(rays, primary=True,
+                                                                    jitter=_last_jitter())
+    agree = (hit.cpu() == rhit).reshape(-1)
+    assert agree.float().mean() > 0.99
+    m = agree & rhit.reshape(-1)
+    assert m.sum() > 100
+    assert (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max() < 1e-4
+    assert (it.n.cpu().reshape(-1, 3)[m] - rit.n.reshape(-1, 3)[m]).abs().max() < 1e-3
+    thr_diff = (it.throughput.cpu().reshape(-1) - rit.throughput.reshape(-1)).abs()
+    # the scan argmin can pick a different sample when two samples tie to ~1 ulp
+    assert (thr_diff < 1e-2).float().mean() > 0.99
+
+
+_JIT = {}
+
+
+def _last_jitter():
+    # the product drew random.random() once; replay the same draw for the oracle
+    random.seed(5)
+    return random.random()
+
+
+def _scene_pair(scene_fn=recipes.baseline_checksum_scene):
+    """Oracle scene and the product scene with identical weights (same seed, same order)."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, NeuralBSDF
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.lights import LightField
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    ref = scene_fn()
+    torch.manual_seed(0)
+    random.seed(0)
+    sphere = SphereSDF(n=128, device="cpu")
+    shape = SDF(sdf=sphere, device="cpu", max_steps=32)
+    bsdf = ComposeSpatialVarying([NeuralBSDF(activation=torch.nn.Softplus(), device="cpu")
+                                  for _ in range(8)], device="cpu")
+    lights = LightField(device="cpu")
+    integ = NeRFIntegrator(Direct())
+    # identical RNG order => identical weights; verify instead of assuming
+    assert torch.equal(sphere.centers, ref["shape"].sdf.centers)
+    assert torch.equal(bsdf.sp_var_fn.out.weight, ref["bsdf"].sp_var_fn.out.weight)
+    assert torch.equal(lights.light_field_approx.init.weight,
+                       ref["lights"].light_field_approx.init.weight)
+    sphere.cuda()
+    for b in bsdf.bsdfs:
+        b.mlp.cuda()
+    bsdf.sp_var_fn.cuda()
+    lights.cuda()
+    cam = pt.cameras.NeRFCamera(cam_to_world=ref["camera"].cam_to_world.cuda(),
+                                focal=ref["camera"].focal, device="cuda")
+    return ref, dict(shape=shape, bsdf=bsdf, lights=lights, integrator=integ, camera=cam)
+
+
+def test_render_matches_oracle_fp32():
+    """The BASELINE.md §2 scene (no camera jitter) rendered by both paths."""
+    import neural_raytracing_amd.pathtracer as pt
+    ref, mine = _scene_pair()
+    random.seed(11)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref["lights"], ref["camera"], ref["integrator"], ref["bsdf"],
+                        size=256, chunk_size=256, background=0.0, with_noise=0.0,
+                        crop=(96, 96, 64))
+    random.seed(11)
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"],
+                                     mine["integrator"], bsdf=mine["bsdf"], size=256,
+                                     chunk_size=256, bundle_size=1, crop_size=64, uv=(96, 96),
+                                     background=0, with_noise=0.0, device="cuda")
+    got = got.cpu()
+    assert got.shape == want.shape == (64, 64, 4)
+    diff = (got - want).abs()
+    assert diff.max().item() <= 1e-4, diff.max()
+
+
+def test_render_fp16_psnr():
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    ref, mine = _scene_pair()
+    random.seed(11)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref["lights"], ref["camera"], ref["integrator"], ref["bsdf"],
+                        size=256, chunk_size=256, background=0.0, with_noise=0.0,
+                        crop=(96, 96, 64))
+    random.seed(11)
+    set_precision("fp16")
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"],
+                                     mine["integrator"], bsdf=mine["bsdf"], size=256,
+                                     chunk_size=256, bundle_size=1, crop_size=64, uv=(96, 96),
+                                     background=0, with_noise=0.0, device="cuda")
+    mse = ((got.cpu().clamp(0, 1) - want.clamp(0, 1)) ** 2).mean()
+    psnr = -10 * math.log10(max(mse.item(), 1e-12))
+    assert psnr > 40, psnr
+
+
+def test_nerf_raygen_matches_oracle():
+    import neural_raytracing_amd.pathtracer as pt
+    c2w = recipes.look_at_c2w((0.3, 0.4, 0.866)).unsqueeze(0)
+    focal = recipes.nerf_focal(64)
+    ref = R.NeRFCameraRef(c2w, focal)
+    pos = R._tile_positions(8, 16, 32)
+    want = ref.sample_positions(pos, 64, 0.0)
+    got = pt.cameras.NeRFCamera(cam_to_world=c2w.cuda(), focal=focal).rays_tile(8, 16, 32, 32, 64)
+    assert torch.allclose(got.cpu(), want, atol=1e-6)
+
+
+def test_dtu_raygen_matches_oracle():
+    import neural_raytracing_amd.pathtracer as pt
+    K = torch.eye(4)
+    K[0, 0], K[1, 1], K[0, 2], K[1, 2], K[0, 1] = 2890.0, 2890.0, 800.0, 600.0, 0.3
+    pose = torch.eye(4)
+    pose[:3, :4] = recipes.look_at_c2w((0.0, 0.5, 0.866))
+    pose[:3, 1:3] *= -1  # DTU looks down +z
+    ref = R.DTUCameraRef(pose[None], K[None])
+    pos = R._tile_positions(0, 0, 16)
+    want = ref.sample_positions(pos, 64)
+    got = pt.cameras.DTUCamera(pose=pose[None].cuda(), intrinsic=K[None].cuda()).rays_tile(0, 0, 16, 16, 64)
+    assert torch.allclose(got.cpu(), want, atol=2e-6)
+
+
+def test_all_miss_tile_and_empty_batch():
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SPHERE_SDF
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    m = SkipConnMLP(device="cuda")
+    with torch.no_grad():
+        assert m(torch.empty(0, 3, device="cuda")).shape == (0, 3)
+        rays = torch.tensor([[0.0, 5.0, 1.5, 0.0, 0.0, -1.0]] * 70).cuda()
+        it, hit = SDF(sdf=SPHERE_SDF).intersect(rays, primary=False)
+    assert not hit.any()
+    assert (it.n == 0).all()
+
+
+def test_pathtrace_fused_tiles_match_oracle():
+    """Full-frame pathtrace (fused tile path, 4 tiles) vs the oracle's tile loop."""
+    import neural_raytracing_amd.pathtracer as pt
+    ref, mine = _scene_pair()
+    for integ_ref, integ in [(ref["integrator"], mine["integrator"]),
+                             (R.DirectRef(), mine["integrator"].sub_integrator)]:
+        random.seed(21)
+        with torch.no_grad():
+            want = R.render(ref["shape"], ref["lights"], ref["camera"], integ_ref, ref["bsdf"],
+                            size=64, chunk_size=32, background=0.25, with_noise=0.0)
+        random.seed(21)
+        with torch.no_grad():
+            got, _ = pt.pathtrace(mine["shape"], mine["lights"], mine["camera"], integ,
+                                  bsdf=mine["bsdf"], size=64, chunk_size=32, bundle_size=1,
+                                  background=0.25, with_noise=0.0)
+        assert got.shape == want.shape
+        assert (got.cpu() - want).abs().max().item() <= 1e-4
