@@ -136,7 +136,7 @@ def main():
 
     import neural_raytracing_amd as nra
     from neural_raytracing_amd import _lib
-    from neural_raytracing_amd.pathtracer.render import RowRenderer, row_shard
+    from neural_raytracing_amd.pathtracer.render import RowRenderer, gather_rows, row_shard
     _lib.load(require_device=True)
     nra.set_precision(args.precision)
 
@@ -149,22 +149,15 @@ def main():
     rows = row_shard(size, rank, world, args.tile_rows)
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
                      size, rows, background=0.0, with_noise=1e-3, device=device)
-    max_rows = max(len(row_shard(size, r, world, args.tile_rows)) for r in range(world))
-    gather_buf = torch.zeros(world, world, max_rows, size, 4, device=device)
     full = torch.zeros(world, size, size, 4, device=device)
+    rows_idx = torch.tensor(rows, dtype=torch.long, device=device)
 
     def step():
         img = rr.render()
         if world > 1:
-            import torch.distributed as dist
-            slab = torch.zeros(world, max_rows, size, 4, device=device)
-            slab[:, :len(rows)] = img
-            dist.all_gather_into_tensor(gather_buf.view(world * world, max_rows, size, 4), slab)
-            for r in range(world):
-                rws = row_shard(size, r, world, args.tile_rows)
-                full[:, rws] = gather_buf[r, :, :len(rws)]
+            gather_rows(img, size, rank, world, args.tile_rows, out=full)
         else:
-            full[:, rows] = img
+            full.index_copy_(1, rows_idx, img)
         return full
 
     with torch.no_grad():

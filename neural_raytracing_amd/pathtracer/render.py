@@ -147,3 +147,26 @@ class RowRenderer:
         b = direct_kernels(direct, self.shapes, rays.reshape(-1, 6), self.bsdf, self.lights)
         composite(b, N, R, self.size, with_alpha, self.background, self.image, 0, 0)
         return self.image
+
+
+def gather_rows(local, size, rank, world, tile_rows, out=None, group=None):
+    """All-gather every rank's row slab ([N, R_rank, W, C]) and assemble [N, size, W, C].
+
+    One ``all_gather_into_tensor`` of equal-sized (padded) slabs -- the only collective of the
+    multi-GPU path (RCCL over xGMI on the box, gloo in the CPU tests).
+    """
+    import torch.distributed as dist
+    shards = [row_shard(size, r, world, tile_rows) for r in range(world)]
+    max_rows = max(len(s) for s in shards)
+    N, R, W, C = local.shape
+    slab = local.new_zeros(N, max_rows, W, C)
+    slab[:, :R] = local
+    buf = local.new_empty(world * N, max_rows, W, C)
+    dist.all_gather_into_tensor(buf, slab, group=group)
+    buf = buf.view(world, N, max_rows, W, C)
+    if out is None:
+        out = local.new_empty(N, size, W, C)
+    for r, rows in enumerate(shards):
+        idx = torch.tensor(rows, device=local.device, dtype=torch.long)
+        out.index_copy_(1, idx, buf[r, :, :len(rows)])
+    return out

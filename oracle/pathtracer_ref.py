@@ -655,6 +655,8 @@ def render(shape, lights, camera, integrator, bsdf, size, chunk_size, background
     """
     n_cam = len(camera)
     dims = integrator.dims()
+    # main.py:54 / :133 assert before pathtrace_sample clamps the chunk to the crop (:135)
+    assert size % chunk_size == 0
     if crop is None:
         u0, v0, extent = 0, 0, size
     else:
@@ -662,7 +664,6 @@ def render(shape, lights, camera, integrator, bsdf, size, chunk_size, background
         u0 = max(min(u0, size - extent), 0)
         v0 = max(min(v0, size - extent), 0)
         chunk_size = min(chunk_size, extent)
-    assert size % chunk_size == 0
     out = torch.full([n_cam, extent, extent, dims], float(background))
     xs = list(range(u0, u0 + extent, chunk_size))
     ys = list(range(v0, v0 + extent, chunk_size))
