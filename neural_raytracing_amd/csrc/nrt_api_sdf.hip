@@ -188,7 +188,31 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
   dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
   int rc0 = NRT_OK;
-  {
+  // FP16 SDF MLPs of width 128/256 with F = 16/32 run the block-cooperative ring kernel
+  const int ne = s->mlp ? s->mlp->host_dev.ke / 16 : 0;
+  const bool ring16 = f16 && s->mlp && (s->host_dev.nb == 8 || s->host_dev.nb == 4) &&
+                      (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&
+                      s->mlp->desc.skip == 3 && s->mlp->desc.out <= 32 &&
+                      std::getenv("NRT_NO_RING") == nullptr;
+  if (ring16) {
+    ProfScope prof("k_intersect", st);
+    constexpr int WV = 8;
+    const bool fold = s->mlp->host_dev.fold != 0;
+    const size_t bias_bytes = (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
+    dim3 g(ceil_div64(P, 32 * WV)), b(64 * WV);
+#define NRT_RING_LAUNCH(NBV, NEV, FOLDV)                                                        \
+    {                                                                                          \
+      auto kern = k_march16<NBV, NEV, WV, FOLDV>;                                              \
+      const size_t lds = ring::Cfg<NBV, NEV, WV>::RING_BYTES + bias_bytes;                     \
+      if (!(rc0 = set_lds(kern, lds)))                                                         \
+        kern<<<g, b, lds, st>>>(s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt); \
+    }
+    if (s->host_dev.nb == 8 && ne == 3) { if (fold) NRT_RING_LAUNCH(8, 3, true) else NRT_RING_LAUNCH(8, 3, false) }
+    else if (s->host_dev.nb == 8) { if (fold) NRT_RING_LAUNCH(8, 5, true) else NRT_RING_LAUNCH(8, 5, false) }
+    else if (ne == 3) { if (fold) NRT_RING_LAUNCH(4, 3, true) else NRT_RING_LAUNCH(4, 3, false) }
+    else { if (fold) NRT_RING_LAUNCH(4, 5, true) else NRT_RING_LAUNCH(4, 5, false) }
+#undef NRT_RING_LAUNCH
+  } else {
   ProfScope prof("k_intersect", st);
   NRT_NB_SWITCH(s->host_dev.nb, {
     if (f16) {

@@ -25,6 +25,10 @@ namespace nrt {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
+// address-space qualifiers: uniform tables through the scalar cache, streams as global loads
+#define NRT_GLOBAL __attribute__((address_space(1)))
+#define NRT_CONST __attribute__((address_space(4)))
+
 constexpr int kMaxLin = 20;  // init + up to 18 hidden + out
 
 enum { ACT_LEAKY = 0, ACT_SOFTPLUS = 1, ACT_NONE = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
@@ -47,6 +51,16 @@ struct MlpDev {
   const float* bias[kMaxLin];      // [rowblocks*32]
   const float* wout_row0;          // out.weight[0, :]  (gradient seed of an SDF head)
   int nbt[kMaxLin];                // row blocks of W^T (input positions / 32, rounded up)
+  // FP16 weight stream for the block-cooperative LDS-ring engine (row-block-major chunks):
+  // chunk (layer l, row block ib) = the nks(l) A fragments of that row block, contiguous.
+  // Softplus MLPs are folded into the log2 domain: z' = log2e * z, a' = log2(1 + 2^z'), so the
+  // init layer's W and every init/hidden bias carry a log2e factor and out.weight carries ln2.
+  const h8* stream16;              // [frags (+ zero tail)][64 lanes]
+  const int* chunk_off;            // first fragment of each chunk
+  int n_chunks;
+  const float* bias16;             // [layer][bias16_stride] (folded like stream16)
+  int bias16_stride;               // max(nb, ob) * 32
+  int fold;                        // 1 when softplus was folded
 };
 
 struct SdfDev {
@@ -468,4 +482,196 @@ __device__ __forceinline__ void mlp32_backward_out0(const MlpDev& m, const EncIn
   wave_lds_fence();
 }
 
+}  // namespace nrt
+
+// ------------------------------------------------------------------------------------------
+// FP16 block-cooperative engine: LDS weight ring shared by the WV waves of a block
+// ------------------------------------------------------------------------------------------
+// Every wave of the block evaluates the same MLP at the same time for its own 32 rays.  The
+// weight stream (MlpDev::stream16) is consumed chunk by chunk, one chunk = one 32-row output
+// block of one layer (row-block-outer order: only one accumulator tile is live, and the
+// activation of tile ib overlaps the MFMAs of tile ib+1).  Chunks are staged through a 3-slot
+// LDS ring: at chunk c a wave writes the fragments it loaded during chunk c-1 (chunk c+1) to
+// LDS, issues its global loads for chunk c+2 into registers, then runs chunk c's MFMAs with A
+// read by ds_read_b128 from LDS; one barrier per chunk.  Loads and stores are unconditional
+// (fixed count per wave; slots are padded) so hipcc never drains vmcnt inside the loop.
+namespace nrt {
+namespace ring {
+
+__device__ __forceinline__ float sp2(float x) {
+  // log2(1 + 2^x) = max(x, 0) + log2(1 + 2^-|x|): softplus in the log2 domain
+  return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_inff()) +
+         __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
+}
+
+template <int NB, int NE, int WV>
+struct Cfg {
+  static constexpr int MAXF = 2 * NB + NE;                // fragments in the largest chunk
+  static constexpr int MAXL = (MAXF + WV - 1) / WV;       // loads per wave per chunk
+  static constexpr int SLOTF = MAXL * WV;                 // fragments per ring slot
+  static constexpr int RING_BYTES = 3 * SLOTF * 1024;
+};
+
+template <int NB, int NE, int WV>
+struct Engine {
+  using C = Cfg<NB, NE, WV>;
+  h8* ring;                 // LDS [3][SLOTF][64]
+  const float* lbias;       // LDS copy of bias16
+  const NRT_GLOBAL h8* stream;
+  const NRT_CONST int* coff;
+  int nch;
+  int c;                    // chunk held in `slot`
+  int slot;
+  int lane, wv;
+  h8 stg[C::MAXL];          // chunk c+1, loaded, not yet written
+
+  __device__ __forceinline__ void load(int chunk) {
+    const int off = coff[chunk];
+#pragma unroll
+    for (int q = 0; q < C::MAXL; ++q) stg[q] = stream[(size_t)(off + wv + WV * q) * 64 + lane];
+  }
+  __device__ __forceinline__ void store(int s) {
+    h8* D = ring + s * C::SLOTF * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < C::MAXL; ++q) D[(wv + WV * q) * 64] = stg[q];
+  }
+  __device__ __forceinline__ int nxt(int x) const { return x + 1 == nch ? 0 : x + 1; }
+
+  // block-wide; afterwards slot 0 = chunk 0, stg = chunk 1
+  __device__ __forceinline__ void init(const MlpDev& m, char* lds) {
+    ring = reinterpret_cast<h8*>(lds);
+    float* lb = reinterpret_cast<float*>(lds + C::RING_BYTES);
+    const int nb16 = (m.n_hidden + 2) * m.bias16_stride;
+    const NRT_GLOBAL float* gb = (const NRT_GLOBAL float*)m.bias16;
+    for (int i = threadIdx.x; i < nb16; i += blockDim.x) lb[i] = gb[i];
+    lbias = lb;
+    bstride_ = m.bias16_stride;
+    stream = (const NRT_GLOBAL h8*)m.stream16;
+    coff = (const NRT_CONST int*)m.chunk_off;
+    nch = m.n_chunks;
+    lane = threadIdx.x & 63;
+    wv = threadIdx.x >> 6;
+    c = 0;
+    slot = 0;
+    load(0);
+    store(0);
+    load(nxt(0));
+    __syncthreads();
+  }
+  // start of chunk c: publish chunk c+1, prefetch chunk c+2; returns this lane's A base
+  __device__ __forceinline__ const h8* begin() {
+    const int s1 = slot == 2 ? 0 : slot + 1;
+    store(s1);
+    load(nxt(nxt(c)));
+    __builtin_amdgcn_sched_barrier(0);
+    return ring + slot * C::SLOTF * 64 + lane;
+  }
+  __device__ __forceinline__ void end() {
+    __syncthreads();
+    c = nxt(c);
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  __device__ __forceinline__ f16v bias_at(int layer, int ib, int h) const {
+    f16v v;
+    const float* b = lbias + layer * bstride_ + 32 * ib + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 q = *reinterpret_cast<const float4*>(b + 8 * g);
+      v[4 * g + 0] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+    }
+    return v;
+  }
+  int bstride_;
+};
+
+// schedule of one chunk's dependent MFMA chain: keep two A reads in flight ahead of the MFMAs
+// (hipcc otherwise hoists all of a chunk's ds_reads and runs out of registers)
+template <int K>
+__device__ __forceinline__ void chain_schedule() {
+  __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+  for (int s = 0; s < K - 2; ++s) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+  }
+  __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+}
+
+template <bool FOLD>
+__device__ __forceinline__ void act_pack1(const f16v& acc, h8& lo, h8& hi, int act) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = acc[j], b = acc[8 + j];
+    if (FOLD) { a = sp2(a); b = sp2(b); }
+    else { a = act_fwd<true>(a, act); b = act_fwd<true>(b, act); }
+    lo[j] = (_Float16)a;
+    hi[j] = (_Float16)b;
+  }
+}
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 32 rays through the ring; L hidden
+// layers and skip period SK are compile-time so the whole evaluation is straight-line code.
+// Every wave of the block must call it the same number of times.
+template <int NB, int NE, int WV, bool FOLD, int L, int SK>
+__device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, const EncIn& e) {
+  const int h = E.lane >> 5;
+  const float kLog2e = 1.4426950408889634f;
+  // encoding fragments, raw (init) and activated (skip inputs)
+  h8 eraw[NE], eact[NE];
+#pragma unroll
+  for (int s = 0; s < NE; ++s) {
+    const int base = 16 * s + 8 * h;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      float a, b;
+      enc_pair<true>(m, e, base + 2 * jj, a, b);
+      eraw[s][2 * jj] = (_Float16)a;
+      eraw[s][2 * jj + 1] = (_Float16)b;
+      if (FOLD) { a = sp2(a * kLog2e); b = sp2(b * kLog2e); }
+      else { a = act_fwd<true>(a, m.act); b = act_fwd<true>(b, m.act); }
+      eact[s][2 * jj] = (_Float16)a;
+      eact[s][2 * jj + 1] = (_Float16)b;
+    }
+  }
+  h8 hv[2][2 * NB];
+  // init layer: NB chunks over the raw encoding
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) {
+    const h8* A = E.begin();
+    f16v acc = E.bias_at(0, ib, h);
+#pragma unroll
+    for (int s = 0; s < NE; ++s) acc = mfma16(A[s * 64], eraw[s], acc);
+    act_pack1<FOLD>(acc, hv[0][2 * ib], hv[0][2 * ib + 1], m.act);
+    E.end();
+  }
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int src = i & 1, dst = src ^ 1;
+    constexpr int dummy = 0;
+    (void)dummy;
+    const bool skip = (i != L - 1) && (i % SK) == 0;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) {
+      const h8* A = E.begin();
+      f16v acc = E.bias_at(1 + i, ib, h);
+#pragma unroll
+      for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[src][s], acc);
+      if (skip) {
+#pragma unroll
+        for (int s = 0; s < NE; ++s) acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
+      }
+      act_pack1<FOLD>(acc, hv[dst][2 * ib], hv[dst][2 * ib + 1], m.act);
+      E.end();
+    }
+  }
+  // out layer (one 32-row block; output row 0 sits in register 0 of the h == 0 lanes)
+  const h8* A = E.begin();
+  f16v acc = E.bias_at(L + 1, 0, h);
+#pragma unroll
+  for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[L & 1][s], acc);
+  E.end();
+  return __shfl(acc[0], E.lane & 31);
+}
+
+}  // namespace ring
 }  // namespace nrt

@@ -343,6 +343,94 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
   }
 }
 
+// FP16 block-cooperative march + scan: the WV waves of a block step through their SDF
+// evaluations together (the LDS weight ring needs every wave at the same chunk), so the march
+// phase ends when no ray of the block is marching.  Results are identical to k_intersect's.
+template <int NB, int NE, int WV, bool FOLD>
+__global__ void __launch_bounds__(64 * WV, 2) k_march16(
+    const SdfDev s, const MlpDev m, const float* __restrict__ rays, int64_t P, MarchArgs a,
+    float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
+    float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,
+    int32_t* __restrict__ hit_idx, int32_t* __restrict__ hit_count) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  ring::Engine<NB, NE, WV> E;
+  E.init(m, smem_c);
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t ray = ((int64_t)blockIdx.x * WV + (threadIdx.x >> 6)) * 32 + r;
+  const bool valid = ray < P;
+  const int64_t rr = valid ? ray : P - 1;
+  const float ox = rays[rr * 6], oy = rays[rr * 6 + 1], oz = rays[rr * 6 + 2];
+  const float dx = rays[rr * 6 + 3], dy = rays[rr * 6 + 4], dz = rays[rr * 6 + 5];
+  float t = 0.f;
+  bool live = valid, hit = false;
+  int i = 0, j = -2, idx = 0;
+  float best = 0.f, thr = 0.f;
+  for (;;) {
+    if (j == -2) {
+      const bool any = __syncthreads_or(live ? 1 : 0) != 0;
+      if (i >= a.max_steps || !any) {
+        if (!a.primary) break;
+        j = -1;
+      } else {
+        live = live && (t < a.max_t);
+      }
+    }
+    float px, py, pz;
+    if (j == -2) {
+      px = __fadd_rn(ox, __fmul_rn(dx, t));
+      py = __fadd_rn(oy, __fmul_rn(dy, t));
+      pz = __fadd_rn(oz, __fmul_rn(dz, t));
+    } else if (j == -1) {
+      px = ox; py = oy; pz = oz;
+    } else {
+      float ts = (j < 128) ? (float)(a.step * (double)(j + 1)) : __fmul_rn((float)idx, (float)a.step);
+      px = __fadd_rn(ox, __fmul_rn(ts, dx));
+      py = __fadd_rn(oy, __fmul_rn(ts, dy));
+      pz = __fadd_rn(oz, __fmul_rn(ts, dz));
+    }
+    float d = (s.kind == 2) ? spheres_value<true>(s, px, py, pz) : 0.f;
+    EncIn e;
+    e.x[0] = px; e.x[1] = py; e.x[2] = pz; e.x[3] = 0.f;
+    e.xg = nullptr; e.lat = nullptr;
+    d += ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, e);
+    if (j == -2) {
+      const bool now = live && (d <= a.eps);
+      hit = hit || now;
+      live = live && !now;
+      if (live) t = t + d;
+      ++i;
+    } else if (j == -1) {
+      best = d;
+      ++j;
+    } else if (j < 128) {
+      if (d < best) idx = j + 1;
+      best = fminf(best, d);
+      ++j;
+    } else {
+      thr = -1000.f * d;
+      break;
+    }
+  }
+  if (valid && lane < 32) {
+    t_out[ray] = t;
+    hit_out[ray] = hit ? 1 : 0;
+    p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
+    p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
+    p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
+    n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
+    if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+    if (a.primary) thr_out[ray] = thr;
+  }
+  if (hit_idx) {
+    const uint64_t mk = __ballot(valid && hit && lane < 32);
+    const int cnt = __popcll(mk);
+    int base = 0;
+    if (lane == 0 && cnt) base = atomicAdd(hit_count, cnt);
+    base = __shfl(base, 0);
+    if (valid && hit && lane < 32) hit_idx[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
+  }
+}
+
 // shading frame of n (0 on misses) and wi = to_local(frame, -d)
 __device__ __forceinline__ void make_frame(float nx, float ny, float nz, float f[9]) {
   // coordinate_system, interaction.py:9-27; f = [s | t | n] as columns: f[3*row + col]

@@ -11,6 +11,7 @@
 //   position 2s + hf.  W^T fragments (FP32 backward) swap the roles of rows and positions.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -173,6 +174,42 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   }
   size_t off_w0 = blob.add(layers.back().W, sizeof(float) * H);  // out.weight[0, :]
 
+  // ---- FP16 row-block-major weight stream (LDS-ring engine)
+  const bool fold = d->activation == NRT_ACT_SOFTPLUS;
+  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  std::vector<_Float16> stream;
+  std::vector<int> chunk_off;
+  const int bstride = std::max(NB, OB) * 32;
+  std::vector<float> bias16(layers.size() * (size_t)bstride, 0.f);
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& ly = layers[l];
+    const bool is_init = (l == 0), is_out = (l + 1 == layers.size());
+    const float wscale = fold ? (is_init ? kLog2e : (is_out ? kLn2 : 1.f)) : 1.f;
+    const float bscale = fold && !is_out ? kLog2e : 1.f;
+    const int nrb = (ly.R + 31) / 32;
+    const int ks_h = ly.hidden_in ? 2 * NB : 0;
+    const int ks_e = ly.enc_in ? ke / 16 : 0;
+    for (int ib = 0; ib < nrb; ++ib) {
+      chunk_off.push_back((int)(stream.size() / (64 * 8)));
+      for (int s2 = 0; s2 < ks_h + ks_e; ++s2)
+        for (int lane = 0; lane < 64; ++lane) {
+          int i = lane & 31, hf = lane >> 5;
+          for (int j = 0; j < 8; ++j) {
+            int col;
+            if (s2 < ks_h) col = col_of_hidden(32 * (s2 >> 1) + 16 * (s2 & 1) + 8 * (j >> 2) + 4 * hf + (j & 3));
+            else col = col_of_slot(ly, 16 * (s2 - ks_h) + 8 * hf + j);
+            stream.push_back((_Float16)(wscale * wval(ly, 32 * ib + i, col)));
+          }
+        }
+    }
+    for (int r = 0; r < ly.R; ++r) bias16[l * bstride + r] = bscale * ly.b[r];
+  }
+  const int n_chunks = (int)chunk_off.size();
+  stream.resize(stream.size() + (size_t)64 * 64 * 8, (_Float16)0.f);  // tail for unguarded prefetch
+  size_t off_stream = blob.add(stream.data(), stream.size() * sizeof(_Float16));
+  size_t off_coff = blob.add(chunk_off.data(), chunk_off.size() * sizeof(int));
+  size_t off_b16 = blob.add(bias16.data(), bias16.size() * sizeof(float));
+
   std::unique_ptr<nrt_mlp> m(new nrt_mlp());
   m->desc = *d;
   m->blob_bytes = blob.bytes.size();
@@ -187,6 +224,12 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
     md.bias[l] = reinterpret_cast<const float*>(base + offb[l]);
   }
   md.wout_row0 = reinterpret_cast<const float*>(base + off_w0);
+  md.stream16 = reinterpret_cast<const h8*>(base + off_stream);
+  md.chunk_off = reinterpret_cast<const int*>(base + off_coff);
+  md.n_chunks = n_chunks;
+  md.bias16 = reinterpret_cast<const float*>(base + off_b16);
+  md.bias16_stride = bstride;
+  md.fold = fold ? 1 : 0;
   m->host_dev = md;
   NRT_HIP(hipMalloc(&m->dev, sizeof(MlpDev)));
   NRT_HIP(hipMemcpy(m->dev, &md, sizeof(MlpDev), hipMemcpyHostToDevice));

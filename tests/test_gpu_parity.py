@@ -286,3 +286,45 @@ def test_pathtrace_fused_tiles_match_oracle():
                                   background=0.25, with_noise=0.0)
         assert got.shape == want.shape
         assert (got.cpu() - want).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("hidden,freqs", [(256, 16), (128, 32)])
+def test_ring_fp16_intersect_matches_oracle(hidden, freqs):
+    """The block-cooperative FP16 kernel (LDS weight ring, log2-folded softplus) vs the oracle."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    seeded(7)
+    ref = R.SphereBlobSDF(n=1, shift_hidden=hidden, shift_freqs=freqs, shift_zero_init=False)
+    with torch.no_grad():
+        ref.centers.zero_()
+        ref.radii.fill_(0.25)
+        ref.shift.out.weight.mul_(0.1)
+        ref.shift.out.bias.mul_(0.1)
+    mine = SphereSDF(n=1, device="cpu")
+    mine.shift = SkipConnMLP(num_layers=8, hidden_size=hidden, in_size=3, out=1, freqs=freqs,
+                             activation=F.softplus, device="cpu")
+    with torch.no_grad():
+        mine.centers.copy_(ref.centers)
+        mine.radii.copy_(ref.radii)
+    copy_mlp(mine.shift, ref.shift)
+    mine = mine.cuda()
+    o = torch.tensor([0.0, 0.2, 1.0]).expand(1, 40, 40, 1, 3)
+    d = F.normalize(torch.cat([torch.rand(1, 40, 40, 1, 2) * 0.7 - 0.35,
+                               -torch.ones(1, 40, 40, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    set_precision("fp16")
+    random.seed(9)
+    with torch.no_grad():
+        it, hit = SDF(sdf=mine, max_steps=48).intersect(rays.cuda(), primary=True)
+    random.seed(9)
+    jit = random.random()
+    with torch.no_grad():
+        rit, rhit = R.MarchedSDF(sdf=ref, max_steps=48).intersect(rays, primary=True, jitter=jit)
+    agree = (hit.cpu() == rhit).reshape(-1)
+    assert agree.float().mean() > 0.98, agree.float().mean()
+    m = agree & rhit.reshape(-1)
+    assert m.sum() > 200
+    assert (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max() < 2e-2
+    thr = (it.throughput.cpu().reshape(-1) - rit.throughput.reshape(-1)).abs()
+    assert (thr < 5.0).float().mean() > 0.95
