@@ -14,7 +14,7 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "nrt.h")
 # -ffp-contract=off: elementwise math rounds like the reference's eager torch ops (no silent FMA
 # contraction); MFMA and explicit fmaf() are unaffected.
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
-         "-Wno-unused-result"]
+         "-fno-slp-vectorize", "-Wno-unused-result"]
 OBJDIR = os.path.join(HERE, "build_obj")
 
 

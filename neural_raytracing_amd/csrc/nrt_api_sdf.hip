@@ -196,21 +196,29 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
                       std::getenv("NRT_NO_RING") == nullptr;
   if (ring16) {
     ProfScope prof("k_intersect", st);
-    constexpr int WV = 8;
+    const char* wv_env = std::getenv("NRT_RING_WAVES");
+    const int WVr = (wv_env && std::atoi(wv_env) == 4) ? 4 : 8;
     const bool fold = s->mlp->host_dev.fold != 0;
     const size_t bias_bytes = (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
-    dim3 g(ceil_div64(P, 32 * WV)), b(64 * WV);
-#define NRT_RING_LAUNCH(NBV, NEV, FOLDV)                                                        \
+#define NRT_RING_LAUNCH(NBV, NEV, WVV, FOLDV)                                                   \
     {                                                                                          \
-      auto kern = k_march16<NBV, NEV, WV, FOLDV>;                                              \
-      const size_t lds = ring::Cfg<NBV, NEV, WV>::RING_BYTES + bias_bytes;                     \
+      auto kern = k_march16<NBV, NEV, WVV, FOLDV>;                                             \
+      const size_t lds = ring::Cfg<NBV, NEV, WVV>::RING_BYTES + bias_bytes;                    \
+      dim3 g(ceil_div64(P, 32 * WVV)), b(64 * WVV);                                            \
       if (!(rc0 = set_lds(kern, lds)))                                                         \
-        kern<<<g, b, lds, st>>>(s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt); \
+        kern<<<g, b, lds, st>>>(s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, \
+                                throughput, idx, cnt);                                         \
     }
-    if (s->host_dev.nb == 8 && ne == 3) { if (fold) NRT_RING_LAUNCH(8, 3, true) else NRT_RING_LAUNCH(8, 3, false) }
-    else if (s->host_dev.nb == 8) { if (fold) NRT_RING_LAUNCH(8, 5, true) else NRT_RING_LAUNCH(8, 5, false) }
-    else if (ne == 3) { if (fold) NRT_RING_LAUNCH(4, 3, true) else NRT_RING_LAUNCH(4, 3, false) }
-    else { if (fold) NRT_RING_LAUNCH(4, 5, true) else NRT_RING_LAUNCH(4, 5, false) }
+#define NRT_RING_FOLD(NBV, NEV, WVV) \
+    { if (fold) NRT_RING_LAUNCH(NBV, NEV, WVV, true) else NRT_RING_LAUNCH(NBV, NEV, WVV, false) }
+    if (s->host_dev.nb == 8 && ne == 3) {
+      if (WVr == 4) NRT_RING_FOLD(8, 3, 4) else NRT_RING_FOLD(8, 3, 8)
+    } else if (s->host_dev.nb == 8) NRT_RING_FOLD(8, 5, 8)
+    else if (ne == 3) NRT_RING_FOLD(4, 3, 8)
+    else {
+      if (WVr == 4) NRT_RING_FOLD(4, 5, 4) else NRT_RING_FOLD(4, 5, 8)
+    }
+#undef NRT_RING_FOLD
 #undef NRT_RING_LAUNCH
   } else {
   ProfScope prof("k_intersect", st);

@@ -500,8 +500,9 @@ namespace ring {
 
 __device__ __forceinline__ float sp2(float x) {
   // log2(1 + 2^x) = max(x, 0) + log2(1 + 2^-|x|): softplus in the log2 domain
-  return __builtin_amdgcn_fmed3f(x, 0.f, __builtin_inff()) +
-         __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
+  // max(x, 0) as one v_max_i32 on the bit pattern (negative floats and -0 are negative ints)
+  const float pos = __int_as_float(max(__float_as_int(x), 0));
+  return pos + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
 }
 
 template <int NB, int NE, int WV>
@@ -517,7 +518,7 @@ struct Engine {
   using C = Cfg<NB, NE, WV>;
   h8* ring;                 // LDS [3][SLOTF][64]
   const float* lbias;       // LDS copy of bias16
-  const NRT_GLOBAL h8* stream;
+  __amdgpu_buffer_rsrc_t srd;  // FP16 weight stream
   const NRT_CONST int* coff;
   int nch;
   int c;                    // chunk held in `slot`
@@ -526,9 +527,13 @@ struct Engine {
   h8 stg[C::MAXL];          // chunk c+1, loaded, not yet written
 
   __device__ __forceinline__ void load(int chunk) {
-    const int off = coff[chunk];
+    // buffer_load_dwordx4 v, v[lane*16], s[rsrc], s[frag*1024]: no per-load VALU address math
+    const int off = coff[chunk] + wv;
 #pragma unroll
-    for (int q = 0; q < C::MAXL; ++q) stg[q] = stream[(size_t)(off + wv + WV * q) * 64 + lane];
+    for (int q = 0; q < C::MAXL; ++q) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(srd, lane * 16, (off + WV * q) * 1024, 0);
+      stg[q] = __builtin_bit_cast(h8, v);
+    }
   }
   __device__ __forceinline__ void store(int s) {
     h8* D = ring + s * C::SLOTF * 64 + lane;
@@ -546,11 +551,11 @@ struct Engine {
     for (int i = threadIdx.x; i < nb16; i += blockDim.x) lb[i] = gb[i];
     lbias = lb;
     bstride_ = m.bias16_stride;
-    stream = (const NRT_GLOBAL h8*)m.stream16;
+    srd = __builtin_amdgcn_make_buffer_rsrc((void*)m.stream16, 0, 0x7ffffff0, 0x00020000);
     coff = (const NRT_CONST int*)m.chunk_off;
     nch = m.n_chunks;
     lane = threadIdx.x & 63;
-    wv = threadIdx.x >> 6;
+    wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c = 0;
     slot = 0;
     load(0);
@@ -634,6 +639,11 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
     }
   }
   h8 hv[2][2 * NB];
+  // Software pipeline: the region of chunk k (between two barriers) holds chunk k's MFMA chain
+  // and the activation of chunk k-1's accumulator (`pend`), so the scheduler can put that VALU
+  // work into the MFMA gaps.  A pending tile that the current chain consumes (last row block of
+  // the previous layer, k-steps 2NB-2 / 2NB-1) is ordered by the register dependency.
+  f16v pend;
   // init layer: NB chunks over the raw encoding
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) {
@@ -641,32 +651,34 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
     f16v acc = E.bias_at(0, ib, h);
 #pragma unroll
     for (int s = 0; s < NE; ++s) acc = mfma16(A[s * 64], eraw[s], acc);
-    act_pack1<FOLD>(acc, hv[0][2 * ib], hv[0][2 * ib + 1], m.act);
+    if (ib > 0) act_pack1<FOLD>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act);
+    pend = acc;
     E.end();
   }
 #pragma unroll
   for (int i = 0; i < L; ++i) {
     const int src = i & 1, dst = src ^ 1;
-    constexpr int dummy = 0;
-    (void)dummy;
     const bool skip = (i != L - 1) && (i % SK) == 0;
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) {
       const h8* A = E.begin();
       f16v acc = E.bias_at(1 + i, ib, h);
+      if (ib == 0) act_pack1<FOLD>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act);
 #pragma unroll
       for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[src][s], acc);
       if (skip) {
 #pragma unroll
         for (int s = 0; s < NE; ++s) acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
       }
-      act_pack1<FOLD>(acc, hv[dst][2 * ib], hv[dst][2 * ib + 1], m.act);
+      if (ib > 0) act_pack1<FOLD>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act);
+      pend = acc;
       E.end();
     }
   }
   // out layer (one 32-row block; output row 0 sits in register 0 of the h == 0 lanes)
   const h8* A = E.begin();
   f16v acc = E.bias_at(L + 1, 0, h);
+  act_pack1<FOLD>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act);
 #pragma unroll
   for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[L & 1][s], acc);
   E.end();
