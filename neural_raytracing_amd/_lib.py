@@ -10,7 +10,8 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnrt_hip.so")
+# NRT_LIB: an alternative build of the same library (timing experiments, tools/exp_variants.sh)
+LIB_PATH = os.environ.get("NRT_LIB") or os.path.join(HERE, "libnrt_hip.so")
 
 NRT_FP32 = 0
 NRT_FP16 = 1

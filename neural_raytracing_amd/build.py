@@ -7,13 +7,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libnrt_hip.so")
 SOURCES = ["nrt_common.hip", "nrt_pack.hip", "nrt_api_mlp.hip", "nrt_api_sdf.hip",
-           "nrt_api_shade.hip", "nrt_api_cam.hip"]
+           "nrt_api_shade.hip", "nrt_api_cam.hip", "nrt_ring_march.hip", "nrt_ring_normal.hip"]
 HEADERS = ["nrt_kernels.h", "nrt_device.h", "nrt_internal.h", "nrt_launch.h"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nrt.h")
 
 # -ffp-contract=off: elementwise math rounds like the reference's eager torch ops (no silent FMA
 # contraction); MFMA and explicit fmaf() are unaffected.
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++20", "-fPIC", "-ffp-contract=off",
          "-fno-slp-vectorize", "-Wno-unused-result"]
 OBJDIR = os.path.join(HERE, "build_obj")
 

@@ -189,55 +189,34 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
   int rc0 = NRT_OK;
   // FP16 SDF MLPs of width 128/256 with F = 16/32 run the block-cooperative ring kernel
-  const int ne = s->mlp ? s->mlp->host_dev.ke / 16 : 0;
-  const bool ring16 = f16 && s->mlp && (s->host_dev.nb == 8 || s->host_dev.nb == 4) &&
-                      (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&
-                      s->mlp->desc.skip == 3 && s->mlp->desc.out <= 32 &&
-                      std::getenv("NRT_NO_RING") == nullptr;
+  const bool ring16 = f16 && ring_supported(s) && std::getenv("NRT_NO_RING") == nullptr;
   if (ring16) {
     ProfScope prof("k_intersect", st);
-    const char* wv_env = std::getenv("NRT_RING_WAVES");
-    const int WVr = (wv_env && std::atoi(wv_env) == 4) ? 4 : 8;
-    const bool fold = s->mlp->host_dev.fold != 0;
-    const size_t bias_bytes = (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
-#define NRT_RING_LAUNCH(NBV, NEV, WVV, FOLDV)                                                   \
-    {                                                                                          \
-      auto kern = k_march16<NBV, NEV, WVV, FOLDV>;                                             \
-      const size_t lds = ring::Cfg<NBV, NEV, WVV>::RING_BYTES + bias_bytes;                    \
-      dim3 g(ceil_div64(P, 32 * WVV)), b(64 * WVV);                                            \
-      if (!(rc0 = set_lds(kern, lds)))                                                         \
-        kern<<<g, b, lds, st>>>(s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, \
-                                throughput, idx, cnt);                                         \
-    }
-#define NRT_RING_FOLD(NBV, NEV, WVV) \
-    { if (fold) NRT_RING_LAUNCH(NBV, NEV, WVV, true) else NRT_RING_LAUNCH(NBV, NEV, WVV, false) }
-    if (s->host_dev.nb == 8 && ne == 3) {
-      if (WVr == 4) NRT_RING_FOLD(8, 3, 4) else NRT_RING_FOLD(8, 3, 8)
-    } else if (s->host_dev.nb == 8) NRT_RING_FOLD(8, 5, 8)
-    else if (ne == 3) NRT_RING_FOLD(4, 3, 8)
-    else {
-      if (WVr == 4) NRT_RING_FOLD(4, 5, 4) else NRT_RING_FOLD(4, 5, 8)
-    }
-#undef NRT_RING_FOLD
-#undef NRT_RING_LAUNCH
+    rc0 = ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, st);
   } else {
-  ProfScope prof("k_intersect", st);
-  NRT_NB_SWITCH(s->host_dev.nb, {
-    if (f16) {
-      if (!(rc0 = set_lds(k_intersect<true, NB>, lp.bytes)))
-        k_intersect<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
-                                                             throughput, idx, cnt, lp.RS, lp.per_wave);
-    } else {
-      if (!(rc0 = set_lds(k_intersect<false, NB>, lp.bytes)))
-        k_intersect<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
-                                                              throughput, idx, cnt, lp.RS, lp.per_wave);
-    }
-  });
+    ProfScope prof("k_intersect", st);
+    NRT_NB_SWITCH(s->host_dev.nb, {
+      if (f16) {
+        if (!(rc0 = set_lds(k_intersect<true, NB>, lp.bytes)))
+          k_intersect<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
+                                                               throughput, idx, cnt, lp.RS, lp.per_wave);
+      } else {
+        if (!(rc0 = set_lds(k_intersect<false, NB>, lp.bytes)))
+          k_intersect<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, ma, t, hit, p, n, raw_n,
+                                                                throughput, idx, cnt, lp.RS, lp.per_wave);
+      }
+    });
   }
   if (rc0) return rc0;
   if (int rc = check_launch("k_intersect")) return rc;
-  // normals on hit rays (f32 backward): raw gradient, unit normal, p += 5 eps n
-  if (int rc = launch_grad(s, p, idx, cnt, P, raw_n, n, p, a->epsilon, ws, st)) return rc;
+  // normals on hit rays: raw gradient, unit normal, p += 5 eps n.  FP16 ring SDFs use the
+  // forward-mode kernel (8 rays per wave-evaluation), everything else the f32 backward.
+  if (ring16 && std::getenv("NRT_F32_NORMALS") == nullptr) {
+    ProfScope prof("k_normal16", st);
+    if (int rc = ring_normals(s, idx, cnt, P, raw_n, n, p, a->epsilon, st)) return rc;
+  } else if (int rc = launch_grad(s, p, idx, cnt, P, raw_n, n, p, a->epsilon, ws, st)) {
+    return rc;
+  }
   if (wi) {
     k_frame_wi<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, st>>>(rays, n, P, nullptr, wi);
     if (int rc = check_launch("k_frame_wi")) return rc;

@@ -495,12 +495,16 @@ __device__ __forceinline__ void mlp32_backward_out0(const MlpDev& m, const EncIn
 // LDS, issues its global loads for chunk c+2 into registers, then runs chunk c's MFMAs with A
 // read by ds_read_b128 from LDS; one barrier per chunk.  Loads and stores are unconditional
 // (fixed count per wave; slots are padded) so hipcc never drains vmcnt inside the loop.
+#ifndef NRT_EXP
+#define NRT_EXP 0  // timing-only experiment bits (tools/exp_variants.sh); 0 in every shipped build
+#endif
 namespace nrt {
 namespace ring {
 
 __device__ __forceinline__ float sp2(float x) {
   // log2(1 + 2^x) = max(x, 0) + log2(1 + 2^-|x|): softplus in the log2 domain
   // max(x, 0) as one v_max_i32 on the bit pattern (negative floats and -0 are negative ints)
+  if (NRT_EXP & 2) return x;
   const float pos = __int_as_float(max(__float_as_int(x), 0));
   return pos + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
 }
@@ -566,13 +570,15 @@ struct Engine {
   // start of chunk c: publish chunk c+1, prefetch chunk c+2; returns this lane's A base
   __device__ __forceinline__ const h8* begin() {
     const int s1 = slot == 2 ? 0 : slot + 1;
-    store(s1);
-    load(nxt(nxt(c)));
+    if (!(NRT_EXP & 4)) {
+      store(s1);
+      load(nxt(nxt(c)));
+    }
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * C::SLOTF * 64 + lane;
   }
   __device__ __forceinline__ void end() {
-    __syncthreads();
+    if (!(NRT_EXP & 1)) __syncthreads();
     c = nxt(c);
     slot = slot == 2 ? 0 : slot + 1;
   }
@@ -614,12 +620,48 @@ __device__ __forceinline__ void act_pack1(const f16v& acc, h8& lo, h8& hi, int a
   }
 }
 
-// One SkipConnMLP evaluation (output row 0) for the wave's 32 rays through the ring; L hidden
-// layers and skip period SK are compile-time so the whole evaluation is straight-line code.
-// Every wave of the block must call it the same number of times.
-template <int NB, int NE, int WV, bool FOLD, int L, int SK>
+// Forward-mode tangent columns (TAN): column c = 4 * ray + comp; comp 0 carries the value
+// pre-activation z, comps 1..3 the tangent dz/dx_{comp-1}.  Every lane takes its ray's z from
+// the quad leader (DPP quad broadcast) and returns act(z) (comp 0) or act'(z) * dz (comps 1..3).
+__device__ __forceinline__ float quad_leader(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x00, 0xf, 0xf, false));
+}
+
+template <bool FOLD>
+__device__ __forceinline__ float act_tan(float z, bool value, int act) {
+  const float zv = quad_leader(z);
+  if (FOLD) {
+    // log2 domain: a = log2(1 + 2^z), da/dz = 1 / (1 + 2^-z)
+    const float e = __builtin_amdgcn_exp2f(-fabsf(zv));
+    const float den = 1.f + e;
+    const float pos = __int_as_float(max(__float_as_int(zv), 0));
+    const float val = pos + __builtin_amdgcn_logf(den);
+    const float sig = (zv >= 0.f ? 1.f : e) * __builtin_amdgcn_rcpf(den);
+    return value ? val : sig * z;
+  }
+  return value ? act_fwd<true>(zv, act) : act_bwd(zv, act) * z;
+}
+
+template <bool FOLD, bool TAN>
+__device__ __forceinline__ void act_pack(const f16v& acc, h8& lo, h8& hi, int act, bool value) {
+  if (!TAN) { act_pack1<FOLD>(acc, lo, hi, act); return; }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    lo[j] = (_Float16)act_tan<FOLD>(acc[j], value, act);
+    hi[j] = (_Float16)act_tan<FOLD>(acc[8 + j], value, act);
+  }
+}
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 32 columns through the ring; L
+// hidden layers and skip period SK are compile-time so the whole evaluation is straight-line
+// code.  Every wave of the block must call it the same number of times.  Columns are rays
+// (TAN = false) or 8 rays x (value, d/dx, d/dy, d/dz) (TAN = true, forward-mode gradient:
+// tangent columns get no bias, and their inputs are the encoding's derivatives).
+template <int NB, int NE, int WV, bool FOLD, int L, int SK, bool TAN = false>
 __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, const EncIn& e) {
   const int h = E.lane >> 5;
+  const int comp = TAN ? (E.lane & 3) : 0;
+  const bool value = comp == 0;
   const float kLog2e = 1.4426950408889634f;
   // encoding fragments, raw (init) and activated (skip inputs)
   h8 eraw[NE], eact[NE];
@@ -629,15 +671,46 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       float a, b;
-      enc_pair<true>(m, e, base + 2 * jj, a, b);
-      eraw[s][2 * jj] = (_Float16)a;
-      eraw[s][2 * jj + 1] = (_Float16)b;
-      if (FOLD) { a = sp2(a * kLog2e); b = sp2(b * kLog2e); }
-      else { a = act_fwd<true>(a, m.act); b = act_fwd<true>(b, m.act); }
-      eact[s][2 * jj] = (_Float16)a;
-      eact[s][2 * jj + 1] = (_Float16)b;
+      const int slot = base + 2 * jj;
+      enc_pair<true>(m, e, slot, a, b);
+      float ra = a, rb = b, xa, xb;
+      if (FOLD) { xa = sp2(a * kLog2e); xb = sp2(b * kLog2e); }
+      else { xa = act_fwd<true>(a, m.act); xb = act_fwd<true>(b, m.act); }
+      if (TAN && !value) {
+        // d enc / d x_k:  sin/cos pair -> (cos, -sin) * B[k][q];  raw input slot i -> [i == k]
+        const int k = comp - 1;
+        float ta, tb;
+        if (slot < 2 * m.freqs) {
+          const float bk = m.basis[k * m.freqs + (slot >> 1)];
+          ta = b * bk;
+          tb = -a * bk;
+        } else {
+          const int i = slot - 2 * m.freqs;
+          ta = (i == k) ? 1.f : 0.f;
+          tb = (i + 1 == k) ? 1.f : 0.f;
+        }
+        ra = ta; rb = tb;
+        if (FOLD) {
+          // d sp2(log2e * a) / da = log2e * sigmoid(a)
+          xa = kLog2e * ta * __builtin_amdgcn_rcpf(1.f + __expf(-a));
+          xb = kLog2e * tb * __builtin_amdgcn_rcpf(1.f + __expf(-b));
+        } else {
+          xa = act_bwd(a, m.act) * ta;
+          xb = act_bwd(b, m.act) * tb;
+        }
+      }
+      eraw[s][2 * jj] = (_Float16)ra;
+      eraw[s][2 * jj + 1] = (_Float16)rb;
+      eact[s][2 * jj] = (_Float16)xa;
+      eact[s][2 * jj + 1] = (_Float16)xb;
     }
   }
+  const float bmask = value ? 1.f : 0.f;
+  auto bias = [&](int layer, int ib) {
+    f16v b = E.bias_at(layer, ib, h);
+    if (TAN) b *= bmask;
+    return b;
+  };
   h8 hv[2][2 * NB];
   // Software pipeline: the region of chunk k (between two barriers) holds chunk k's MFMA chain
   // and the activation of chunk k-1's accumulator (`pend`), so the scheduler can put that VALU
@@ -648,10 +721,10 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) {
     const h8* A = E.begin();
-    f16v acc = E.bias_at(0, ib, h);
+    f16v acc = bias(0, ib);
 #pragma unroll
     for (int s = 0; s < NE; ++s) acc = mfma16(A[s * 64], eraw[s], acc);
-    if (ib > 0) act_pack1<FOLD>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act);
+    if (ib > 0) act_pack<FOLD, TAN>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act, value);
     pend = acc;
     E.end();
   }
@@ -662,23 +735,24 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) {
       const h8* A = E.begin();
-      f16v acc = E.bias_at(1 + i, ib, h);
-      if (ib == 0) act_pack1<FOLD>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act);
+      f16v acc = bias(1 + i, ib);
+      if (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
 #pragma unroll
-      for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[src][s], acc);
+      for (int s = 0; s < 2 * NB; ++s)
+        acc = mfma16((NRT_EXP & 16) ? hv[src][(s + 1) % (2 * NB)] : A[s * 64], hv[src][s], acc);
       if (skip) {
 #pragma unroll
         for (int s = 0; s < NE; ++s) acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
       }
-      if (ib > 0) act_pack1<FOLD>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act);
+      if (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
       pend = acc;
       E.end();
     }
   }
   // out layer (one 32-row block; output row 0 sits in register 0 of the h == 0 lanes)
   const h8* A = E.begin();
-  f16v acc = E.bias_at(L + 1, 0, h);
-  act_pack1<FOLD>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act);
+  f16v acc = bias(L + 1, 0);
+  act_pack<FOLD, TAN>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act, value);
 #pragma unroll
   for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[L & 1][s], acc);
   E.end();

@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(64 * WV, 2) k_march16(
   float best = 0.f, thr = 0.f;
   for (;;) {
     if (j == -2) {
-      const bool any = __syncthreads_or(live ? 1 : 0) != 0;
+      const bool any = (NRT_EXP & 8) || __syncthreads_or(live ? 1 : 0) != 0;
       if (i >= a.max_steps || !any) {
         if (!a.primary) break;
         j = -1;
@@ -428,6 +428,50 @@ __global__ void __launch_bounds__(64 * WV, 2) k_march16(
     if (lane == 0 && cnt) base = atomicAdd(hit_count, cnt);
     base = __shfl(base, 0);
     if (valid && hit && lane < 32) hit_idx[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
+  }
+}
+
+// FP16 normals on the ring engine by forward-mode differentiation: a wave's 32 MFMA columns
+// are 8 hit rays x (value, d/dx, d/dy, d/dz), so one evaluation yields the SDF gradient of 8
+// rays with no saved pre-activations.  Same outputs as k_sdf_grad: raw gradient, unit normal
+// normalize(g, 1e-6), p += 5 eps n (sdfs.py:156-157, autograd normal sdfs.py:184-197).
+// Blocks stride over the (device-counted) hit list together; the loop bound is block-uniform.
+template <int NB, int NE, int WV, bool FOLD>
+__global__ void __launch_bounds__(64 * WV, 2) k_normal16(
+    const SdfDev s, const MlpDev m, const int32_t* __restrict__ index,
+    const int32_t* __restrict__ count, int64_t M, float* __restrict__ grad,
+    float* __restrict__ n_out, float* __restrict__ p_io, float offset_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int64_t total = count ? (int64_t)(*(const NRT_GLOBAL int32_t*)count) : M;
+  const int64_t per_block = 8 * WV;
+  if ((int64_t)blockIdx.x * per_block >= total) return;  // whole block, before the ring starts
+  ring::Engine<NB, NE, WV> E;
+  E.init(m, smem_c);
+  const int lane = lane_id(), comp = lane & 3;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < total; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 8 * wv + ((lane & 31) >> 2);
+    const bool valid = i < total;
+    const int64_t ii = valid ? i : total - 1;
+    const int64_t idx = index ? (int64_t)index[ii] : ii;
+    const float x = p_io[idx * 3], y = p_io[idx * 3 + 1], z = p_io[idx * 3 + 2];
+    EncIn e;
+    e.x[0] = x; e.x[1] = y; e.x[2] = z; e.x[3] = 0.f;
+    e.xg = nullptr; e.lat = nullptr;
+    const float v = ring::eval<NB, NE, WV, FOLD, 8, 3, true>(E, m, e);
+    const float gx = __shfl(v, lane + 1), gy = __shfl(v, lane + 2), gz = __shfl(v, lane + 3);
+    if (valid && lane < 32 && comp == 0) {
+      float g[3] = {0.f, 0.f, 0.f};
+      if (s.kind == 2) spheres_grad(s, x, y, z, g);
+      g[0] += gx; g[1] += gy; g[2] += gz;
+      if (grad) { grad[idx * 3] = g[0]; grad[idx * 3 + 1] = g[1]; grad[idx * 3 + 2] = g[2]; }
+      float nx = g[0], ny = g[1], nz = g[2];
+      normalize3(nx, ny, nz, 1e-6f);
+      n_out[idx * 3] = nx; n_out[idx * 3 + 1] = ny; n_out[idx * 3 + 2] = nz;
+      p_io[idx * 3] = x + (nx * offset_eps) * 5.f;
+      p_io[idx * 3 + 1] = y + (ny * offset_eps) * 5.f;
+      p_io[idx * 3 + 2] = z + (nz * offset_eps) * 5.f;
+    }
   }
 }
 

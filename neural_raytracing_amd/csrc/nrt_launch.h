@@ -77,4 +77,46 @@ static inline int sdf_dims(const nrt_sdf* s, int& hidden, int& ke) {
   return NRT_OK;
 }
 
+// ---- FP16 ring engine (nrt_ring_march.hip / nrt_ring_normal.hip) ----
+// Configurations with a compiled ring kernel: 8 hidden layers of 128/256, skip 3, F = 16/32
+// (3 or 5 encoding k-steps), <= 32 outputs.
+inline bool ring_supported(const nrt_sdf* s) {
+  if (!s->mlp) return false;
+  const MlpDev& m = s->mlp->host_dev;
+  const int ne = m.ke / 16;
+  return (m.nb == 8 || m.nb == 4) && (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&
+         s->mlp->desc.skip == 3 && s->mlp->desc.out <= 32;
+}
+
+inline size_t ring_bias_bytes(const nrt_sdf* s) {
+  return (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
+}
+
+// kWV waves per block share one LDS weight ring
+constexpr int kRingWaves = 8;
+
+// call F.template operator()<NB, NE, FOLD>() for the SDF's ring configuration
+template <class F>
+int ring_dispatch(const nrt_sdf* s, F&& f) {
+  const MlpDev& m = s->mlp->host_dev;
+  const int ne = m.ke / 16;
+  const bool fold = m.fold != 0;
+#define NRT_RING_CASE(NBV, NEV)                                               \
+  if (m.nb == NBV && ne == NEV)                                               \
+    return fold ? f.template operator()<NBV, NEV, true>() : f.template operator()<NBV, NEV, false>();
+  NRT_RING_CASE(8, 3)
+  NRT_RING_CASE(8, 5)
+  NRT_RING_CASE(4, 3)
+  NRT_RING_CASE(4, 5)
+#undef NRT_RING_CASE
+  set_error("ring engine: unsupported SDF configuration");
+  return NRT_EINVAL;
+}
+
+int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+               uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+               int32_t* cnt, hipStream_t st);
+int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
+                 float* n, float* p_io, float eps, hipStream_t st);
+
 }  // namespace nrt
