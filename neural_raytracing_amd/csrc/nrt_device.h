@@ -515,6 +515,11 @@ struct Cfg {
   static constexpr int MAXL = (MAXF + WV - 1) / WV;       // loads per wave per chunk
   static constexpr int SLOTF = MAXL * WV;                 // fragments per ring slot
   static constexpr int RING_BYTES = 3 * SLOTF * 1024;
+  // ring SDFs have 3 inputs, no latent and F = 8 (NE - 1) frequencies (2F + 3 slots -> NE k-steps)
+  static constexpr int F = 8 * (NE - 1);
+  static constexpr int BASIS_BYTES = F * 16;  // float4 (B[0][q], B[1][q], B[2][q], 0) per q
+  // LDS of one block: ring | basis | bias16
+  static size_t lds_bytes(size_t bias_bytes) { return RING_BYTES + BASIS_BYTES + bias_bytes; }
 };
 
 template <int NB, int NE, int WV>
@@ -522,6 +527,7 @@ struct Engine {
   using C = Cfg<NB, NE, WV>;
   h8* ring;                 // LDS [3][SLOTF][64]
   const float* lbias;       // LDS copy of bias16
+  const float4* lbasis;     // LDS copy of the Fourier basis, one float4 per frequency
   __amdgpu_buffer_rsrc_t srd;  // FP16 weight stream
   const NRT_CONST int* coff;
   int nch;
@@ -549,7 +555,11 @@ struct Engine {
   // block-wide; afterwards slot 0 = chunk 0, stg = chunk 1
   __device__ __forceinline__ void init(const MlpDev& m, char* lds) {
     ring = reinterpret_cast<h8*>(lds);
-    float* lb = reinterpret_cast<float*>(lds + C::RING_BYTES);
+    float4* lq = reinterpret_cast<float4*>(lds + C::RING_BYTES);
+    for (int q = threadIdx.x; q < C::F; q += blockDim.x)
+      lq[q] = make_float4(m.basis[q], m.basis[C::F + q], m.basis[2 * C::F + q], 0.f);
+    lbasis = lq;
+    float* lb = reinterpret_cast<float*>(lds + C::RING_BYTES + C::BASIS_BYTES);
     const int nb16 = (m.n_hidden + 2) * m.bias16_stride;
     const NRT_GLOBAL float* gb = (const NRT_GLOBAL float*)m.bias16;
     for (int i = threadIdx.x; i < nb16; i += blockDim.x) lb[i] = gb[i];
@@ -658,21 +668,34 @@ __device__ __forceinline__ void act_pack(const f16v& acc, h8& lo, h8& hi, int ac
 // (TAN = false) or 8 rays x (value, d/dx, d/dy, d/dz) (TAN = true, forward-mode gradient:
 // tangent columns get no bias, and their inputs are the encoding's derivatives).
 template <int NB, int NE, int WV, bool FOLD, int L, int SK, bool TAN = false>
-__device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, const EncIn& e) {
+__device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, float x0, float x1,
+                                      float x2) {
   const int h = E.lane >> 5;
   const int comp = TAN ? (E.lane & 3) : 0;
   const bool value = comp == 0;
   const float kLog2e = 1.4426950408889634f;
-  // encoding fragments, raw (init) and activated (skip inputs)
+  // encoding fragments, raw (init) and activated (skip inputs).  Slot 16s + 8h + 2jj: k-steps
+  // s < NE-1 hold the sin/cos pairs of projection q = 8s + 4h + jj (utils.py:37-40, same fma
+  // order as proj()), the last k-step holds x0, x1, x2 in the h = 0 half and zeros.
+  constexpr int F = Engine<NB, NE, WV>::C::F;
   h8 eraw[NE], eact[NE];
 #pragma unroll
   for (int s = 0; s < NE; ++s) {
-    const int base = 16 * s + 8 * h;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       float a, b;
-      const int slot = base + 2 * jj;
-      enc_pair<true>(m, e, slot, a, b);
+      float4 bq;
+      if (s < NE - 1) {
+        bq = E.lbasis[8 * s + 4 * h + jj];
+        float pr = __fmul_rn(x0, bq.x);
+        pr = fmaf(x1, bq.y, pr);
+        pr = fmaf(x2, bq.z, pr);
+        a = __sinf(pr);
+        b = __cosf(pr);
+      } else {
+        a = (h == 0 && jj == 0) ? x0 : (h == 0 && jj == 1) ? x2 : 0.f;
+        b = (h == 0 && jj == 0) ? x1 : 0.f;
+      }
       float ra = a, rb = b, xa, xb;
       if (FOLD) { xa = sp2(a * kLog2e); xb = sp2(b * kLog2e); }
       else { xa = act_fwd<true>(a, m.act); xb = act_fwd<true>(b, m.act); }
@@ -680,12 +703,12 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, co
         // d enc / d x_k:  sin/cos pair -> (cos, -sin) * B[k][q];  raw input slot i -> [i == k]
         const int k = comp - 1;
         float ta, tb;
-        if (slot < 2 * m.freqs) {
-          const float bk = m.basis[k * m.freqs + (slot >> 1)];
+        if (s < NE - 1) {
+          const float bk = k == 0 ? bq.x : (k == 1 ? bq.y : bq.z);
           ta = b * bk;
           tb = -a * bk;
         } else {
-          const int i = slot - 2 * m.freqs;
+          const int i = 8 * h + 2 * jj;
           ta = (i == k) ? 1.f : 0.f;
           tb = (i + 1 == k) ? 1.f : 0.f;
         }

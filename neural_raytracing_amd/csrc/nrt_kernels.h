@@ -389,10 +389,7 @@ __global__ void __launch_bounds__(64 * WV, 2) k_march16(
       pz = __fadd_rn(oz, __fmul_rn(ts, dz));
     }
     float d = (s.kind == 2) ? spheres_value<true>(s, px, py, pz) : 0.f;
-    EncIn e;
-    e.x[0] = px; e.x[1] = py; e.x[2] = pz; e.x[3] = 0.f;
-    e.xg = nullptr; e.lat = nullptr;
-    d += ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, e);
+    d += ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, px, py, pz);
     if (j == -2) {
       const bool now = live && (d <= a.eps);
       hit = hit || now;
@@ -455,10 +452,7 @@ __global__ void __launch_bounds__(64 * WV, 2) k_normal16(
     const int64_t ii = valid ? i : total - 1;
     const int64_t idx = index ? (int64_t)index[ii] : ii;
     const float x = p_io[idx * 3], y = p_io[idx * 3 + 1], z = p_io[idx * 3 + 2];
-    EncIn e;
-    e.x[0] = x; e.x[1] = y; e.x[2] = z; e.x[3] = 0.f;
-    e.xg = nullptr; e.lat = nullptr;
-    const float v = ring::eval<NB, NE, WV, FOLD, 8, 3, true>(E, m, e);
+    const float v = ring::eval<NB, NE, WV, FOLD, 8, 3, true>(E, m, x, y, z);
     const float gx = __shfl(v, lane + 1), gy = __shfl(v, lane + 2), gz = __shfl(v, lane + 3);
     if (valid && lane < 32 && comp == 0) {
       float g[3] = {0.f, 0.f, 0.f};

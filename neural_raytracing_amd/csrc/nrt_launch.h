@@ -79,13 +79,14 @@ static inline int sdf_dims(const nrt_sdf* s, int& hidden, int& ke) {
 
 // ---- FP16 ring engine (nrt_ring_march.hip / nrt_ring_normal.hip) ----
 // Configurations with a compiled ring kernel: 8 hidden layers of 128/256, skip 3, F = 16/32
-// (3 or 5 encoding k-steps), <= 32 outputs.
+// (3 or 5 encoding k-steps), 3 inputs, no latent, <= 32 outputs.
 inline bool ring_supported(const nrt_sdf* s) {
   if (!s->mlp) return false;
   const MlpDev& m = s->mlp->host_dev;
   const int ne = m.ke / 16;
   return (m.nb == 8 || m.nb == 4) && (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&
-         s->mlp->desc.skip == 3 && s->mlp->desc.out <= 32;
+         s->mlp->desc.skip == 3 && s->mlp->desc.out <= 32 && m.in_size == 3 && m.latent == 0 &&
+         m.freqs == 8 * (ne - 1);
 }
 
 inline size_t ring_bias_bytes(const nrt_sdf* s) {

@@ -9,7 +9,7 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
   const size_t bias_bytes = ring_bias_bytes(s);
   return ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
     auto kern = k_march16<NB, NE, kRingWaves, FOLD>;
-    const size_t lds = ring::Cfg<NB, NE, kRingWaves>::RING_BYTES + bias_bytes;
+    const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
     if (int rc = set_lds(kern, lds)) return rc;
     kern<<<dim3(ceil_div64(P, 32 * kRingWaves)), dim3(64 * kRingWaves), lds, st>>>(
         s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, thr, idx, cnt);

@@ -8,7 +8,7 @@ int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64
   const size_t bias_bytes = ring_bias_bytes(s);
   return ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
     auto kern = k_normal16<NB, NE, kRingWaves, FOLD>;
-    const size_t lds = ring::Cfg<NB, NE, kRingWaves>::RING_BYTES + bias_bytes;
+    const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
     if (int rc = set_lds(kern, lds)) return rc;
     // 8 rays per wave; blocks stride over the device-side hit count
     const int64_t blocks = std::min<int64_t>(ceil_div64(M, 8 * kRingWaves), 2048);
