@@ -17,6 +17,7 @@ int nrt_light_create_field(const nrt_mlp* mlp, const float* color3, nrt_light** 
   l->mlp = mlp;
   NRT_HIP(hipMalloc(&l->dev, sizeof(LightDev)));
   NRT_HIP(hipMemcpy(l->dev, &l->host_dev, sizeof(LightDev), hipMemcpyHostToDevice));
+  if (int rc = build_light_program(l.get())) return rc;
   *out = l.release();
   return NRT_OK;
 }
@@ -79,6 +80,7 @@ int nrt_bsdf_create(int32_t n, const nrt_bsdf_component* comps, const nrt_mlp* s
   }
   NRT_HIP(hipMalloc(&b->dev, sizeof(BsdfDev)));
   NRT_HIP(hipMemcpy(b->dev, &b->host_dev, sizeof(BsdfDev), hipMemcpyHostToDevice));
+  if (int rc = build_bsdf_program(b.get())) return rc;
   *out = b.release();
   return NRT_OK;
 }
@@ -108,9 +110,15 @@ int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, cons
   upd(l->mlp);
   upd(b->spatial);
   for (auto* m : b->mlps) upd(m);
+  hipStream_t st = (hipStream_t)stream;
+  // FP16: light field, spatial weights and NeuralBSDFs on the program engine when compiled for
+  // their shapes (NRT_NO_PROGRAM keeps the per-wave register path)
+  if (f16 && std::getenv("NRT_NO_PROGRAM") == nullptr) {
+    const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, rgb, weights_out, st);
+    if (rc != NRT_EUNSUPPORTED) return rc;
+  }
   LdsPlan lp = plan_lds(hidden, ke, 64, f16, false);
   int blocks = std::max(1, std::min(ceil_div64(ceil_div64(P, 32), lp.waves), 2048));
-  hipStream_t st = (hipStream_t)stream;
   ProfScope prof("k_shade_direct", st);
   if (f16) {
     if (int rc = set_lds(k_shade_direct<true>, lp.bytes)) return rc;

@@ -61,6 +61,36 @@ struct MlpDev {
   const float* bias16;             // [layer][bias16_stride] (folded like stream16)
   int bias16_stride;               // max(nb, ob) * 32
   int fold;                        // 1 when softplus was folded
+  // FP16 k-outer stream for the program engine (shading MLPs): layer by layer, chunks of kc
+  // consecutive k-steps x all row blocks ([kstep][rowblock][64 lanes], kc = 16 / nb), same
+  // fragments as w16 (never folded).
+  const h8* streamk16;
+  const int* chunkk_off;           // per chunk, fragment offset within streamk16
+  int nk_chunks;
+  int kc;
+  int nk_frags;                    // fragments in streamk16 (without tail)
+};
+
+// A shading "program": the MLPs one kernel evaluates per ray batch, concatenated into one
+// k-outer weight stream so the LDS ring prefetches across MLP boundaries.
+constexpr int kMaxProgMlp = 40;
+struct ProgMlp {
+  int nb, ne, ob, L, skip, out, act, F;
+  int bias_off;      // floats into ProgDev::bias (layer stride bstride)
+  int bstride;
+  int basis_off;     // float4 index into ProgDev::basis
+  int chunk0;        // first chunk of this MLP in the program
+};
+struct ProgDev {
+  const h8* stream;        // [frags + tail][64 lanes]
+  const int* coff;         // per chunk, fragment offset
+  int n_chunks;
+  const float* bias;       // all MLPs' biases [mlp][layer][bstride]
+  int bias_floats;
+  const float4* basis;     // all MLPs' (B0q, B1q, B2q, 0)
+  int basis_q;
+  int n_mlp;
+  ProgMlp mlp[kMaxProgMlp];
 };
 
 struct SdfDev {
@@ -780,6 +810,213 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
   for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[L & 1][s], acc);
   E.end();
   return __shfl(acc[0], E.lane & 31);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// k-outer program engine (shading MLPs): chunk = KC k-steps x all NB row blocks, so the NB
+// accumulators are independent MFMA chains; the encoding k-steps are computed on the fly (once
+// per layer), which keeps wide encodings (F = 64 / 128) out of the register file.  The layer
+// count and skip period are runtime values.
+// ------------------------------------------------------------------------------------------
+template <int WV>
+struct KEngine {
+  static constexpr int MAXF = 16;  // fragments per chunk: KC * NB <= 16 (out layer: KC)
+  static constexpr int MAXL = (MAXF + WV - 1) / WV;
+  static constexpr int SLOTF = MAXL * WV;
+  static constexpr int RING_BYTES = 3 * SLOTF * 1024;
+  h8* ring;
+  const float* lbias;
+  const float4* lbasis;
+  __amdgpu_buffer_rsrc_t srd;
+  const NRT_CONST int* coff;
+  int nch, c, slot, lane, wv;
+  h8 stg[MAXL];
+
+  __host__ __device__ static size_t lds_bytes(const ProgDev& p) {
+    return RING_BYTES + (size_t)p.basis_q * 16 + (size_t)p.bias_floats * 4;
+  }
+  __device__ __forceinline__ void load(int chunk) {
+    const int off = coff[chunk] + wv;
+#pragma unroll
+    for (int q = 0; q < MAXL; ++q) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(srd, lane * 16, (off + WV * q) * 1024, 0);
+      stg[q] = __builtin_bit_cast(h8, v);
+    }
+  }
+  __device__ __forceinline__ void store(int sl) {
+    h8* D = ring + sl * SLOTF * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < MAXL; ++q) D[(wv + WV * q) * 64] = stg[q];
+  }
+  __device__ __forceinline__ int nxt(int x) const { return x + 1 == nch ? 0 : x + 1; }
+  // block-wide: LDS = ring | basis | bias; afterwards slot 0 = chunk 0, stg = chunk 1
+  __device__ __forceinline__ void init(const ProgDev& p, char* lds) {
+    ring = reinterpret_cast<h8*>(lds);
+    float4* lq = reinterpret_cast<float4*>(lds + RING_BYTES);
+    for (int q = threadIdx.x; q < p.basis_q; q += blockDim.x) lq[q] = p.basis[q];
+    lbasis = lq;
+    float* lb = reinterpret_cast<float*>(lds + RING_BYTES + (size_t)p.basis_q * 16);
+    for (int i = threadIdx.x; i < p.bias_floats; i += blockDim.x) lb[i] = p.bias[i];
+    lbias = lb;
+    srd = __builtin_amdgcn_make_buffer_rsrc((void*)p.stream, 0, 0x7ffffff0, 0x00020000);
+    coff = (const NRT_CONST int*)p.coff;
+    nch = p.n_chunks;
+    lane = threadIdx.x & 63;
+    wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    c = 0;
+    slot = 0;
+    load(0);
+    store(0);
+    load(nxt(0));
+    __syncthreads();
+  }
+  __device__ __forceinline__ const h8* begin() {
+    const int s1 = slot == 2 ? 0 : slot + 1;
+    store(s1);
+    load(nxt(nxt(c)));
+    __builtin_amdgcn_sched_barrier(0);
+    return ring + slot * SLOTF * 64 + lane;
+  }
+  __device__ __forceinline__ void end() {
+    __syncthreads();
+    c = nxt(c);
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  // acc[reg] = bias[layer][32 ib + (reg&3) + 8 (reg>>2) + 4h]
+  __device__ __forceinline__ f16v bias_at(const ProgMlp& pm, int layer, int ib, int h) const {
+    f16v v;
+    const float* b = lbias + pm.bias_off + layer * pm.bstride + 32 * ib + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      float4 q = *reinterpret_cast<const float4*>(b + 8 * g);
+      v[4 * g + 0] = q.x; v[4 * g + 1] = q.y; v[4 * g + 2] = q.z; v[4 * g + 3] = q.w;
+    }
+    return v;
+  }
+};
+
+// B fragment of encoding k-step s for 3-input, latent-free MLPs with F = 8 (NE - 1):
+// s < NE-1 -> sin/cos of projections q = 8s + 4h + jj, s = NE-1 -> (x0, x1, x2, 0...) in half 0.
+template <int ACTIN>
+__device__ __forceinline__ h8 enc_frag_k(const float4* basis, int s, int last, int h, float x0,
+                                         float x1, float x2) {
+  h8 f;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    float a, b;
+    if (s < last) {
+      const float4 bq = basis[8 * s + 4 * h + jj];
+      float pr = __fmul_rn(x0, bq.x);
+      pr = fmaf(x1, bq.y, pr);
+      pr = fmaf(x2, bq.z, pr);
+      a = __sinf(pr);
+      b = __cosf(pr);
+    } else {
+      a = (h == 0 && jj == 0) ? x0 : (h == 0 && jj == 1) ? x2 : 0.f;
+      b = (h == 0 && jj == 0) ? x1 : 0.f;
+    }
+    if (ACTIN >= 0) { a = act_fwd<true>(a, ACTIN); b = act_fwd<true>(b, ACTIN); }
+    f[2 * jj] = (_Float16)a;
+    f[2 * jj + 1] = (_Float16)b;
+  }
+  return f;
+}
+
+template <int NB, int ACT>
+__device__ __forceinline__ void kact(const f16v (&acc)[NB], h8 (&hv)[2 * NB]) {
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      h8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = (_Float16)act_fwd<true>(acc[ib][8 * s2 + j], ACT);
+      hv[2 * ib + s2] = f;
+    }
+}
+
+// One evaluation of program MLP `pm` (compile-time NB, NE, activation) for the wave's 32 rays;
+// returns the first output row block (rows (reg&3) + 8(reg>>2) + 4h of column lane&31).
+// Every wave of the block must run the same sequence of evaluations (the ring is shared).
+template <int NB, int NE, int WV, int ACT>
+__device__ __forceinline__ f16v keval(KEngine<WV>& E, const ProgMlp& pm, float x0, float x1,
+                                      float x2) {
+  constexpr int KC = 16 / NB;
+  constexpr int CE = (NE + KC - 1) / KC;   // chunks of the encoding part
+  constexpr int CH = (2 * NB + KC - 1) / KC;  // chunks of the hidden part
+  const int h = E.lane >> 5;
+  const float4* basis = E.lbasis + pm.basis_off;
+  f16v acc[NB];
+  h8 hv[2 * NB];
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
+  // init layer: raw encoding (neural_blocks.py:80)
+#pragma unroll
+  for (int cc = 0; cc < CE; ++cc) {
+    const h8* A = E.begin();
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int s = cc * KC + j;
+      if (s < NE) {
+        const h8 b = enc_frag_k<-1>(basis, s, NE - 1, h, x0, x1, x2);
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(j * NB + ib) * 64], b, acc[ib]);
+      }
+    }
+    E.end();
+  }
+  // hidden layers: x = layer(act(cat[x, enc] if skip else x)) (neural_blocks.py:81-84)
+  for (int i = 0; i < pm.L; ++i) {
+    kact<NB, ACT>(acc, hv);
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 1 + i, ib, h);
+#pragma unroll
+    for (int cc = 0; cc < CH; ++cc) {
+      const h8* A = E.begin();
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int s = cc * KC + j;
+        if (s < 2 * NB) {
+#pragma unroll
+          for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(j * NB + ib) * 64], hv[s], acc[ib]);
+        }
+      }
+      E.end();
+    }
+    if (i != pm.L - 1 && (i % pm.skip) == 0) {
+#pragma unroll
+      for (int cc = 0; cc < CE; ++cc) {
+        const h8* A = E.begin();
+#pragma unroll
+        for (int j = 0; j < KC; ++j) {
+          const int s = cc * KC + j;
+          if (s < NE) {
+            const h8 b = enc_frag_k<ACT>(basis, s, NE - 1, h, x0, x1, x2);
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(j * NB + ib) * 64], b, acc[ib]);
+          }
+        }
+        E.end();
+      }
+    }
+  }
+  kact<NB, ACT>(acc, hv);
+  // out layer (one row block, all 2NB k-steps in one chunk)
+  f16v o = E.bias_at(pm, pm.L + 1, 0, h);
+  {
+    const h8* A = E.begin();
+#pragma unroll
+    for (int s = 0; s < 2 * NB; ++s) o = mfma16(A[s * 64], hv[s], o);
+    E.end();
+  }
+  return o;
+}
+
+// output row j (< 32) of a keval tile for this lane's column
+__device__ __forceinline__ float tile_row(const f16v& o, int j, int lane) {
+  const int reg = (j & 3) + 4 * (j >> 3), hh = (j >> 2) & 1;
+  return __shfl(o[reg], (lane & 31) + 32 * hh);
 }
 
 }  // namespace ring

@@ -14,6 +14,18 @@ struct nrt_mlp {
   nrt::MlpDev* dev = nullptr;    // device copy
   void* blob = nullptr;          // all packed arrays
   size_t blob_bytes = 0;
+  // host copies used to assemble shading programs (nrt_prog.hip)
+  std::vector<int> host_chunkk;  // k-outer chunk offsets
+  std::vector<float> host_bias;  // unfolded biases [layer][bias16_stride]
+  std::vector<float> host_basis; // [in][F]
+};
+
+// A device program (ProgDev) and the buffer holding its stream, chunk table, biases and basis.
+struct nrt_prog {
+  nrt::ProgDev d{};
+  void* buf = nullptr;
+  bool ok = false;       // false: some MLP has a shape without a compiled program kernel
+  ~nrt_prog() { if (buf) (void)hipFree(buf); }
 };
 
 struct nrt_sdf {
@@ -55,6 +67,7 @@ struct nrt_light {
   nrt::LightDev host_dev;
   nrt::LightDev* dev = nullptr;
   const nrt_mlp* mlp = nullptr;
+  nrt_prog prog;          // [light field MLP]
 };
 
 struct nrt_bsdf {
@@ -62,6 +75,7 @@ struct nrt_bsdf {
   nrt::BsdfDev* dev = nullptr;
   std::vector<const nrt_mlp*> mlps;
   const nrt_mlp* spatial = nullptr;
+  nrt_prog prog;          // [spatial] + neural components, in component order
 };
 
 namespace nrt {

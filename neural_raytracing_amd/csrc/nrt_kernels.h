@@ -702,6 +702,159 @@ __global__ void __launch_bounds__(256) k_shade_direct(
 }
 
 // ------------------------------------------------------------------------------------------
+// FP16 shading on the program engine: k_light16 (emitter sample per hit) then k_bsdf16
+// (spatial weights + components).  Same math as k_shade_direct; LS carries, per position i of
+// the hit list, le (3) | feat = param_rusin2(wi, wo) (3) | wo (3) | pad (3).
+// ------------------------------------------------------------------------------------------
+constexpr int kLsStride = 12;
+
+__device__ __forceinline__ void light_from_field(float vx, float vy, float vz, const LightDev& lt,
+                                                 const float fr[9], float wix, float wiy,
+                                                 float wiz, float le[3], float wo[3],
+                                                 float feat[3]) {
+  // LightField.sample_direction (lights.py:175-195)
+  const float mag = sqrtf(vx * vx + vy * vy + vz * vz);
+  float ldx = vx, ldy = vy, ldz = vz;
+  normalize3(ldx, ldy, ldz, 1e-6f);
+  ldx = fminf(fmaxf(ldx, 1e-6f), 1.f);
+  ldy = fminf(fmaxf(ldy, 1e-6f), 1.f);
+  ldz = fminf(fmaxf(ldz, 1e-6f), 1.f);
+  le[0] = mag * lt.color_sig[0]; le[1] = mag * lt.color_sig[1]; le[2] = mag * lt.color_sig[2];
+  to_local(fr, ldx, ldy, ldz, wo);
+  rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
+}
+
+// FIELD: LightField MLP (8 x 32 hidden blocks, F = 16) on the ring; else a point light (VALU only)
+template <int WV, bool FIELD>
+__global__ void __launch_bounds__(64 * WV, 1) k_light16(
+    const ProgDev prog, const LightDev* __restrict__ lp, const float* __restrict__ P_,
+    const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
+    const int32_t* __restrict__ hit_count, float* __restrict__ LS) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const LightDev& lt = *lp;
+  const int64_t total = *(const NRT_GLOBAL int32_t*)hit_count;
+  const int64_t per_block = 32 * WV;
+  if ((int64_t)blockIdx.x * per_block >= total) return;
+  ring::KEngine<WV> E;
+  if (FIELD) E.init(prog, smem_c);
+  const int lane = lane_id(), r = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < total; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 32 * wv + r;
+    const bool valid = i < total;
+    const int64_t idx = hit_idx[valid ? i : total - 1];
+    const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
+    float fr[9];
+    make_frame(N_[idx * 3], N_[idx * 3 + 1], N_[idx * 3 + 2], fr);
+    const float wix = WI[idx * 3], wiy = WI[idx * 3 + 1], wiz = WI[idx * 3 + 2];
+    float le[3], wo[3], feat[3];
+    if (FIELD) {
+      const f16v o = ring::keval<8, 3, WV, ACT_LEAKY>(E, prog.mlp[0], px, py, pz);
+      light_from_field(ring::tile_row(o, 0, lane), ring::tile_row(o, 1, lane),
+                       ring::tile_row(o, 2, lane), lt, fr, wix, wiy, wiz, le, wo, feat);
+    } else {
+      // PointLights.sample_direction (lights.py:89-110)
+      float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
+      float dist = sqrtf(vx * vx + vy * vy + vz * vz);
+      float ldx = vx, ldy = vy, ldz = vz;
+      normalize3(ldx, ldy, ldz, 1e-6f);
+      float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
+      le[0] = lt.scaled_dir[0] / fall; le[1] = lt.scaled_dir[1] / fall; le[2] = lt.scaled_dir[2] / fall;
+      to_local(fr, ldx, ldy, ldz, wo);
+      rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
+    }
+    if (valid && lane < 32) {
+      float* o = LS + i * kLsStride;
+      o[0] = le[0]; o[1] = le[1]; o[2] = le[2];
+      o[3] = feat[0]; o[4] = feat[1]; o[5] = feat[2];
+      o[6] = wo[0]; o[7] = wo[1]; o[8] = wo[2];
+    }
+  }
+}
+
+// Spatial weights (16 layers x 256, F = 128) and NeuralBSDF components (6 x 96, F = 64) on the
+// ring; program order = [spatial] + neural components in component order.
+template <int WV, bool SPATIAL>
+__global__ void __launch_bounds__(64 * WV, 1) k_bsdf16(
+    const ProgDev prog, const BsdfDev* __restrict__ bp, const float* __restrict__ P_,
+    const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
+    const int32_t* __restrict__ hit_count, const float* __restrict__ LS, float* __restrict__ rgb,
+    float* __restrict__ wout) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const BsdfDev& bs = *bp;
+  const int nc = bs.n;
+  const int64_t total = *(const NRT_GLOBAL int32_t*)hit_count;
+  const int64_t per_block = 32 * WV;
+  if ((int64_t)blockIdx.x * per_block >= total) return;
+  ring::KEngine<WV> E;
+  E.init(prog, smem_c);
+  const int lane = lane_id(), r = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // per-wave spatial weights K[32 rays][kMaxComponents] after the program's LDS
+  float* Kw = reinterpret_cast<float*>(smem_c + ring::KEngine<WV>::lds_bytes(prog)) +
+              wv * 32 * kMaxComponents;
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < total; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 32 * wv + r;
+    const bool valid = i < total;
+    const int64_t ii = valid ? i : total - 1;
+    const int64_t idx = hit_idx[ii];
+    const float* ls = LS + ii * kLsStride;
+    const float le0 = ls[0], le1 = ls[1], le2 = ls[2];
+    const float ft0 = ls[3], ft1 = ls[4], ft2 = ls[5];
+    const float wo0 = ls[6], wo1 = ls[7], wo2 = ls[8];
+    int k = 0;
+    if (SPATIAL) {
+      const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
+      const f16v o = ring::keval<8, 17, WV, ACT_LEAKY>(E, prog.mlp[0], px, py, pz);
+      k = 1;
+#pragma unroll
+      for (int j = 0; j < kMaxComponents; ++j) {
+        const float v = ring::tile_row(o, j, lane);
+        if (j < nc && lane < 32) Kw[r * kMaxComponents + j] = sigmoidf_(v);
+      }
+    } else {
+      for (int j = lane >> 5; j < nc; j += 2) Kw[r * kMaxComponents + j] = 1.f;
+    }
+    wave_lds_fence();
+    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    for (int j = 0; j < nc; ++j) {
+      const BsdfCompDev& c = bs.comp[j];
+      float v[3];
+      if (c.kind == 0) {
+        const f16v o = ring::keval<3, 9, WV, ACT_LEAKY>(E, prog.mlp[k], ft0, ft1, ft2);
+        ++k;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) v[q] = act_fwd<false>(ring::tile_row(o, q, lane), c.act);
+      } else if (c.kind == 1) {
+        // Diffuse.eval_and_pdf (bsdfs.py:108-118)
+        for (int q = 0; q < 3; ++q) {
+          float x = wo2 * c.params[q];
+          v[q] = (c.act == ACT_NONE) ? x / (float)M_PI : act_fwd<false>(x, c.act);
+        }
+      } else {
+        // Conductor.eval_and_pdf (bsdfs.py:364-388)
+        const float wix = WI[idx * 3], wiy = WI[idx * 3 + 1], wiz = WI[idx * 3 + 2];
+        float rx = -wix, ry = -wiy, rz = wiz;
+        bool th = ((rx * wo0 + ry * wo1) + rz * wo2) > 0.94f;
+        float fres = fresnel_conductor(wiz, c.params[3]);
+        for (int q = 0; q < 3; ++q) v[q] = th ? fres * act_fwd<false>(c.params[q], c.act) : 0.f;
+      }
+      const float kj = Kw[r * kMaxComponents + j];
+      f0 += v[0] * kj; f1 += v[1] * kj; f2 += v[2] * kj;
+    }
+    if (valid && lane < 32) {
+      // integrators.py:186-189: mis(=1) * bsdf_val * emitter_val, / emitter_samples(=1)
+      rgb[idx * 3] = (1.f * f0) * le0;
+      rgb[idx * 3 + 1] = (1.f * f1) * le1;
+      rgb[idx * 3 + 2] = (1.f * f2) * le2;
+      if (wout)
+        for (int j = 0; j < nc; ++j) wout[idx * nc + j] = Kw[r * kMaxComponents + j];
+    }
+    wave_lds_fence();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // cameras + composite
 // ------------------------------------------------------------------------------------------
 template <int = 0>

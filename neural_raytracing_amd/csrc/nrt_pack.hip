@@ -206,6 +206,41 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   }
   const int n_chunks = (int)chunk_off.size();
   stream.resize(stream.size() + (size_t)64 * 64 * 8, (_Float16)0.f);  // tail for unguarded prefetch
+
+  // ---- FP16 k-outer stream (program engine): per layer the w16 fragments [kstep][rowblock] in
+  // chunks of kc k-steps (hidden and encoding parts chunked separately; the out layer is one
+  // chunk of all its k-steps)
+  const int kc = std::max(1, 16 / NB);
+  std::vector<_Float16> streamk;
+  std::vector<int> chunkk_off;
+  for (size_t l = 0; l < layers.size(); ++l) {
+    const Layer& ly = layers[l];
+    const bool is_out = (l + 1 == layers.size());
+    const int nrb = (ly.R + 31) / 32;
+    const int ks_h = ly.hidden_in ? 2 * NB : 0;
+    const int ks_e = ly.enc_in ? ke / 16 : 0;
+    const int base = (int)(streamk.size() / (64 * 8));
+    auto frag = [&](int s, int ib, int lane, int j) {
+      int i = lane & 31, hf = lane >> 5;
+      int col = (s < ks_h) ? col_of_hidden(32 * (s >> 1) + 16 * (s & 1) + 8 * (j >> 2) + 4 * hf + (j & 3))
+                           : col_of_slot(ly, 16 * (s - ks_h) + 8 * hf + j);
+      return (_Float16)wval(ly, 32 * ib + i, col);
+    };
+    for (int s = 0; s < ks_h + ks_e; ++s)
+      for (int ib = 0; ib < nrb; ++ib)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) streamk.push_back(frag(s, ib, lane, j));
+    if (is_out) {
+      chunkk_off.push_back(base);
+    } else {
+      for (int s = 0; s < ks_h; s += kc) chunkk_off.push_back(base + s * nrb);
+      for (int s = 0; s < ks_e; s += kc) chunkk_off.push_back(base + (ks_h + s) * nrb);
+    }
+  }
+  const int nk_frags = (int)(streamk.size() / (64 * 8));
+  streamk.resize(streamk.size() + (size_t)64 * 64 * 8, (_Float16)0.f);
+  size_t off_streamk = blob.add(streamk.data(), streamk.size() * sizeof(_Float16));
+  size_t off_coffk = blob.add(chunkk_off.data(), chunkk_off.size() * sizeof(int));
   size_t off_stream = blob.add(stream.data(), stream.size() * sizeof(_Float16));
   size_t off_coff = blob.add(chunk_off.data(), chunk_off.size() * sizeof(int));
   size_t off_b16 = blob.add(bias16.data(), bias16.size() * sizeof(float));
@@ -213,6 +248,11 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   std::unique_ptr<nrt_mlp> m(new nrt_mlp());
   m->desc = *d;
   m->blob_bytes = blob.bytes.size();
+  m->host_chunkk = chunkk_off;
+  m->host_bias.assign(layers.size() * (size_t)bstride, 0.f);
+  for (size_t l = 0; l < layers.size(); ++l)
+    for (int r = 0; r < layers[l].R; ++r) m->host_bias[l * bstride + r] = layers[l].b[r];
+  m->host_basis.assign(basis, basis + (size_t)in * F);
   NRT_HIP(hipMalloc(&m->blob, m->blob_bytes));
   NRT_HIP(hipMemcpy(m->blob, blob.bytes.data(), m->blob_bytes, hipMemcpyHostToDevice));
   char* base = static_cast<char*>(m->blob);
@@ -230,6 +270,11 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   md.bias16 = reinterpret_cast<const float*>(base + off_b16);
   md.bias16_stride = bstride;
   md.fold = fold ? 1 : 0;
+  md.streamk16 = reinterpret_cast<const h8*>(base + off_streamk);
+  md.chunkk_off = reinterpret_cast<const int*>(base + off_coffk);
+  md.nk_chunks = (int)chunkk_off.size();
+  md.kc = kc;
+  md.nk_frags = nk_frags;
   m->host_dev = md;
   NRT_HIP(hipMalloc(&m->dev, sizeof(MlpDev)));
   NRT_HIP(hipMemcpy(m->dev, &md, sizeof(MlpDev), hipMemcpyHostToDevice));

@@ -380,3 +380,56 @@ def test_fp16_normals_match_f32_backward(monkeypatch):
     assert (p16.reshape(-1, 3)[m] - p32.reshape(-1, 3)[m]).abs().max() < 1e-5
     # misses keep zero normals
     assert n16.reshape(-1, 3)[~m].abs().max() == 0
+
+
+@pytest.mark.gpu
+def test_program_shading_nerf_synthetic_scene(monkeypatch):
+    """k_light16 + k_bsdf16 (program engine: LightField 10x256, spatial 16x256 F=128, 8 x
+    NeuralBSDF 6x96 F=64) against the per-wave FP16 register path (same MFMA order: equal to
+    rounding) and against the oracle (PSNR)."""
+    import bench
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd import _lib
+    scene = bench.build_scene("cuda", samples=32, seed=2)
+    pt = scene["pt"]
+    size, crop = 200, 40
+    c0 = (size - crop) // 2
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    c2w = bench.view_c2w(0, 1).unsqueeze(0)
+    cam = pt.cameras.NeRFCamera(cam_to_world=c2w.cuda(), focal=focal)
+
+    def render():
+        random.seed(7)
+        with torch.no_grad():
+            img, _ = pt.pathtrace_sample(scene["shape"], scene["lights"], cam, scene["integrator"],
+                                         bsdf=scene["bsdf"], size=size, chunk_size=size,
+                                         bundle_size=1, crop_size=crop, uv=(c0, c0), background=0,
+                                         with_noise=0.0)
+        return img.cpu()
+
+    nra.set_precision("fp16")
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    prog = render()
+    _, n_bsdf = _lib.profile_read("k_bsdf16")
+    _, n_light = _lib.profile_read("k_light16")
+    _lib.profile_enable(False)
+    assert n_bsdf >= 1 and n_light >= 1, "program shading path did not run"
+    monkeypatch.setenv("NRT_NO_PROGRAM", "1")
+    regs = render()
+    monkeypatch.delenv("NRT_NO_PROGRAM")
+    nra.set_precision("fp32")
+    assert (prog - regs).abs().max() < 2e-3, (prog - regs).abs().max()
+    # oracle (fp32 restatement) on the same crop
+    from oracle import pathtracer_ref as R
+    osc = bench.oracle_scene(scene)
+    random.seed(7)
+    with torch.no_grad():
+        want = R.render(osc["shape"], osc["lights"], R.NeRFCameraRef(c2w, focal), osc["integrator"],
+                        osc["bsdf"], size=size, chunk_size=size, background=0.0, with_noise=0.0,
+                        crop=(c0, c0, crop))
+    hit = prog[..., 3] if prog.shape[-1] == 4 else None
+    assert hit is None or (prog[..., :3].abs().sum() > 0)
+    mse = ((prog.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
+    psnr = -10 * math.log10(max(mse, 1e-12))
+    assert psnr > 40, psnr
