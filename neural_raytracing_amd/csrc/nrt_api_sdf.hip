@@ -146,9 +146,12 @@ int nrt_sdf_grad(const nrt_sdf* s, const float* p, int64_t M, float* grad, void*
   return rc;
 }
 
+// [f32 normal-pass scratch | 256 B align | FP16 ring march scan keys (P x u64)]
+static size_t grad_ws_aligned(const nrt_sdf* s) { return (grad_workspace_bytes(s) + 255) & ~(size_t)255; }
+
 size_t nrt_intersect_workspace_bytes(const nrt_sdf* s, int64_t P) {
-  (void)P;
-  return s ? grad_workspace_bytes(s) + 256 : 0;
+  if (!s) return 0;
+  return grad_ws_aligned(s) + (ring_supported(s) ? ring_march_ws_bytes(std::max<int64_t>(P, 0)) : 0) + 256;
 }
 
 int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_march_params* a,
@@ -192,7 +195,8 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   const bool ring16 = f16 && ring_supported(s) && std::getenv("NRT_NO_RING") == nullptr;
   if (ring16) {
     ProfScope prof("k_intersect", st);
-    rc0 = ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, st);
+    auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
+    rc0 = ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
   } else {
     ProfScope prof("k_intersect", st);
     NRT_NB_SWITCH(s->host_dev.nb, {

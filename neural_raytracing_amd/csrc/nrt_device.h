@@ -532,11 +532,17 @@ namespace nrt {
 namespace ring {
 
 __device__ __forceinline__ float sp2(float x) {
-  // log2(1 + 2^x) = max(x, 0) + log2(1 + 2^-|x|): softplus in the log2 domain
-  // max(x, 0) as one v_max_i32 on the bit pattern (negative floats and -0 are negative ints)
+  // softplus in the log2 domain, log2(1 + 2^x), as exp + add + log (20 issue cycles, 3 VALU per
+  // element: one MFMA gap holds one element's activation).  Against max(x,0) + log2(1 + 2^-|x|)
+  // the only loss is below the f16 the result is rounded to: 1 + 2^x rounds to 1 for x < -24
+  // (true value < 9e-8) and 2^x overflows for x >= 128 (a natural pre-activation above 88),
+  // which the FP16 path does not support; the FP32 path keeps torch's exact form.
   if (NRT_EXP & 2) return x;
-  const float pos = __int_as_float(max(__float_as_int(x), 0));
-  return pos + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
+  if (NRT_EXP & 32) {
+    const float pos = __int_as_float(max(__float_as_int(x), 0));
+    return pos + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
+  }
+  return __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(x));
 }
 
 template <int NB, int NE, int WV>

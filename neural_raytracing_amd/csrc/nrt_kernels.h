@@ -343,88 +343,165 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
   }
 }
 
-// FP16 block-cooperative march + scan: the WV waves of a block step through their SDF
-// evaluations together (the LDS weight ring needs every wave at the same chunk), so the march
-// phase ends when no ray of the block is marching.  Results are identical to k_intersect's.
+// FP16 march + coarse scan on the ring engine, load-balanced per lane.
+//
+// The reference evaluates every ray at every one of max_steps march steps and at the 130 scan
+// points (sdfs.py:119-131, 232-249); only the march is data-dependent (hit / t >= max_t end it
+// early), the scan is a fixed walk that does not depend on the march.  A wave therefore works
+// through a private job list instead of a fixed 32-ray tile: the grid is persistent (one block
+// per resident slot), wave w owns rays w, w + nw, w + 2 nw, ... (a strided sample of the image,
+// so every wave gets a similar mix of short hit marches and long miss marches), and its list is
+//     [march of each owned ray] [scan segment 0 of each ray] ... [scan segment NSEG-1 ...]
+// A lane whose job has ended takes the next list entry (ballot + prefix count on a wave-uniform
+// cursor, no atomics), so lanes never idle on a finished ray; the list ends with short
+// fixed-length segments, so lanes run out of work within one segment of each other.
+// A segment keeps the running (min, first index) exactly as the reference loop does and merges
+// it into the ray's 64-bit key [ordered min | index] with an atomic min: the smallest key is the
+// smallest value and, among equal values, the first sample -- the reference's strict-< update.
+// A second launch (mode 1) evaluates sdf(best) for the throughput.  Lanes l and l + 32 carry the
+// same ray (the MFMA K halves) and run identical state machines.
+constexpr int kScanSegs = 8;  // sample j in [0, 128]: segment 0 = [0, 16], segment q = [16q+1, 16q+16]
+
+__device__ __forceinline__ uint64_t scan_key(float v, int idx) {
+  uint32_t b = __float_as_uint(v + 0.f);  // -0 -> +0: equal values tie, as under the reference's <
+  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return ((uint64_t)b << 32) | (uint32_t)idx;
+}
+
 template <int NB, int NE, int WV, bool FOLD>
 __global__ void __launch_bounds__(64 * WV, 2) k_march16(
     const SdfDev s, const MlpDev m, const float* __restrict__ rays, int64_t P, MarchArgs a,
-    float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
+    int mode, float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
     float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,
-    int32_t* __restrict__ hit_idx, int32_t* __restrict__ hit_count) {
+    unsigned long long* __restrict__ keys) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int lane = lane_id(), r = lane & 31;
+  const int64_t nw = (int64_t)gridDim.x * WV;
+  const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t R = w < P ? (P - 1 - w) / nw + 1 : 0;  // rays owned by this wave
+  const bool scan = mode == 0 && a.primary;
+  const int64_t J = mode == 0 ? R * (scan ? 1 + kScanSegs : 1) : R;
+  const uint32_t lt = (1u << r) - 1u;
   ring::Engine<NB, NE, WV> E;
   E.init(m, smem_c);
-  const int lane = lane_id(), r = lane & 31;
-  const int64_t ray = ((int64_t)blockIdx.x * WV + (threadIdx.x >> 6)) * 32 + r;
-  const bool valid = ray < P;
-  const int64_t rr = valid ? ray : P - 1;
-  const float ox = rays[rr * 6], oy = rays[rr * 6 + 1], oz = rays[rr * 6 + 2];
-  const float dx = rays[rr * 6 + 3], dy = rays[rr * 6 + 4], dz = rays[rr * 6 + 5];
-  float t = 0.f;
-  bool live = valid, hit = false;
-  int i = 0, j = -2, idx = 0;
-  float best = 0.f, thr = 0.f;
+  // lane state: kind -1 = wants a job, -2 = list exhausted, 0 march, 1 scan segment, 2 sdf(best)
+  int kind = -1;
+  int64_t ray = 0;
+  float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
+  float t = 0.f, best = 0.f;
+  int i = 0, j = 0, jend = 0, idx = 0;
+  bool ended = false, hit = false;
+  int64_t cursor = 0;  // wave-uniform
   for (;;) {
-    if (j == -2) {
-      const bool any = (NRT_EXP & 8) || __syncthreads_or(live ? 1 : 0) != 0;
-      if (i >= a.max_steps || !any) {
-        if (!a.primary) break;
-        j = -1;
-      } else {
-        live = live && (t < a.max_t);
+    // retire ended jobs and hand out list entries until every lane has an evaluation to do
+    for (;;) {
+      if (kind == 0) {
+        // sdfs.py:119-131: a march ends on a hit, when t leaves [0, max_t) or after max_steps
+        if (ended || !(t < a.max_t) || i >= a.max_steps) {
+          if (lane < 32) {
+            t_out[ray] = t;
+            hit_out[ray] = hit ? 1 : 0;
+            p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
+            p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
+            p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
+            n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
+            if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+          }
+          kind = -1;
+        }
+      } else if (kind == 1) {
+        if (j > jend) {
+          if (lane < 32) atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
+          kind = -1;
+        }
+      } else if (kind == 2) {
+        if (ended) kind = -1;
       }
+      const uint32_t want = (uint32_t)__ballot(kind == -1);
+      if (want == 0u) break;
+      if (cursor >= J) {
+        if (kind == -1) kind = -2;
+        break;
+      }
+      if (kind == -1) {
+        const int64_t q = cursor + __popc(want & lt);
+        if (q < J) {
+          int64_t k = q;
+          int seg = -1;
+          if (mode == 0 && q >= R) { seg = (int)((q - R) / R); k = (q - R) - (int64_t)seg * R; }
+          ray = w + k * nw;
+          const float* rp = rays + ray * 6;
+          ox = rp[0]; oy = rp[1]; oz = rp[2]; dx = rp[3]; dy = rp[4]; dz = rp[5];
+          ended = false;
+          if (mode == 1) {
+            kind = 2;
+            idx = (int)(uint32_t)keys[ray];
+          } else if (seg < 0) {
+            kind = 0; t = 0.f; i = 0; hit = false;
+          } else {
+            kind = 1;
+            j = seg == 0 ? 0 : 16 * seg + 1;
+            jend = 16 * seg + 16;
+            idx = -1;
+          }
+        } else {
+          kind = -2;
+        }
+      }
+      cursor += __popc(want);
     }
-    float px, py, pz;
-    if (j == -2) {
+    if (__syncthreads_or(kind >= 0 ? 1 : 0) == 0) break;
+    float px = 0.f, py = 0.f, pz = 0.f;
+    if (kind == 0) {
       px = __fadd_rn(ox, __fmul_rn(dx, t));
       py = __fadd_rn(oy, __fmul_rn(dy, t));
       pz = __fadd_rn(oz, __fmul_rn(dz, t));
-    } else if (j == -1) {
-      px = ox; py = oy; pz = oz;
-    } else {
-      float ts = (j < 128) ? (float)(a.step * (double)(j + 1)) : __fmul_rn((float)idx, (float)a.step);
-      px = __fadd_rn(ox, __fmul_rn(ts, dx));
-      py = __fadd_rn(oy, __fmul_rn(ts, dy));
-      pz = __fadd_rn(oz, __fmul_rn(ts, dz));
+    } else if (kind == 1 || kind == 2) {
+      // scan point j: o + (step * j) dir (sdfs.py:241-245); sdf(best): o + (idx * step) dir
+      if (kind == 1 && j == 0) {
+        px = ox; py = oy; pz = oz;
+      } else {
+        const float ts = kind == 1 ? (float)(a.step * (double)j) : __fmul_rn((float)idx, (float)a.step);
+        px = __fadd_rn(ox, __fmul_rn(ts, dx));
+        py = __fadd_rn(oy, __fmul_rn(ts, dy));
+        pz = __fadd_rn(oz, __fmul_rn(ts, dz));
+      }
     }
     float d = (s.kind == 2) ? spheres_value<true>(s, px, py, pz) : 0.f;
     d += ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, px, py, pz);
-    if (j == -2) {
-      const bool now = live && (d <= a.eps);
-      hit = hit || now;
-      live = live && !now;
-      if (live) t = t + d;
+    if (kind == 0) {
+      if (d <= a.eps) { hit = true; ended = true; }
+      else t = t + d;
       ++i;
-    } else if (j == -1) {
-      best = d;
+    } else if (kind == 1) {
+      // sdfs.py:246-248: idx = where(s < m, i + 1, idx); m = min(m, s)
+      if (idx < 0) { best = d; idx = j; }  // first sample of the segment
+      else {
+        if (d < best) idx = j;
+        best = fminf(best, d);
+      }
       ++j;
-    } else if (j < 128) {
-      if (d < best) idx = j + 1;
-      best = fminf(best, d);
-      ++j;
-    } else {
-      thr = -1000.f * d;
-      break;
+    } else if (kind == 2) {
+      if (lane < 32) thr_out[ray] = -1000.f * d;
+      ended = true;
     }
   }
-  if (valid && lane < 32) {
-    t_out[ray] = t;
-    hit_out[ray] = hit ? 1 : 0;
-    p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
-    p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
-    p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
-    n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
-    if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
-    if (a.primary) thr_out[ray] = thr;
-  }
-  if (hit_idx) {
-    const uint64_t mk = __ballot(valid && hit && lane < 32);
-    const int cnt = __popcll(mk);
+}
+
+// hit list of a finished march (order is irrelevant downstream): wave-aggregated appends
+template <int = 0>
+__global__ void k_hit_list(const uint8_t* __restrict__ hit, int64_t P, int32_t* __restrict__ idx,
+                           int32_t* __restrict__ cnt) {
+  const int lane = lane_id();
+  for (int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ray - lane < P;
+       ray += (int64_t)gridDim.x * blockDim.x) {
+    const bool h = ray < P && hit[ray] != 0;
+    const uint64_t mk = __ballot(h);
+    const int c = __popcll(mk);
     int base = 0;
-    if (lane == 0 && cnt) base = atomicAdd(hit_count, cnt);
+    if (lane == 0 && c) base = atomicAdd(cnt, c);
     base = __shfl(base, 0);
-    if (valid && hit && lane < 32) hit_idx[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
+    if (h) idx[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
   }
 }
 

@@ -116,7 +116,9 @@ int ring_dispatch(const nrt_sdf* s, F&& f) {
 
 int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
-               int32_t* cnt, hipStream_t st);
+               int32_t* cnt, unsigned long long* keys, hipStream_t st);
+// workspace of ring_march: one 64-bit scan key per ray
+inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
                  float* n, float* p_io, float eps, hipStream_t st);
 

@@ -1,20 +1,42 @@
-// FP16 march + coarse scan on the block-cooperative LDS weight ring (k_march16).
+// FP16 march + coarse scan on the block-cooperative LDS weight ring (k_march16), load-balanced
+// job lists on a persistent grid; then sdf(best) (mode 1) and the hit list.
 #include "nrt_launch.h"
 
 namespace nrt {
 
 int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
-               int32_t* cnt, hipStream_t st) {
+               int32_t* cnt, unsigned long long* keys, hipStream_t st) {
   const size_t bias_bytes = ring_bias_bytes(s);
-  return ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
+  int dev = 0, cus = 0;
+  NRT_HIP(hipGetDevice(&dev));
+  NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const bool scan = ma.primary != 0;
+  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
+  int rc = ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
     auto kern = k_march16<NB, NE, kRingWaves, FOLD>;
     const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
     if (int rc = set_lds(kern, lds)) return rc;
-    kern<<<dim3(ceil_div64(P, 32 * kRingWaves)), dim3(64 * kRingWaves), lds, st>>>(
-        s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, thr, idx, cnt);
-    return check_launch("k_march16");
+    int per_cu = 0;
+    NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kRingWaves, lds));
+    // persistent grid: every resident block slot, but no more waves than 32-ray tiles
+    const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+    int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 32 * kRingWaves)));
+    // NRT_MARCH_BLOCKS: force the grid (tests check that results do not depend on the schedule)
+    if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
+    for (int mode = 0; mode < (scan ? 2 : 1); ++mode) {
+      kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
+          s->host_dev, s->mlp->host_dev, rays, P, ma, mode, t, hit, p, n, raw_n, thr, keys);
+      if (int rc = check_launch("k_march16")) return rc;
+    }
+    return NRT_OK;
   });
+  if (rc) return rc;
+  if (idx) {
+    k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
+    if (int rc2 = check_launch("k_hit_list")) return rc2;
+  }
+  return NRT_OK;
 }
 
 }  // namespace nrt
