@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+
 namespace nrt {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -56,6 +58,7 @@ struct MlpDev {
   // Softplus MLPs are folded into the log2 domain: z' = log2e * z, a' = log2(1 + 2^z'), so the
   // init layer's W and every init/hidden bias carry a log2e factor and out.weight carries ln2.
   const h8* stream16;              // [frags (+ zero tail)][64 lanes]
+  int stream16_bytes;              // buffer range of stream16 (loads past it return zeros)
   const int* chunk_off;            // first fragment of each chunk
   int n_chunks;
   const float* bias16;             // [layer][bias16_stride] (folded like stream16)
@@ -545,52 +548,129 @@ __device__ __forceinline__ float sp2(float x) {
   return __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(x));
 }
 
+// Chunk schedule of one 8-layer (L hidden, skip period SK) evaluation, fixed at compile time:
+// chunk 0 = the whole init layer (NB row blocks x NE encoding k-steps), chunk 1 + NB i + ib =
+// row block ib of hidden layer i (2NB hidden k-steps, + NE encoding k-steps on skip layers),
+// chunk NCH-1 = the out layer's row block.  The stream16 layout is exactly this order, so a
+// chunk's first fragment is a prefix sum; every index below folds to a constant once eval()
+// is unrolled, and each wave loads and stores only the fragments a chunk has.
+template <int NB, int NE, int L, int SK>
+struct Sched {
+  static constexpr int NCH = 2 + L * NB;
+  static constexpr bool skip(int i) { return i != L - 1 && i % SK == 0; }
+  static constexpr int size(int c) {
+    return c == 0 ? NB * NE : (c == NCH - 1 ? 2 * NB : 2 * NB + (skip((c - 1) / NB) ? NE : 0));
+  }
+  // skip layers among hidden layers 0..i-1 (i <= L - 1, so layer L - 1 is never counted)
+  static constexpr int skips_before(int i) { return (i + SK - 1) / SK; }
+  // closed form (no loops: it must fold to a constant inside the unrolled evaluation)
+  static constexpr int offset(int c) {
+    if (c == 0) return 0;
+    const int i = (c - 1) / NB, ib = (c - 1) % NB;
+    return NB * NE + (c - 1) * 2 * NB + NE * NB * skips_before(i) + (skip(i) ? ib * NE : 0);
+  }
+  static constexpr int max_size() { return NB * NE > 2 * NB + NE ? NB * NE : 2 * NB + NE; }
+};
+
+#ifndef NRT_RING_DEPTH
+#define NRT_RING_DEPTH 4  // ring slots = chunks in flight + 1 (the one being read)
+#endif
+
 template <int NB, int NE, int WV>
 struct Cfg {
-  static constexpr int MAXF = 2 * NB + NE;                // fragments in the largest chunk
+  using S = Sched<NB, NE, 8, 3>;
+  static constexpr int D = NRT_RING_DEPTH;
+  static constexpr int MAXF = S::max_size();              // fragments in the largest chunk
   static constexpr int MAXL = (MAXF + WV - 1) / WV;       // loads per wave per chunk
   static constexpr int SLOTF = MAXL * WV;                 // fragments per ring slot
-  static constexpr int RING_BYTES = 3 * SLOTF * 1024;
+  static constexpr int RING_BYTES = D * SLOTF * 1024;
   // ring SDFs have 3 inputs, no latent and F = 8 (NE - 1) frequencies (2F + 3 slots -> NE k-steps)
   static constexpr int F = 8 * (NE - 1);
   static constexpr int BASIS_BYTES = F * 16;  // float4 (B[0][q], B[1][q], B[2][q], 0) per q
   // LDS of one block: ring | basis | bias16
   static size_t lds_bytes(size_t bias_bytes) { return RING_BYTES + BASIS_BYTES + bias_bytes; }
+  // LDS-DMA instructions one wave issues for chunk c
+  static constexpr int loads(int c) { return (S::size(c % S::NCH) + WV - 1) / WV; }
 };
+
+// s_waitcnt vmcnt(n) lgkmcnt(0) (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4] left at 7,
+// lgkmcnt [11:8])
+__device__ __forceinline__ constexpr int waitcnt_vm_lgkm0(int n) {
+  return (n & 15) | (7 << 4) | (0 << 8) | ((n >> 4) << 14);
+}
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>): chunk indices that are
+// C++ constants (waitcnt immediates, LDS offsets) in a straight-line evaluation
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  [&]<int... I>(std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+  }(std::make_integer_sequence<int, N>{});
+}
+
+// One 1-KiB LDS-DMA piece: lane l's 16 bytes at stream + soff + voff land at LDS m0 + 16 l.
+// Written as asm so hipcc neither drains it with vmcnt(0) before every ring read (it cannot
+// tell the DMA target from the slot being read) nor counts it: the engine waits for it itself.
+// M0 is compiler-reserved, so it is saved and restored inside the statement.
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t srd, int voff, int soff,
+                                          uint32_t lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
 
 template <int NB, int NE, int WV>
 struct Engine {
   using C = Cfg<NB, NE, WV>;
-  h8* ring;                 // LDS [3][SLOTF][64]
+  using S = typename C::S;
+  static constexpr int D = C::D;
+  h8* ring;                 // LDS [D][SLOTF][64]
+  uint32_t ring_lds;        // LDS byte address of the ring
   const float* lbias;       // LDS copy of bias16
   const float4* lbasis;     // LDS copy of the Fourier basis, one float4 per frequency
-  __amdgpu_buffer_rsrc_t srd;  // FP16 weight stream
-  const NRT_CONST int* coff;
-  int nch;
-  int c;                    // chunk held in `slot`
-  int slot;
+  const void* sbase;        // FP16 weight stream (buffer base and range)
+  int sbytes;
+  int slot;                 // ring slot of the current chunk
   int lane, wv;
-  h8 stg[C::MAXL];          // chunk c+1, loaded, not yet written
 
-  __device__ __forceinline__ void load(int chunk) {
-    // buffer_load_dwordx4 v, v[lane*16], s[rsrc], s[frag*1024]: no per-load VALU address math
-    const int off = coff[chunk] + wv;
+  // Wave wv moves fragments wv + WV q (q < loads) of a chunk by LDS-DMA.  Slots hold SLOTF =
+  // MAXL * WV fragments, so in a chunk of n < SLOTF fragments the waves past the end load out
+  // of the buffer's range (the lane offset is pushed past num_records = the stream's size: no
+  // memory access) into the slot's unused tail: the count per wave is compile-time.
+  static constexpr int kOutOfRange = 0x40000000;
+  __device__ __forceinline__ void issue(int c, int s) {
+    // the asm wants SGPR operands: re-assert uniformity (inside the static_for lambdas hipcc
+    // can lose track of it and would otherwise fail with "illegal VGPR to SGPR copy")
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    int base = w * 1024;
+    asm volatile("" : "+s"(base));  // per-chunk s_add in place, not ~130 hoisted constants
+    const int n = S::size(c % S::NCH);
+    const int off = S::offset(c % S::NCH) * 1024 + base;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)(s * C::SLOTF * 1024)) + base;
+    const uint64_t sp = (uint64_t)(uintptr_t)sbase;
+    const uint64_t spu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)spu, 0, __builtin_amdgcn_readfirstlane(sbytes), 0x00020000);
 #pragma unroll
-    for (int q = 0; q < C::MAXL; ++q) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(srd, lane * 16, (off + WV * q) * 1024, 0);
-      stg[q] = __builtin_bit_cast(h8, v);
-    }
+    for (int q = 0; q < C::MAXL; ++q)
+      if (WV * q < n) {
+        const bool own = WV * (q + 1) <= n || w < n - WV * q;
+        lds_dma16(r, own ? lane * 16 : kOutOfRange + lane * 16, off + WV * q * 1024,
+                  dst + WV * q * 1024);
+      }
   }
-  __device__ __forceinline__ void store(int s) {
-    h8* D = ring + s * C::SLOTF * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < C::MAXL; ++q) D[(wv + WV * q) * 64] = stg[q];
-  }
-  __device__ __forceinline__ int nxt(int x) const { return x + 1 == nch ? 0 : x + 1; }
 
-  // block-wide; afterwards slot 0 = chunk 0, stg = chunk 1
+  // block-wide; afterwards chunks 0 .. D-2 are in flight into slots 0 .. D-2
   __device__ __forceinline__ void init(const MlpDev& m, char* lds) {
     ring = reinterpret_cast<h8*>(lds);
+    ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
     float4* lq = reinterpret_cast<float4*>(lds + C::RING_BYTES);
     for (int q = threadIdx.x; q < C::F; q += blockDim.x)
       lq[q] = make_float4(m.basis[q], m.basis[C::F + q], m.basis[2 * C::F + q], 0.f);
@@ -601,33 +681,40 @@ struct Engine {
     for (int i = threadIdx.x; i < nb16; i += blockDim.x) lb[i] = gb[i];
     lbias = lb;
     bstride_ = m.bias16_stride;
-    srd = __builtin_amdgcn_make_buffer_rsrc((void*)m.stream16, 0, 0x7ffffff0, 0x00020000);
-    coff = (const NRT_CONST int*)m.chunk_off;
-    nch = m.n_chunks;
+    sbase = m.stream16;
+    sbytes = m.stream16_bytes;
     lane = threadIdx.x & 63;
     wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    c = 0;
     slot = 0;
-    load(0);
-    store(0);
-    load(nxt(0));
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < D - 1; ++k) issue(k, k);
+    __syncthreads();  // bias / basis copies
   }
-  // start of chunk c: publish chunk c+1, prefetch chunk c+2; returns this lane's A base
+  // start of chunk c (schedule index 0..NCH-1): wait until chunk c has landed in every wave's
+  // share of the slot, then refill the slot read in chunk c-1 with chunk c + D - 1 (the next
+  // evaluation's first chunks near the end); returns this lane's A base.
+  static constexpr int after(int c) {  // this wave's DMAs issued after chunk c's: c+1 .. c+D-2
+    int a = 0;
+    for (int k = 1; k <= D - 2; ++k) a += C::loads(c + k);
+    return a;
+  }
+  template <int CH>
   __device__ __forceinline__ const h8* begin() {
-    const int s1 = slot == 2 ? 0 : slot + 1;
+    constexpr int c = CH;
+    // own DMAs of chunk c landed; own LDS reads (of slot c-1, about to be refilled) retired --
+    // hipcc may leave the last A reads of chunk c-1 in flight past the barrier otherwise
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(after(c)));
+    if (!(NRT_EXP & 1)) __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     if (!(NRT_EXP & 4)) {
-      store(s1);
-      load(nxt(nxt(c)));
+      const int s = slot == 0 ? D - 1 : slot - 1;
+      issue(c + D - 1, s);
     }
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * C::SLOTF * 64 + lane;
   }
-  __device__ __forceinline__ void end() {
-    if (!(NRT_EXP & 1)) __syncthreads();
-    c = nxt(c);
-    slot = slot == 2 ? 0 : slot + 1;
-  }
+  __device__ __forceinline__ void end() { slot = slot == D - 1 ? 0 : slot + 1; }
   __device__ __forceinline__ f16v bias_at(int layer, int ib, int h) const {
     f16v v;
     const float* b = lbias + layer * bstride_ + 32 * ib + 4 * h;
@@ -776,24 +863,26 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
   // work into the MFMA gaps.  A pending tile that the current chain consumes (last row block of
   // the previous layer, k-steps 2NB-2 / 2NB-1) is ordered by the register dependency.
   f16v pend;
-  // init layer: NB chunks over the raw encoding
-#pragma unroll
-  for (int ib = 0; ib < NB; ++ib) {
-    const h8* A = E.begin();
-    f16v acc = bias(0, ib);
-#pragma unroll
-    for (int s = 0; s < NE; ++s) acc = mfma16(A[s * 64], eraw[s], acc);
-    if (ib > 0) act_pack<FOLD, TAN>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act, value);
-    pend = acc;
-    E.end();
-  }
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-    const int src = i & 1, dst = src ^ 1;
-    const bool skip = (i != L - 1) && (i % SK) == 0;
+  // init layer: one chunk of NB row blocks x NE k-steps over the raw encoding
+  {
+    const h8* A = E.template begin<0>();
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) {
-      const h8* A = E.begin();
+      f16v acc = bias(0, ib);
+#pragma unroll
+      for (int s = 0; s < NE; ++s) acc = mfma16(A[(ib * NE + s) * 64], eraw[s], acc);
+      if (ib > 0) act_pack<FOLD, TAN>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act, value);
+      pend = acc;
+    }
+    E.end();
+  }
+  static_for<L>([&](auto I) {
+    constexpr int i = I;
+    constexpr int src = i & 1, dst = src ^ 1;
+    constexpr bool skip = (i != L - 1) && (i % SK) == 0;
+    static_for<NB>([&](auto IB) {
+      constexpr int ib = IB;
+      const h8* A = E.template begin<1 + i * NB + ib>();
       f16v acc = bias(1 + i, ib);
       if (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
 #pragma unroll
@@ -806,10 +895,10 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
       if (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
       pend = acc;
       E.end();
-    }
-  }
+    });
+  });
   // out layer (one 32-row block; output row 0 sits in register 0 of the h == 0 lanes)
-  const h8* A = E.begin();
+  const h8* A = E.template begin<1 + L * NB>();
   f16v acc = bias(L + 1, 0);
   act_pack<FOLD, TAN>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act, value);
 #pragma unroll

@@ -265,6 +265,7 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   }
   md.wout_row0 = reinterpret_cast<const float*>(base + off_w0);
   md.stream16 = reinterpret_cast<const h8*>(base + off_stream);
+  md.stream16_bytes = (int)(stream.size() * sizeof(_Float16));
   md.chunk_off = reinterpret_cast<const int*>(base + off_coff);
   md.n_chunks = n_chunks;
   md.bias16 = reinterpret_cast<const float*>(base + off_b16);
