@@ -29,6 +29,8 @@ sys.path.insert(0, ROOT)
 
 FLOP_SDF_8x256 = 1_120_864  # per evaluation (F=16, in 3, out 1)
 SCAN_EVALS = 130             # sdf(o) + 128 samples + sdf(best)
+# k_march16 evaluates the march and the 129 scan points; sdf(best) is k_scan_best16's
+MARCH_KERNEL_SCAN_EVALS = 129
 PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 
 
@@ -42,7 +44,7 @@ def parse():
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     ap.add_argument("--tile-rows", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-crop", type=int, default=48, help="side of the CPU-baseline crop")
+    ap.add_argument("--cpu-crop", type=int, default=128, help="side of the CPU-baseline crop")
     ap.add_argument("--no-fp32-check", action="store_true")
     return ap.parse_args()
 
@@ -177,7 +179,8 @@ def main():
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
-        k_ms, k_n = _lib.profile_read("k_intersect")
+        k_ms, k_n = _lib.profile_read("k_march16")
+        i_ms, i_n = _lib.profile_read("k_intersect")
         if world > 1:
             t = torch.tensor([elapsed], device=device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -187,12 +190,15 @@ def main():
     rays_per_rank = len(rows) * size * world  # this rank's rows of every view
     rays_total = world * size * size * args.steps
     value = rays_total * args.samples / elapsed
-    flop_launch = rays_per_rank * (args.samples + SCAN_EVALS) * FLOP_SDF_8x256
+    # algorithmic FLOP of one k_march16 launch: every ray at every march step and every scan
+    # point, the reference's own count (sdfs.py:119-131, 232-249); the lane-level job lists
+    # lower the executed work, not this count
+    flop_launch = rays_per_rank * (args.samples + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
     avg_kernel_ms = k_ms / max(k_n, 1)
     achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_intersect.json")
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
@@ -237,7 +243,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "k_intersect",
+                "kernel": "k_march16",
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",
@@ -246,6 +252,7 @@ def main():
                 "flop_per_launch": flop_launch,
                 "avg_kernel_ms": avg_kernel_ms,
                 "launches": k_n,
+                "intersect_ms": i_ms / max(i_n, 1),
             },
             "sdf_evals_per_s": rays_total * (args.samples + SCAN_EVALS) / elapsed,
         }

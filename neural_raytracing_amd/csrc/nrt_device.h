@@ -621,8 +621,7 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t srd, int voff, 
       "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(voff), "s"(srd), "s"(lds_addr), "s"(soff)
-      : "memory");
+      : "v"(voff), "s"(srd), "s"(lds_addr), "s"(soff));
 }
 
 template <int NB, int NE, int WV>
@@ -644,6 +643,35 @@ struct Engine {
   // of the buffer's range (the lane offset is pushed past num_records = the stream's size: no
   // memory access) into the slot's unused tail: the count per wave is compile-time.
   static constexpr int kOutOfRange = 0x40000000;
+  // piece q of chunk c into slot s (see issue())
+  __device__ __forceinline__ void piece(int c, int s, int q) {
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    int base = w * 1024;
+    asm volatile("" : "+s"(base));
+    const int n = S::size(c % S::NCH);
+    const int off = S::offset(c % S::NCH) * 1024 + base;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)(s * C::SLOTF * 1024)) + base;
+    const uint64_t sp = (uint64_t)(uintptr_t)sbase;
+    const uint64_t spu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)spu, 0, __builtin_amdgcn_readfirstlane(sbytes), 0x00020000);
+    const bool own = WV * (q + 1) <= n || w < n - WV * q;
+    lds_dma16(r, own ? lane * 16 : kOutOfRange + lane * 16, off + WV * q * 1024, dst + WV * q * 1024);
+  }
+  // Spread the refill of chunk CH's predecessor slot over chunk CH's MFMA chain: call at every
+  // MFMA index k < nm of the chunk; piece q goes out at k = (2q + 1) nm / (2 pieces).  Issuing
+  // all pieces right after the barrier makes every wave of the block queue on the texture unit at
+  // once, stalling their MFMA issue.
+  template <int CH>
+  __device__ __forceinline__ void dma_at(int k, int nm) {
+    if (NRT_EXP & 4) return;
+    constexpr int c = CH + D - 1;
+    const int pieces = C::loads(c);
+#pragma unroll
+    for (int q = 0; q < C::MAXL; ++q)
+      if (q < pieces && k == (2 * q + 1) * nm / (2 * pieces)) piece(c, slot == 0 ? D - 1 : slot - 1, q);
+  }
   __device__ __forceinline__ void issue(int c, int s) {
     // the asm wants SGPR operands: re-assert uniformity (inside the static_for lambdas hipcc
     // can lose track of it and would otherwise fail with "illegal VGPR to SGPR copy")
@@ -707,10 +735,6 @@ struct Engine {
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(after(c)));
     if (!(NRT_EXP & 1)) __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (!(NRT_EXP & 4)) {
-      const int s = slot == 0 ? D - 1 : slot - 1;
-      issue(c + D - 1, s);
-    }
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * C::SLOTF * 64 + lane;
   }
@@ -870,7 +894,10 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
     for (int ib = 0; ib < NB; ++ib) {
       f16v acc = bias(0, ib);
 #pragma unroll
-      for (int s = 0; s < NE; ++s) acc = mfma16(A[(ib * NE + s) * 64], eraw[s], acc);
+      for (int s = 0; s < NE; ++s) {
+        acc = mfma16(A[(ib * NE + s) * 64], eraw[s], acc);
+        E.template dma_at<0>(ib * NE + s, NB * NE);
+      }
       if (ib > 0) act_pack<FOLD, TAN>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act, value);
       pend = acc;
     }
@@ -885,12 +912,18 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
       const h8* A = E.template begin<1 + i * NB + ib>();
       f16v acc = bias(1 + i, ib);
       if (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
+      constexpr int nm = 2 * NB + (skip ? NE : 0);
 #pragma unroll
-      for (int s = 0; s < 2 * NB; ++s)
+      for (int s = 0; s < 2 * NB; ++s) {
         acc = mfma16((NRT_EXP & 16) ? hv[src][(s + 1) % (2 * NB)] : A[s * 64], hv[src][s], acc);
+        E.template dma_at<1 + i * NB + ib>(s, nm);
+      }
       if (skip) {
 #pragma unroll
-        for (int s = 0; s < NE; ++s) acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
+        for (int s = 0; s < NE; ++s) {
+          acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
+          E.template dma_at<1 + i * NB + ib>(2 * NB + s, nm);
+        }
       }
       if (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
       pend = acc;
@@ -902,7 +935,10 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
   f16v acc = bias(L + 1, 0);
   act_pack<FOLD, TAN>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act, value);
 #pragma unroll
-  for (int s = 0; s < 2 * NB; ++s) acc = mfma16(A[s * 64], hv[L & 1][s], acc);
+  for (int s = 0; s < 2 * NB; ++s) {
+    acc = mfma16(A[s * 64], hv[L & 1][s], acc);
+    E.template dma_at<1 + L * NB>(s, 2 * NB);
+  }
   E.end();
   return __shfl(acc[0], E.lane & 31);
 }

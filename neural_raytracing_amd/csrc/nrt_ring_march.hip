@@ -14,21 +14,23 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
   const bool scan = ma.primary != 0;
   if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   int rc = ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
-    auto kern = k_march16<NB, NE, kRingWaves, FOLD>;
-    const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
-    if (int rc = set_lds(kern, lds)) return rc;
-    int per_cu = 0;
-    NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kRingWaves, lds));
-    // persistent grid: every resident block slot, but no more waves than 32-ray tiles
-    const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
-    int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 32 * kRingWaves)));
-    // NRT_MARCH_BLOCKS: force the grid (tests check that results do not depend on the schedule)
-    if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
-    for (int mode = 0; mode < (scan ? 2 : 1); ++mode) {
+    auto launch = [&](auto kern, const char* name) -> int {
+      const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
+      if (int rc = set_lds(kern, lds)) return rc;
+      int per_cu = 0;
+      NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kRingWaves, lds));
+      // persistent grid: every resident block slot, but no more waves than 32-ray tiles
+      const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+      int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 32 * kRingWaves)));
+      // NRT_MARCH_BLOCKS: force the grid (tests check that results do not depend on the schedule)
+      if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
+      ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, ma, mode, t, hit, p, n, raw_n, thr, keys);
-      if (int rc = check_launch("k_march16")) return rc;
-    }
+          s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, thr, keys);
+      return check_launch(name);
+    };
+    if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
+    if (scan) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
     return NRT_OK;
   });
   if (rc) return rc;

@@ -1,10 +1,11 @@
-"""Build timing-only variants of libnrt_hip.so (NRT_EXP bits, nrt_device.h) into build_var/.
+"""Build timing variants of libnrt_hip.so into build_var/ (one box session then times them all).
 
-Only the SDF translation units are recompiled; the others come from the normal build.  Variants
-compute wrong results on purpose (no barrier, no activation, ...) and exist to price one
-component of the march kernel: never ship or test them.  Usage:
-    python tools/exp_variants.py 8 9 10 12 24
-then on the box:  NRT_LIB=build_var/libnrt_hip_e9.so python bench.py ...
+A variant is NAME=FLAGS, e.g.  e1=-DNRT_EXP=1  d3=-DNRT_RING_DEPTH=3.  Only the SDF translation
+units are recompiled; the others come from the normal build.  NRT_EXP variants compute wrong
+results on purpose (no barrier, no activation, ...) and exist to price one component of the
+march kernel: never ship or test them.  Usage:
+    python tools/exp_variants.py e1=-DNRT_EXP=1 d3=-DNRT_RING_DEPTH=3
+then on the box:  bash tools/exp_run.sh e1 d3
 """
 import os
 import subprocess
@@ -23,19 +24,21 @@ others = [os.path.join(B.OBJDIR, os.path.splitext(s)[0] + ".o") for s in B.SOURC
           if s not in VARIED]
 
 
-def one(v):
-    objs = []
-    for src in VARIED:
-        obj = os.path.join(out, f"{os.path.splitext(src)[0]}_e{v}.o")
-        subprocess.run(["/opt/rocm/bin/hipcc", *B.FLAGS, f"-DNRT_EXP={v}", "-c",
-                        os.path.join(B.CSRC, src), "-o", obj], check=True)
-        objs.append(obj)
-    lib = os.path.join(out, f"libnrt_hip_e{v}.so")
+def compile_one(job):
+    name, flags, src = job
+    obj = os.path.join(out, f"{os.path.splitext(src)[0]}_{name}.o")
+    subprocess.run(["/opt/rocm/bin/hipcc", *B.FLAGS, *flags.split(), "-c",
+                    os.path.join(B.CSRC, src), "-o", obj], check=True)
+    return obj
+
+
+variants = [a.split("=", 1) for a in sys.argv[1:]]
+jobs = [(n, f, src) for n, f in variants for src in VARIED]
+with ThreadPoolExecutor(8) as ex:
+    objs = list(ex.map(compile_one, jobs))
+for i, (name, _) in enumerate(variants):
+    lib = os.path.join(out, f"libnrt_hip_{name}.so")
+    mine = objs[i * len(VARIED):(i + 1) * len(VARIED)]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib,
-                    *objs, *others], check=True)
-    return lib
-
-
-with ThreadPoolExecutor(4) as ex:
-    for lib in ex.map(one, [int(a) for a in sys.argv[1:]]):
-        print(lib)
+                    *mine, *others], check=True)
+    print(lib)

@@ -1,18 +1,25 @@
-# GPU round script: tests, smoke, bench, rocprof (each step time-limited; stop at first failure)
+# GPU round script: tests, smoke, bench, rocprof, PMC traffic (each step time-limited; stop at
+# the first failure).  bash tools/run_gpu_round.sh [all|tests|bench|prof|pmc]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 STEP=${1:-all}
+mkdir -p gpurun_out
 if [ "$STEP" = all ] || [ "$STEP" = tests ]; then
-  timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+  timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "TESTS EXIT $rc"; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  rc=$?; echo "SMOKE EXIT $rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$STEP" = all ] || [ "$STEP" = bench ]; then
-  timeout -k 10 600 python bench.py --steps 3 --warmup 1 > gpurun_out/bench.log 2>&1
-  rc=$?; echo "BENCH EXIT $rc"; tail -3 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 600 python -u bench.py > gpurun_out/bench.log 2>&1
+  rc=$?; echo "BENCH EXIT $rc"; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fp32-check > gpurun_out/prof.log 2>&1
-  rc=$?; echo "PROF EXIT $rc"; tail -2 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
-  find gpurun_out/prof -name "*stats*" | head
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-fp32-check > gpurun_out/prof.log 2>&1
+  rc=$?; echo "PROF EXIT $rc"; tail -1 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$STEP" = all ] || [ "$STEP" = pmc ]; then
+  rm -rf gpurun_out/pmc
+  SIZE=800 bash tools/pmc.sh k_march16 "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" || exit 1
 fi
