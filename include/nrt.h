@@ -171,6 +171,20 @@ int nrt_shade_direct(const nrt_bsdf* bsdf, const nrt_light* light, const float* 
                      const int32_t* hit_count, int64_t P, float* rgb, float* weights_out,
                      int precision, void* stream);
 
+/* Direct.sample with w_isect=True (integrators.py:163 -> sample_emitter_dir_w_isect,
+ * scene.py:290-298): for each listed hit ray, a point-light sample, a shadow ray
+ * [p, d_light] marched like SDF.intersect_test (sdfs.py:162-181; t0 = 100*eps, max_steps,
+ * max_t = light distance), Le = 0 where occluded, then the shading of nrt_shade_direct.
+ * visible_out [P] (optional) receives the visibility per hit-list position.  Needs a point light
+ * (NRT_EUNSUPPORTED otherwise: the reference's LightField samples carry no distance).
+ * workspace: nrt_shadow_workspace_bytes(P) bytes of device memory. */
+size_t nrt_shadow_workspace_bytes(int64_t P);
+int nrt_shade_direct_shadowed(const nrt_bsdf* bsdf, const nrt_light* light, const nrt_sdf* sdf,
+                              int32_t max_steps, float epsilon, const float* p, const float* n,
+                              const float* wi, const int32_t* hit_idx, const int32_t* hit_count,
+                              int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
+                              void* workspace, int precision, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Cameras (cameras/cameras.py) and the tile composite (main.py:85-90, integrators.py:251)
  * ------------------------------------------------------------------------------------- */

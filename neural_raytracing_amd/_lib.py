@@ -76,6 +76,9 @@ _SIGNATURES = {
     "nrt_bsdf_create": (_I32, [_I32, _P, _P, ctypes.POINTER(_P)]),
     "nrt_bsdf_destroy": (_I32, [_P]),
     "nrt_shade_direct": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I32, _P]),
+    "nrt_shadow_workspace_bytes": (ctypes.c_size_t, [_I64]),
+    "nrt_shade_direct_shadowed": (_I32, [_P, _P, _P, _I32, _F, _P, _P, _P, _P, _P, _I64, _P, _P,
+                                         _P, _P, _I32, _P]),
     "nrt_raygen": (_I32, [_P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P]),
     "nrt_frames": (_I32, [_P, _P, _I64, _P, _P, _P]),
     "nrt_profile_enable": (None, [_I32]),

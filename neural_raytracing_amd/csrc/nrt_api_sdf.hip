@@ -232,29 +232,41 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   return NRT_OK;
 }
 
+}  // extern "C"
+
+namespace nrt {
+// shadow march over rays[0, P) (or [0, *count) when count is a device counter)
+int launch_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const int32_t* count,
+                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible, bool f16,
+                     hipStream_t st) {
+  int hidden, ke;
+  sdf_dims(s, hidden, ke);
+  LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
+  dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
+  int rc = NRT_OK;
+  ProfScope prof("k_occlusion", st);
+  NRT_NB_SWITCH(s->host_dev.nb, {
+    if (f16) {
+      if (!(rc = set_lds(k_occlusion<true, NB>, lp.bytes)))
+        k_occlusion<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, count, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
+    } else {
+      if (!(rc = set_lds(k_occlusion<false, NB>, lp.bytes)))
+        k_occlusion<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, count, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
+    }
+  });
+  if (rc) return rc;
+  return check_launch("k_occlusion");
+}
+}  // namespace nrt
+
+extern "C" {
 int nrt_sdf_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const float* max_t,
                       int32_t max_steps, float eps, uint8_t* visible, int precision, void* stream) {
   if (!s || P < 0) { set_error("nrt_sdf_occlusion: bad argument"); return NRT_EINVAL; }
   if (P == 0) return NRT_OK;
   if (!rays || !max_t || !visible) { set_error("nrt_sdf_occlusion: null argument"); return NRT_EINVAL; }
-  const bool f16 = precision == NRT_FP16;
-  int hidden, ke;
-  sdf_dims(s, hidden, ke);
-  LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
-  dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
-  hipStream_t st = (hipStream_t)stream;
-  int rc = NRT_OK;
-  NRT_NB_SWITCH(s->host_dev.nb, {
-    if (f16) {
-      if (!(rc = set_lds(k_occlusion<true, NB>, lp.bytes)))
-        k_occlusion<true, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
-    } else {
-      if (!(rc = set_lds(k_occlusion<false, NB>, lp.bytes)))
-        k_occlusion<false, NB><<<grid, block, lp.bytes, st>>>(s->dev, rays, P, max_t, max_steps, eps, visible, lp.RS, lp.per_wave);
-    }
-  });
-  if (rc) return rc;
-  return check_launch("k_occlusion");
+  return launch_occlusion(s, rays, P, nullptr, max_t, max_steps, eps, visible,
+                          precision == NRT_FP16, (hipStream_t)stream);
 }
 
 int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi, void* stream) {

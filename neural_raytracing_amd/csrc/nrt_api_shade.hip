@@ -92,15 +92,12 @@ int nrt_bsdf_destroy(nrt_bsdf* b) {
   return NRT_OK;
 }
 
-int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
-                     const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                     float* rgb, float* weights_out, int precision, void* stream) {
-  if (!b || !l || !p || !n || !wi || !hit_idx || !hit_count || !rgb || P < 0) {
-    set_error("nrt_shade_direct: bad argument");
-    return NRT_EINVAL;
-  }
-  if (P == 0) return NRT_OK;
-  const bool f16 = precision == NRT_FP16;
+}  // extern "C"
+
+namespace {
+int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
+                      const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+                      const uint8_t* vis, float* rgb, float* weights_out, bool f16, hipStream_t st) {
   int hidden = 32, ke = 16;
   auto upd = [&](const nrt_mlp* m) {
     if (!m) return;
@@ -110,11 +107,10 @@ int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, cons
   upd(l->mlp);
   upd(b->spatial);
   for (auto* m : b->mlps) upd(m);
-  hipStream_t st = (hipStream_t)stream;
   // FP16: light field, spatial weights and NeuralBSDFs on the program engine when compiled for
   // their shapes (NRT_NO_PROGRAM keeps the per-wave register path)
   if (f16 && std::getenv("NRT_NO_PROGRAM") == nullptr) {
-    const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, rgb, weights_out, st);
+    const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, vis, rgb, weights_out, st);
     if (rc != NRT_EUNSUPPORTED) return rc;
   }
   LdsPlan lp = plan_lds(hidden, ke, 64, f16, false);
@@ -123,13 +119,63 @@ int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, cons
   if (f16) {
     if (int rc = set_lds(k_shade_direct<true>, lp.bytes)) return rc;
     k_shade_direct<true><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
-        b->dev, l->dev, p, n, wi, hit_idx, hit_count, rgb, weights_out, lp.RS, lp.per_wave);
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, vis, rgb, weights_out, lp.RS, lp.per_wave);
   } else {
     if (int rc = set_lds(k_shade_direct<false>, lp.bytes)) return rc;
     k_shade_direct<false><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
-        b->dev, l->dev, p, n, wi, hit_idx, hit_count, rgb, weights_out, lp.RS, lp.per_wave);
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, vis, rgb, weights_out, lp.RS, lp.per_wave);
   }
   return check_launch("k_shade_direct");
 }
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+}  // namespace
+
+extern "C" {
+int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
+                     const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+                     float* rgb, float* weights_out, int precision, void* stream) {
+  if (!b || !l || !p || !n || !wi || !hit_idx || !hit_count || !rgb || P < 0) {
+    set_error("nrt_shade_direct: bad argument");
+    return NRT_EINVAL;
+  }
+  if (P == 0) return NRT_OK;
+  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, nullptr, rgb, weights_out,
+                           precision == NRT_FP16, (hipStream_t)stream);
+}
+
+size_t nrt_shadow_workspace_bytes(int64_t P) {
+  P = std::max<int64_t>(P, 1);
+  return align256((size_t)P * 6 * 4) + align256((size_t)P * 4) + align256((size_t)P);
+}
+
+int nrt_shade_direct_shadowed(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s,
+                              int32_t max_steps, float eps, const float* p, const float* n,
+                              const float* wi, const int32_t* hit_idx, const int32_t* hit_count,
+                              int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
+                              void* workspace, int precision, void* stream) {
+  if (!b || !l || !s || !p || !n || !wi || !hit_idx || !hit_count || !rgb || P < 0 || !workspace) {
+    set_error("nrt_shade_direct_shadowed: bad argument");
+    return NRT_EINVAL;
+  }
+  if (l->host_dev.kind != 1) {
+    // the reference's LightField samples carry no distance, so its shadow test cannot run
+    set_error("nrt_shade_direct_shadowed: shadow rays need a point light (LightField samples "
+              "have no distance, lights.py:175-195)");
+    return NRT_EUNSUPPORTED;
+  }
+  if (P == 0) return NRT_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const bool f16 = precision == NRT_FP16;
+  char* ws = (char*)workspace;
+  float* rays = (float*)ws;
+  float* max_t = (float*)(ws + align256((size_t)P * 24));
+  uint8_t* vis = visible_out ? visible_out
+                             : (uint8_t*)(ws + align256((size_t)P * 24) + align256((size_t)P * 4));
+  k_point_shadow_rays<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(
+      l->dev, p, hit_idx, hit_count, rays, max_t);
+  if (int rc = check_launch("k_point_shadow_rays")) return rc;
+  if (int rc = launch_occlusion(s, rays, P, hit_count, max_t, max_steps, eps, vis, f16, st)) return rc;
+  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, vis, rgb, weights_out, f16, st);
+}
 }  // extern "C"

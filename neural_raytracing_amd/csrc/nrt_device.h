@@ -911,7 +911,7 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
       constexpr int ib = IB;
       const h8* A = E.template begin<1 + i * NB + ib>();
       f16v acc = bias(1 + i, ib);
-      if (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
+      if constexpr (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
       constexpr int nm = 2 * NB + (skip ? NE : 0);
 #pragma unroll
       for (int s = 0; s < 2 * NB; ++s) {
@@ -925,7 +925,7 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
           E.template dma_at<1 + i * NB + ib>(2 * NB + s, nm);
         }
       }
-      if (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
+      if constexpr (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
       pend = acc;
       E.end();
     });

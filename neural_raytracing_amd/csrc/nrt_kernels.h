@@ -609,6 +609,7 @@ __global__ void k_frame_wi(const float* __restrict__ rays, const float* __restri
 template <bool F16, int NB>
 __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_occlusion(const SdfDev* __restrict__ sp,
                                                     const float* __restrict__ rays, int64_t P,
+                                                    const int32_t* __restrict__ count,
                                                     const float* __restrict__ max_t, int max_steps,
                                                     float eps, uint8_t* __restrict__ visible,
                                                     int RS, int per_wave) {
@@ -616,6 +617,7 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_occlusion(const SdfDev* __
   const SdfDev& s = *sp;
   WaveLds l = wave_lds(smem, per_wave, RS, F16);
   const int lane = lane_id(), r = lane & 31;
+  if (count) P = min(P, (int64_t)*count);  // a compacted list (shadow rays of the hit list)
   const int64_t ray0 = wave_global() * 32;
   if (ray0 >= P) return;
   const int64_t ray = ray0 + r;
@@ -636,6 +638,29 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_occlusion(const SdfDev* __
     live = live && !now;
   }
   if (valid && lane < 32) visible[ray] = ((t >= max_t[ray]) || live) ? 1 : 0;
+}
+
+// shadow rays toward a point light for each hit-list position i (sample_emitter_dir_w_isect,
+// scene.py:290-298 with PointLights.sample_direction, lights.py:89-110): [p, normalize(loc - p)],
+// max_t = |loc - p|
+template <int = 0>
+__global__ void k_point_shadow_rays(const LightDev* __restrict__ lp, const float* __restrict__ P_,
+                                    const int32_t* __restrict__ hit_idx,
+                                    const int32_t* __restrict__ hit_count,
+                                    float* __restrict__ rays, float* __restrict__ max_t) {
+  const int64_t total = *hit_count;
+  const LightDev& lt = *lp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t idx = hit_idx[i];
+    const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
+    float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
+    const float dist = sqrtf(vx * vx + vy * vy + vz * vz);
+    normalize3(vx, vy, vz, 1e-6f);
+    float* o = rays + i * 6;
+    o[0] = px; o[1] = py; o[2] = pz; o[3] = vx; o[4] = vy; o[5] = vz;
+    max_t[i] = dist;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -691,8 +716,8 @@ template <bool F16>
 __global__ void __launch_bounds__(256) k_shade_direct(
     const BsdfDev* __restrict__ bp, const LightDev* __restrict__ lp, const float* __restrict__ P_,
     const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
-    const int32_t* __restrict__ hit_count, float* __restrict__ rgb, float* __restrict__ wout,
-    int RS, int per_wave) {
+    const int32_t* __restrict__ hit_count, const uint8_t* __restrict__ vis,
+    float* __restrict__ rgb, float* __restrict__ wout, int RS, int per_wave) {
   extern __shared__ float smem[];
   const BsdfDev& bs = *bp;
   const LightDev& lt = *lp;
@@ -783,6 +808,7 @@ __global__ void __launch_bounds__(256) k_shade_direct(
       }
       wave_lds_fence();
     }
+    if (vis && !vis[valid ? i : total - 1]) le[0] = le[1] = le[2] = 0.f;  // scene.py:297
     if (valid && lane < 32) {
       // integrators.py:186-189: mis(=1) * bsdf_val * emitter_val, / emitter_samples(=1)
       rgb[idx * 3] = (1.f * f[0]) * le[0];
@@ -823,7 +849,7 @@ template <int WV, bool FIELD>
 __global__ void __launch_bounds__(64 * WV, 1) k_light16(
     const ProgDev prog, const LightDev* __restrict__ lp, const float* __restrict__ P_,
     const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
-    const int32_t* __restrict__ hit_count, float* __restrict__ LS) {
+    const int32_t* __restrict__ hit_count, const uint8_t* __restrict__ vis, float* __restrict__ LS) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const LightDev& lt = *lp;
   const int64_t total = *(const NRT_GLOBAL int32_t*)hit_count;
@@ -857,6 +883,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_light16(
       to_local(fr, ldx, ldy, ldz, wo);
       rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
     }
+    if (vis && !vis[valid ? i : total - 1]) le[0] = le[1] = le[2] = 0.f;  // scene.py:297
     if (valid && lane < 32) {
       float* o = LS + i * kLsStride;
       o[0] = le[0]; o[1] = le[1]; o[2] = le[2];

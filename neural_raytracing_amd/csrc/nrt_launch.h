@@ -122,12 +122,16 @@ inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
                  float* n, float* p_io, float eps, hipStream_t st);
 
+int launch_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const int32_t* count,
+                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible, bool f16,
+                     hipStream_t st);
+
 // ---- shading programs (nrt_prog.hip) ----
 int build_program(const std::vector<const nrt_mlp*>& mlps, nrt_prog& out);
 int build_light_program(nrt_light* l);
 int build_bsdf_program(nrt_bsdf* b);
 int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                   const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                  float* rgb, float* weights_out, hipStream_t st);
+                  const uint8_t* vis, float* rgb, float* weights_out, hipStream_t st);
 
 }  // namespace nrt

@@ -118,8 +118,9 @@ class Direct(Integrator):
     def sample(self, shapes, rays, bsdf, **kwargs):
         lights = kwargs.get("lights", self.lights)
         w_isect = kwargs.get("w_isect")
-        if w_isect not in (None, False):
-            raise _lib.NrtError("Direct(w_isect=...) shadow rays are not on the HIP path yet")
+        if w_isect not in (None, False, True):
+            raise _lib.NrtError("Direct(w_isect=<occlusion MLP>) (learned occlusion, "
+                                "scene.py:301-319) is not on the HIP path yet")
         if self.emitter_samples != 1 or self.bsdf_samples != 0:
             raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
         result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
@@ -129,10 +130,22 @@ class Direct(Integrator):
         rgb = result.reshape(P, 3)
         nb = len(getattr(bsdf, "bsdfs", [bsdf]))
         weights = torch.zeros(P, nb, device=rays.device)
-        _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights),
-                  _lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
-                  _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
-                  _lib.ptr(rgb), _lib.ptr(weights), _lib.precision_code(), _lib.stream())
+        args = (_lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
+                _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
+                _lib.ptr(rgb), _lib.ptr(weights))
+        if w_isect is True:
+            # sample_emitter_dir_w_isect (scene.py:290-298): shadow ray to the point light,
+            # marched like SDF.intersect_test (sdfs.py:162-181)
+            from ..shapes.sdfs import sdf_handle
+            lib = _lib.load(require_device=True)
+            ws = torch.empty(lib.nrt_shadow_workspace_bytes(P), dtype=torch.uint8,
+                             device=rays.device)
+            _lib.call("nrt_shade_direct_shadowed", _bsdf_handle(bsdf), _light_handle(lights),
+                      sdf_handle(shapes.sdf), int(shapes.max_steps), float(shapes.epsilon),
+                      *args, None, _lib.ptr(ws), _lib.precision_code(), _lib.stream())
+        else:
+            _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), *args,
+                      _lib.precision_code(), _lib.stream())
         setattr(it, "normalized_weights", weights.reshape(rays.shape[:-1] + (nb,)))
         return result, active, it
 

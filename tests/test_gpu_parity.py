@@ -516,3 +516,85 @@ def test_ring_march_schedule_invariant(monkeypatch):
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert torch.equal(a, b)
+
+
+def _shadow_scene():
+    """A large sphere with a small one floating between it and a point light (it casts a shadow
+    on the large one); Diffuse BSDF; NeRF camera.  Oracle and product objects, same numbers."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import Diffuse
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    seeded(3)
+    ref = R.SphereBlobSDF(n=2, shift_zero_init=True)
+    with torch.no_grad():
+        ref.centers.copy_(torch.tensor([[0.0, 0.0, 0.0], [0.05, 0.45, 0.12]]))
+        ref.radii.copy_(torch.tensor([0.3, 0.1]))
+    mine = SphereSDF(n=2, device="cpu")
+    with torch.no_grad():
+        mine.centers.copy_(ref.centers)
+        mine.radii.copy_(ref.radii)
+    copy_mlp(mine.shift, ref.shift)
+    loc = (0.15, 1.4, 0.4)
+    c2w = recipes.look_at_c2w((0.0, 0.7, 0.9)).unsqueeze(0)
+    focal = recipes.nerf_focal(64)
+    oracle = dict(shape=R.MarchedSDF(sdf=ref, max_steps=48), bsdf=R.DiffuseRef(),
+                  lights=R.PointLightRef(location=loc, scale=5.0),
+                  camera=R.NeRFCameraRef(c2w, focal))
+    prod = dict(shape=SDF(sdf=mine.cuda(), max_steps=48), bsdf=Diffuse(device="cuda"),
+                lights=PointLights(location=list(loc), scale=5.0, device="cuda"),
+                camera=pt.cameras.NeRFCamera(cam_to_world=c2w.cuda(), focal=focal, device="cuda"))
+    return oracle, prod
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_direct_shadow_rays_match_oracle(prec):
+    """Direct with w_isect=True (sample_emitter_dir_w_isect, scene.py:290-298 + intersect_test,
+    sdfs.py:162-181): HIP shadow march + masked shading vs the oracle.  FP32 within 1e-4 except
+    at most 0.5 % of pixels (shadow-boundary flips from ulp-level march differences); FP16 by
+    PSNR."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    ref, mine = _shadow_scene()
+    imgs = {}
+    for w_isect in (False, True):
+        random.seed(8)
+        with torch.no_grad():
+            imgs[w_isect] = R.render(ref["shape"], ref["lights"], ref["camera"], R.DirectRef(),
+                                     ref["bsdf"], size=64, chunk_size=64, background=0.0,
+                                     with_noise=0.0, w_isect=w_isect)
+    shadowed = (imgs[False] - imgs[True]).abs().amax(-1) > 1e-3
+    assert shadowed.sum() > 40, "the scene must cast a shadow for this test to mean anything"
+    set_precision(prec)
+    random.seed(8)
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                                     bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
+                                     crop_size=64, uv=(0, 0), background=0, with_noise=0.0,
+                                     w_isect=True)
+    got = got.cpu()
+    want = imgs[True]
+    assert got.shape == want.shape
+    if prec == "fp32":
+        close = (got - want).abs().amax(-1) <= 1e-4
+        assert close.float().mean() >= 0.995, (got - want).abs().max()
+    else:
+        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
+        assert -10 * math.log10(max(mse, 1e-12)) > 40
+
+
+def test_direct_shadow_rays_need_point_light():
+    """The reference's LightField samples carry no distance (lights.py:175-195), so
+    w_isect=True cannot run with it there; the HIP path refuses it loudly."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import NrtError
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    from neural_raytracing_amd.pathtracer.lights import LightField
+    _, mine = _shadow_scene()
+    with pytest.raises(NrtError):
+        with torch.no_grad():
+            pt.pathtrace_sample(mine["shape"], LightField(device="cuda"), mine["camera"], Direct(),
+                                bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
+                                crop_size=32, uv=(0, 0), background=0, with_noise=0.0,
+                                w_isect=True)
