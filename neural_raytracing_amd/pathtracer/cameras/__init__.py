@@ -1,1 +1,2 @@
-from .cameras import Camera, DTUCamera, NeRFCamera  # noqa: F401
+from .cameras import (Camera, DTUCamera, FoVPerspectiveCameras, NeRFCamera,  # noqa: F401
+                      OpenGLPerspectiveCameras, look_at_view_transform)

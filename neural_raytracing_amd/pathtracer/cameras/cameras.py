@@ -1,8 +1,11 @@
 """Cameras (cameras/cameras.py).  Primary rays come from the HIP kernel ``nrt_raygen``."""
 import ctypes
+import math
 from dataclasses import dataclass
 
+import numpy as np
 import torch
+import torch.nn.functional as F
 
 from ... import _lib
 
@@ -74,6 +77,144 @@ class NeRFCamera(Camera):
         W, H, _ = position_samples.shape
         pos = position_samples.float().contiguous()
         return self.rays_tile(0, 0, W, H, size, with_noise, positions=pos)
+
+
+def _f32(v, device="cpu"):
+    t = v if torch.is_tensor(v) else torch.tensor(v, dtype=torch.float32)
+    return t.to(device=device, dtype=torch.float32).reshape(-1)
+
+
+def look_at_view_transform(dist=1.0, elev=0.0, azim=0.0, degrees=True, eye=None,
+                           at=((0, 0, 0),), up=((0, 1, 0),), device="cpu"):
+    """R [N,3,3], T [N,3] of the look-at world -> view transform (renderer/cameras.py:1363-1422,
+    with camera_position_from_spherical_angles :1275-1310 and look_at_rotation :1313-1360).
+    Host-side float32 math on the camera parameters, as in the reference."""
+    at = torch.tensor(at, dtype=torch.float32).reshape(-1, 3)
+    up = torch.tensor(up, dtype=torch.float32).reshape(-1, 3)
+    if eye is not None:
+        C = torch.tensor(eye, dtype=torch.float32).reshape(-1, 3)
+    else:
+        dist, elev, azim = _f32(dist), _f32(elev), _f32(azim)
+        if degrees:
+            elev = math.pi / 180.0 * elev
+            azim = math.pi / 180.0 * azim
+        C = torch.stack([dist * torch.cos(elev) * torch.sin(azim), dist * torch.sin(elev),
+                         dist * torch.cos(elev) * torch.cos(azim)], dim=1).view(-1, 3) + at
+    n = max(C.shape[0], at.shape[0], up.shape[0])
+    C, at, up = C.expand(n, 3), at.expand(n, 3), up.expand(n, 3)
+    z_axis = F.normalize(at - C, eps=1e-5)
+    x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
+    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
+    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
+    if is_close.any():
+        x_axis = torch.where(is_close, F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5),
+                             x_axis)
+    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
+    R = R.transpose(1, 2)
+    T = -torch.bmm(R.transpose(1, 2), C[:, :, None])[:, :, 0]
+    return R.to(device), T.to(device)
+
+
+class FoVPerspectiveCameras:
+    """OpenGL-style perspective camera used by colocate.py (renderer/cameras.py:314-575).
+
+    Rays (sample_positions, :539-575) come from ``nrt_raygen`` (NRT_CAM_FOV): the inverse of the
+    full projection Rotate(R) . Translate(T) . K^T is built on the host in float32 with the
+    reference's Transform3d.inverse() order (transforms/transform3d.py:225-272: inv(K^T), then
+    Translate(-T), then R^T), and the kernel applies it to (ndc_x, ndc_y, 1) with a homogeneous
+    divide and r_d = normalize(point) (the reference normalises the point, not point - centre).
+    """
+
+    def __init__(self, znear=1e-2, zfar=1e4, aspect_ratio=1.0, fov=60.0, degrees=True,
+                 R=None, T=None, K=None, device="cpu"):
+        if K is not None:
+            raise NotImplementedError("FoVPerspectiveCameras(K=...) is not on the HIP path")
+        self.R = torch.eye(3)[None] if R is None else R
+        self.T = torch.zeros(1, 3) if T is None else T
+        self.znear, self.zfar, self.aspect_ratio, self.fov = znear, zfar, aspect_ratio, fov
+        self.degrees = degrees
+        self.device = device
+
+    def __len__(self):
+        return self.R.shape[0]
+
+    def compute_projection_matrix(self):
+        """[N,4,4] K (renderer/cameras.py:389-439); parameters float32 [N] as TensorProperties
+        (renderer/utils.py:91-130) makes them."""
+        N = len(self)
+        znear, zfar = _f32(self.znear).expand(N), _f32(self.zfar).expand(N)
+        aspect, fov = _f32(self.aspect_ratio).expand(N), _f32(self.fov).expand(N)
+        if self.degrees:
+            fov = (np.pi / 180) * fov
+        tan_half = torch.tan(fov / 2)
+        max_y = tan_half * znear
+        min_y = -max_y
+        max_x = max_y * aspect
+        min_x = -max_x
+        K = torch.zeros((N, 4, 4), dtype=torch.float32)
+        K[:, 0, 0] = 2.0 * znear / (max_x - min_x)
+        K[:, 1, 1] = 2.0 * znear / (max_y - min_y)
+        K[:, 0, 2] = (max_x + min_x) / (max_x - min_x)
+        K[:, 1, 2] = (max_y + min_y) / (max_y - min_y)
+        K[:, 3, 2] = 1.0 * torch.ones(N)
+        K[:, 2, 2] = 1.0 * zfar / (zfar - znear)
+        K[:, 2, 3] = -(zfar * znear) / (zfar - znear)
+        return K
+
+    def _rt(self):
+        R = self.R.detach().float().cpu()
+        T = self.T.detach().float().cpu()
+        N = R.shape[0]
+        rot = torch.eye(4).repeat(N, 1, 1)
+        rot[:, :3, :3] = R
+        tinv = torch.eye(4).repeat(N, 1, 1)
+        tinv[:, 3, :3] = -T
+        return rot, tinv
+
+    def get_camera_center(self):
+        """renderer/cameras.py:143-149: row 3 of (Rotate . Translate)^-1."""
+        rot, tinv = self._rt()
+        return torch.bmm(tinv, rot.transpose(1, 2))[:, 3, :3]
+
+    def inverse_full_projection(self):
+        rot, tinv = self._rt()
+        m = torch.inverse(self.compute_projection_matrix().transpose(1, 2).contiguous())
+        return torch.bmm(torch.bmm(m, tinv), rot.transpose(1, 2))
+
+    def _structs(self, size):
+        inv = self.inverse_full_projection()
+        ctr = self.get_camera_center()
+        return [_cam_struct(_lib.NRT_CAM_FOV, size, mat=inv[n], origin=ctr[n])
+                for n in range(len(self))]
+
+    def rays_tile(self, x0, y0, W, H, size, with_noise=False, positions=None, noise=None,
+                  bundle_size=1, device="cuda"):
+        """[N, W, H, B, 6].  noise: [W, H, 2] uniforms (the sampler's draw), drawn here if None."""
+        if bundle_size != 1:
+            raise NotImplementedError("FoVPerspectiveCameras on the HIP path renders bundle_size 1")
+        if with_noise and noise is None:
+            noise = torch.rand(W, H, 2, device=device)
+        rays = raygen(self._structs(size), x0, y0, W, H, with_noise, noise if with_noise else None,
+                      positions, device)
+        return rays.reshape(len(self), W, H, 1, 6)
+
+    def sample_positions(self, position_samples, sampler, bundle_size=8, size=512,
+                         with_noise=False, N=1):
+        """renderer/cameras.py:539-575 (one sampler draw of the jitter, [W, H, B, 2])."""
+        W, H, _ = position_samples.shape
+        dev = position_samples.device
+        noise = None
+        if with_noise:
+            noise = sampler.sample((W, H, bundle_size, 2), device=dev).reshape(W, H, 2)
+        return self.rays_tile(0, 0, W, H, size, with_noise, positions=position_samples.float()
+                              .contiguous(), noise=noise, bundle_size=bundle_size, device=dev)
+
+
+def OpenGLPerspectiveCameras(znear=1.0, zfar=100.0, aspect_ratio=1.0, fov=60.0, degrees=True,
+                             R=None, T=None, device="cpu"):
+    """renderer/cameras.py:280-311 (deprecated alias with its own defaults)."""
+    return FoVPerspectiveCameras(znear=znear, zfar=zfar, aspect_ratio=aspect_ratio, fov=fov,
+                                 degrees=degrees, R=R, T=T, device=device)
 
 
 @dataclass

@@ -18,6 +18,7 @@ arithmetic (batched BLAS calls, squeeze quirks) so results match op for op.
 """
 import math
 import random
+import numpy as np
 
 import torch
 import torch.nn as nn
@@ -633,6 +634,113 @@ class DTUCameraRef:
         r_d = F.normalize(world - r_o, dim=-1)
         return torch.cat([r_o, r_d], dim=-1).reshape(N, W, H, 1, 6) \
             .expand(N, W, H, bundle_size, 6)
+
+
+def look_at_view_transform_ref(dist=1.0, elev=0.0, azim=0.0, degrees=True, at=(0.0, 0.0, 0.0),
+                               up=(0.0, 1.0, 0.0)):
+    """renderer/cameras.py:1275-1310 (camera_position_from_spherical_angles), :1313-1360
+    (look_at_rotation), :1363-1422 (look_at_view_transform) for one camera."""
+    dist, elev, azim = (torch.tensor([float(v)]) for v in (dist, elev, azim))
+    if degrees:
+        elev = math.pi / 180.0 * elev
+        azim = math.pi / 180.0 * azim
+    x = dist * torch.cos(elev) * torch.sin(azim)
+    y = dist * torch.sin(elev)
+    z = dist * torch.cos(elev) * torch.cos(azim)
+    at_t = torch.tensor([list(at)], dtype=torch.float)
+    up_t = torch.tensor([list(up)], dtype=torch.float)
+    C = torch.stack([x, y, z], dim=1).view(-1, 3) + at_t
+    z_axis = F.normalize(at_t - C, eps=1e-5)
+    x_axis = F.normalize(torch.cross(up_t, z_axis, dim=1), eps=1e-5)
+    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
+    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
+    if is_close.any():
+        x_axis = torch.where(is_close, F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5),
+                             x_axis)
+    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
+    R = R.transpose(1, 2)
+    T = -torch.bmm(R.transpose(1, 2), C[:, :, None])[:, :, 0]
+    return R, T
+
+
+class FoVCameraRef:
+    """FoVPerspectiveCameras (renderer/cameras.py:314-575) with its Transform3d algebra
+    (transforms/transform3d.py:175-324), one camera.
+
+    The full projection is Rotate(R) . Translate(T) . K^T (row vectors, :170-195, :491-494);
+    Transform3d.inverse() (invert_composed=False, :225-272) inverts the pieces and composes them in
+    reverse: inv(K^T) @ Translate(-T) @ R^T, in that bmm order.  sample_positions (:539-575):
+    jitter d*u - d/2, ndc = -2 pos/size + 1, unproject (x, y, 1) with a homogeneous divide and
+    r_d = normalize(point) -- the point itself, not point - centre; r_o = the camera centre
+    (get_camera_center, :143-149).
+    """
+
+    def __init__(self, R, T, znear=1e-2, zfar=1e4, aspect_ratio=1.0, fov=60.0, degrees=True):
+        self.R, self.T = R.float(), T.float()
+        self.znear, self.zfar, self.aspect, self.fov, self.degrees = znear, zfar, aspect_ratio, fov, degrees
+
+    def __len__(self):
+        return 1
+
+    def projection(self):
+        # compute_projection_matrix, renderer/cameras.py:389-439; TensorProperties
+        # (renderer/utils.py:91-130) has made znear, zfar, aspect_ratio and fov float32 [N]
+        f32 = lambda v: torch.tensor([float(v)], dtype=torch.float32)  # noqa: E731
+        znear, zfar, aspect, fov = f32(self.znear), f32(self.zfar), f32(self.aspect), f32(self.fov)
+        if self.degrees:
+            fov = (np.pi / 180) * fov
+        tan_half = torch.tan(fov / 2)
+        max_y = tan_half * znear
+        min_y = -max_y
+        max_x = max_y * aspect
+        min_x = -max_x
+        ones = torch.ones(1, dtype=torch.float32)
+        K = torch.zeros((1, 4, 4), dtype=torch.float32)
+        K[:, 0, 0] = 2.0 * znear / (max_x - min_x)
+        K[:, 1, 1] = 2.0 * znear / (max_y - min_y)
+        K[:, 0, 2] = (max_x + min_x) / (max_x - min_x)
+        K[:, 1, 2] = (max_y + min_y) / (max_y - min_y)
+        K[:, 3, 2] = 1.0 * ones
+        K[:, 2, 2] = 1.0 * zfar / (zfar - znear)
+        K[:, 2, 3] = -(zfar * znear) / (zfar - znear)
+        return K
+
+    def _rot(self):
+        M = torch.eye(4).unsqueeze(0).clone()
+        M[:, :3, :3] = self.R
+        return M
+
+    def _trans(self, sign=1.0):
+        M = torch.eye(4).unsqueeze(0).clone()
+        M[:, 3, :3] = sign * self.T
+        return M
+
+    def inverse_full_projection(self):
+        kt = self.projection().transpose(1, 2).contiguous()
+        m = torch.inverse(kt)
+        m = torch.bmm(m, self._trans(-1.0))                    # Translate._get_matrix_inverse
+        m = torch.bmm(m, self._rot().transpose(1, 2))           # Rotate._get_matrix_inverse
+        return m
+
+    def center(self):
+        # (Rotate . Translate).inverse() = Translate^-1 then Rotate^-1; row 3, :3
+        m = torch.bmm(self._trans(-1.0), self._rot().transpose(1, 2))
+        return m[:, 3, :3]
+
+    def sample_positions(self, pos, size, with_noise=0.0, noise=None, bundle_size=1):
+        ps = pos.unsqueeze(-2).expand(*pos.shape[:-1], bundle_size, 2)
+        if with_noise:
+            d = with_noise
+            ps = ps + (d * noise - d / 2)
+        ps = -2 * (ps / size) + 1
+        pts = torch.cat([ps, torch.ones(ps.shape[:-1] + (1,))], dim=-1)
+        flat = pts.reshape(1, -1, 3)
+        hom = torch.cat([flat, torch.ones(1, flat.shape[1], 1)], dim=2)
+        out = torch.bmm(hom, self.inverse_full_projection())
+        dirs = out[..., :3] / out[..., 3:]
+        dirs = F.normalize(dirs.reshape(1, *pts.shape), dim=-1)
+        origins = self.center()[:, None, None, None, :].expand_as(dirs)
+        return torch.cat([origins, dirs], dim=-1)
 
 
 # ---------------------------------------------------------------------------------------------

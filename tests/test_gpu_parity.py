@@ -598,3 +598,93 @@ def test_direct_shadow_rays_need_point_light():
                                 bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
                                 crop_size=32, uv=(0, 0), background=0, with_noise=0.0,
                                 w_isect=True)
+
+
+def test_fov_raygen_matches_oracle():
+    """nrt_raygen(NRT_CAM_FOV) vs FoVPerspectiveCameras.sample_positions (renderer/cameras.py:
+    539-575), without and with the sampler's jitter (the same uniforms injected into both)."""
+    from neural_raytracing_amd.pathtracer.cameras import OpenGLPerspectiveCameras
+    Rm, Tm = R.look_at_view_transform_ref(dist=1.0, elev=30.0, azim=45.0)
+    ref = R.FoVCameraRef(Rm, Tm, znear=1.0, zfar=100.0)
+    cam = OpenGLPerspectiveCameras(R=Rm, T=Tm, device="cuda")
+    pos = R._tile_positions(8, 16, 32)
+    want = ref.sample_positions(pos, 64)
+    got = cam.rays_tile(8, 16, 32, 32, 64)
+    assert torch.allclose(got.cpu(), want, atol=2e-6)
+    noise = torch.rand(32, 32, 2)
+    want = ref.sample_positions(pos, 64, with_noise=0.5, noise=noise.unsqueeze(-2))
+    got = cam.rays_tile(8, 16, 32, 32, 64, with_noise=0.5, noise=noise.cuda())
+    assert torch.allclose(got.cpu(), want, atol=2e-6)
+
+
+def _colocate_pair():
+    """cfg3-like scene (colocate.py:63-80, 109): SphereSDF(n=64), OpenGLPerspectiveCameras from
+    look_at_view_transform(dist=1, elev=30, azim=45), PointLights(scale=5) at 1.05 x the camera
+    centre, ComposeSpatialVarying([NeuralBSDF x 2, Diffuse(Softplus).random(),
+    Conductor(Softplus).random()]), Direct().  Oracle built first, product copies its numbers."""
+    from neural_raytracing_amd.pathtracer.bsdf import (ComposeSpatialVarying, Conductor, Diffuse,
+                                                        NeuralBSDF)
+    from neural_raytracing_amd.pathtracer.cameras import OpenGLPerspectiveCameras
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    seeded(13)
+    ref_sdf = R.SphereBlobSDF(n=64)
+    parts = [R.NeuralBSDFRef(), R.NeuralBSDFRef(),
+             R.DiffuseRef(reflectance=torch.rand(3).tolist(), preprocess="softplus"),
+             R.ConductorRef(specular=torch.rand(3).tolist(), activation="softplus")]
+    ref_bsdf = R.SpatialMixBSDF(parts)
+    Rm, Tm = R.look_at_view_transform_ref(dist=1.0, elev=30.0, azim=45.0)
+    ref_cam = R.FoVCameraRef(Rm, Tm, znear=1.0, zfar=100.0)
+    loc = (ref_cam.center()[0] * 1.05).tolist()
+    ref = dict(shape=R.MarchedSDF(sdf=ref_sdf, max_steps=64), bsdf=ref_bsdf,
+               lights=R.PointLightRef(location=loc, scale=5.0), camera=ref_cam)
+    sphere = SphereSDF(n=64, device="cpu")
+    with torch.no_grad():
+        sphere.centers.copy_(ref_sdf.centers)
+        sphere.radii.copy_(ref_sdf.radii)
+        sphere.tfs.copy_(ref_sdf.tfs)
+    copy_mlp(sphere.shift, ref_sdf.shift)
+    comps = [NeuralBSDF(device="cpu"), NeuralBSDF(device="cpu"),
+             Diffuse(reflectance=parts[2].reflectance.tolist(), preprocess=torch.nn.Softplus(),
+                     device="cuda"),
+             Conductor(specular=parts[3].specular.tolist(), activation=torch.nn.Softplus(),
+                       device="cuda")]
+    for c, r in zip(comps[:2], parts[:2]):
+        copy_mlp(c.mlp, r.mlp)
+        c.mlp.cuda()
+    bsdf = ComposeSpatialVarying(comps, device="cpu")
+    copy_mlp(bsdf.sp_var_fn, ref_bsdf.sp_var_fn)
+    bsdf.sp_var_fn.cuda()
+    mine = dict(shape=SDF(sdf=sphere.cuda(), max_steps=64), bsdf=bsdf,
+                lights=PointLights(location=loc, scale=5.0, device="cuda"),
+                camera=OpenGLPerspectiveCameras(R=Rm, T=Tm, device="cuda"))
+    return ref, mine
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_colocate_fov_render_matches_oracle(prec):
+    """Full-frame pathtrace of the colocate-like scene (FoV camera, point light, 4-component
+    spatially varying BSDF incl. Diffuse and Conductor) on the fused tile path vs the oracle."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    ref, mine = _colocate_pair()
+    random.seed(17)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref["lights"], ref["camera"], R.DirectRef(), ref["bsdf"],
+                        size=64, chunk_size=32, background=0.5, with_noise=0.0)
+    assert (want != 0.5).any(-1).float().mean() > 0.1  # the object covers part of the frame
+    set_precision(prec)
+    random.seed(17)
+    with torch.no_grad():
+        got, _ = pt.pathtrace(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                              bsdf=mine["bsdf"], size=64, chunk_size=32, bundle_size=1,
+                              background=0.5, with_noise=0.0)
+    got = got.cpu()
+    assert got.shape == want.shape == (64, 64, 3)
+    if prec == "fp32":
+        close = (got - want).abs().amax(-1) <= 1e-4
+        assert close.float().mean() >= 0.995, (got - want).abs().max()
+    else:
+        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
+        assert -10 * math.log10(max(mse, 1e-12)) > 40

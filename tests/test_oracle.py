@@ -121,3 +121,40 @@ def test_coarse_scan_argmin_kat():
     k = round(2.0 / step)
     assert abs(best[0, 2].item() - (2.0 - k * step)) < 1e-5
     assert thr.item() < -0.99
+
+
+def test_fov_camera_kat():
+    """FoVCameraRef (renderer/cameras.py:539-575): the unprojected point of NDC (x, y, 1) lies on
+    the far plane, so r_d = normalize(C + zfar (f + x tan(fov/2) a right + y tan(fov/2) up)) --
+    the point normalised, not the point minus the centre C (:570).  Centre and corner pixels."""
+    Rm, Tm = R.look_at_view_transform_ref(dist=2.0, elev=30.0, azim=45.0)
+    cam = R.FoVCameraRef(Rm, Tm, znear=1.0, zfar=100.0, fov=60.0)
+    C = cam.center()[0]
+    el, az = math.radians(30.0), math.radians(45.0)
+    want_c = 2.0 * torch.tensor([math.cos(el) * math.sin(az), math.sin(el), math.cos(el) * math.cos(az)])
+    assert torch.allclose(C, want_c, atol=1e-6)
+    # camera axes are the columns of R: x (right), y (up), z (forward, towards the origin)
+    xa, ya, za = Rm[0, :, 0], Rm[0, :, 1], Rm[0, :, 2]
+    assert torch.allclose(za, F.normalize(-C, dim=0), atol=1e-6)
+    size = 64
+    tan = math.tan(math.radians(30.0))
+    pos = torch.tensor([[[size / 2, size / 2], [0.0, 0.0]]])  # [W=1, H=2, 2]: centre, corner
+    rays = cam.sample_positions(pos, size)
+    for j, (nx, ny) in enumerate([(0.0, 0.0), (1.0, 1.0)]):
+        far = C + 100.0 * (za + nx * tan * xa + ny * tan * ya)
+        assert torch.allclose(rays[0, 0, j, 0, 3:], F.normalize(far, dim=0), atol=2e-6)
+        assert torch.allclose(rays[0, 0, j, 0, :3], C, atol=1e-6)
+
+
+def test_product_look_at_matches_oracle():
+    """Host-side camera math of the product (look_at_view_transform, camera centre, inverse full
+    projection) equals the oracle's bit for bit: both are the reference's float32 op order."""
+    from neural_raytracing_amd.pathtracer.cameras import OpenGLPerspectiveCameras, look_at_view_transform
+    for dist, elev, azim in [(1.0, 30.0, 45.0), (2.5, -10.0, 170.0), (1.0, 89.0, 0.0)]:
+        Rp, Tp = look_at_view_transform(dist=dist, elev=elev, azim=azim)
+        Ro, To = R.look_at_view_transform_ref(dist=dist, elev=elev, azim=azim)
+        assert torch.equal(Rp, Ro) and torch.equal(Tp, To)
+        cam = OpenGLPerspectiveCameras(R=Rp, T=Tp)
+        ref = R.FoVCameraRef(Ro, To, znear=1.0, zfar=100.0)
+        assert torch.equal(cam.get_camera_center(), ref.center())
+        assert torch.equal(cam.inverse_full_projection(), ref.inverse_full_projection())
