@@ -229,6 +229,20 @@ int nrt_composite(const float* rgb, const float* throughput, const uint8_t* hit,
                   int32_t channels, int32_t X0, int32_t Y0, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * NeRFLE (shapes/nerf.py:153-214, envmap=False), driven by NeRFReproduce.sample
+ * (integrators.py:260-267): for each ray and each depth ts[s] (the caller's
+ * linspace(0, 2 + random()*0.1, S)), first = MLP_5x128(o + ts[s] d) -> (alpha_raw, latent[64]),
+ * rgb_s = sigmoid(MLP_8x64([latent, d, light])), composited with the reference's weights
+ * (alpha = 1 - exp(-relu(alpha_raw) t), rolled cumprod with the last entry 1).
+ * first: 3 -> 65, second: 70 -> 3.  ts[S] and light[3] are device arrays; rgb [P,3].
+ * workspace: nrt_nerfle_workspace_bytes(P, S) bytes of device memory.
+ * ------------------------------------------------------------------------------------- */
+size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S);
+int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays, int64_t P,
+                       const float* ts, int32_t S, const float* light, float* rgb,
+                       void* workspace, int precision, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Kernel timing (bench / profiling aid; no reference counterpart)
  * When enabled, the heavy launches (k_intersect, k_sdf_grad, k_shade_direct, k_mlp_forward)
  * are bracketed by hipEvents on the stream they run on.  nrt_profile_read synchronises those

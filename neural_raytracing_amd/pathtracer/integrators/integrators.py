@@ -150,6 +150,20 @@ class Direct(Integrator):
         return result, active, it
 
 
+class NeRFReproduce(Integrator):
+    """Runs a volumetric NeRF on the rays (integrators.py:260-267): result = nerf(rays, lights)."""
+
+    def dims(self):
+        return 3
+
+    def sample(self, nerf, rays, lights, **kwargs):
+        result = nerf(rays, lights)
+
+        class Dummy:
+            ...
+        return result, torch.tensor(True, device=result.device), Dummy()
+
+
 class NeRFIntegrator(Integrator):
     """Appends sigmoid(throughput) as alpha (integrators.py:243-257)."""
 

@@ -1,0 +1,51 @@
+"""Volumetric NeRF shapes (shapes/nerf.py).  ``NeRFLE`` (NeRF + point light, envmap=False) renders
+through ``nrt_nerfle_forward``: sample points, both MLPs and the reference's compositing on the
+GPU.  Constructor and RNG consumption follow nerf.py:153-172."""
+import random
+
+import torch
+import torch.nn as nn
+
+from ... import _lib
+from ..neural_blocks import SkipConnMLP
+
+
+class NeRFLE(nn.Module):
+    """NeRF with a point-light emitter input (nerf.py:153-214).
+
+    forward(rays [..., 6], lights) -> rgb [..., 3] with 64 samples at
+    ts = linspace(0, 2 + random.random() * 0.1, 64) (nerf.py:178; one ``random.random()`` draw per
+    call, as in the reference).  ``envmap=True`` (light encoded by ``lights.envmap``) is not on the
+    HIP path yet.
+    """
+
+    def __init__(self, envmap=False, bins=4, device="cuda"):
+        super().__init__()
+        self.latent_size = 64
+        self.first = SkipConnMLP(num_layers=5, hidden_size=128, in_size=3,
+                                 out=1 + self.latent_size, device=device).to(device)
+        self.bins = bins
+        self.second = SkipConnMLP(in_size=self.latent_size + (6 if not envmap else 3 + bins * bins * 3),
+                                  out=3, device=device).to(device)
+        self.envmap = envmap
+        self.steps = 64  # nerf.py:178 hard-codes 64
+
+    def forward(self, rays, lights):
+        if getattr(self, "envmap", False):
+            raise _lib.NrtError("NeRFLE(envmap=True) is not on the HIP path yet")
+        if not rays.is_cuda:
+            raise _lib.NrtError("NeRFLE renders on the HIP path only: move it and the rays to the GPU")
+        lead = rays.shape[:-1]
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        dev = flat.device
+        # torch.linspace on the host: the same float32 sequence the CPU reference computes
+        ts = torch.linspace(0, 2 + random.random() * 0.1, self.steps).to(dev)
+        light = lights.location.reshape(-1, 3)[0].detach().float().to(dev).contiguous()
+        rgb = torch.empty(P, 3, device=dev)
+        lib = _lib.load(require_device=True)
+        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(P, self.steps), dtype=torch.uint8, device=dev)
+        _lib.call("nrt_nerfle_forward", self.first.nrt(), self.second.nrt(), _lib.ptr(flat), P,
+                  _lib.ptr(ts), self.steps, _lib.ptr(light), _lib.ptr(rgb), _lib.ptr(ws),
+                  _lib.precision_code(), _lib.stream())
+        return rgb.reshape(lead + (3,))
