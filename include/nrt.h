@@ -185,6 +185,23 @@ int nrt_shade_direct_shadowed(const nrt_bsdf* bsdf, const nrt_light* light, cons
                               int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
                               void* workspace, int precision, void* stream);
 
+/* One bounce of Path.sample (integrators.py:309-350) over the rays with active[i] != 0:
+ *   result[i] += throughput[i] * f(wi, wo_light) * Le   (the emitter term; shadow rays toward the
+ *                point light when shadow != 0, as w_isect=True)
+ *   BSDF sample (ComposeSpatialVarying.sample, bsdfs.py:500-513; NeuralBSDF / Diffuse components)
+ *     from injected uniforms: u_comp [P, n_components, 2] (each component's sampler draw, in
+ *     component order) and u_sel [P] (inverse CDF of k / sum k, standing in for multinomial)
+ *   throughput[i] = clamp(spectrum_sel, 1e-10) * throughput[i]; active[i] &= any(throughput > 0)
+ *   rays_out[i] = [p, from_local(frame(n), wo_sel)]  (inactive rays: [p, (0,0,1)])
+ * The caller intersects rays_out (primary = 0) and clears active where it missed.  sdf may be
+ * NULL when shadow == 0.  workspace: nrt_path_workspace_bytes(P). */
+size_t nrt_path_workspace_bytes(int64_t P);
+int nrt_path_bounce(const nrt_bsdf* bsdf, const nrt_light* light, const nrt_sdf* sdf,
+                    int32_t shadow, int32_t max_steps, float epsilon, const float* p,
+                    const float* n, const float* wi, int64_t P, uint8_t* active,
+                    float* throughput, float* result, const float* u_comp, const float* u_sel,
+                    float* rays_out, void* workspace, int precision, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Cameras (cameras/cameras.py) and the tile composite (main.py:85-90, integrators.py:251)
  * ------------------------------------------------------------------------------------- */

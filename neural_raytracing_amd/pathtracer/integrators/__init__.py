@@ -1,2 +1,2 @@
 from .integrators import (Debug, Depth, Direct, Integrator, Mask, NeRFIntegrator,  # noqa: F401
-                          NeRFReproduce)
+                          NeRFReproduce, Path)

@@ -150,6 +150,75 @@ class Direct(Integrator):
         return result, active, it
 
 
+class Path(Integrator):
+    """Light path integrator (integrators.py:275-354): per bounce (max_depth 2) the emitter term
+    weighted by the path throughput, then a BSDF sample of the spatially varying mixture and a
+    secondary intersection.  Each bounce is one ``nrt_path_bounce`` call plus ``nrt_sdf_intersect``
+    of the spawned rays.  ``training`` stays False (the reference sets it after
+    ``nn.Module.__init__``), so the primary intersection has no coarse scan.
+
+    Randomness: each BSDF component draws ``sampler.sample(shape + (2,))`` in component order, as
+    in the reference; the component selection (torch.multinomial there) is the inverse CDF of the
+    spatial weights at one more uniform draw.  ``uniforms=[(u_comp, u_sel), ...]`` (one pair per
+    bounce) replaces the draws, for parity tests.
+    """
+
+    def __init__(self, training=False, **kwargs):
+        super().__init__(**kwargs)
+        self.training = training
+
+    def dims(self):
+        return 3
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        from ..shapes.sdfs import sdf_handle
+        sampler = kwargs.get("sampler", self.sampler)
+        lights = kwargs.get("lights", self.lights)
+        w_isect = kwargs.get("w_isect", False)
+        uniforms = kwargs.get("uniforms")
+        if w_isect not in (None, False, True):
+            raise _lib.NrtError("Path(w_isect=<occlusion MLP>) is not on the HIP path yet")
+        dev = rays.device
+        lead = rays.shape[:-1]
+        it, active = shapes.intersect(rays, primary=self.training)
+        result = torch.zeros(*lead, 3, device=dev)
+        if not bool(active.any()):
+            return result, active, it
+        original_active = active.clone()
+        P = active.numel()
+        nc = len(getattr(bsdf, "bsdfs", [bsdf]))
+        act = active.reshape(-1).to(torch.uint8).contiguous()
+        thr = torch.ones(P, 3, device=dev)
+        res = result.reshape(P, 3)
+        rays_out = torch.empty(P, 6, device=dev)
+        lib = _lib.load(require_device=True)
+        ws = torch.empty(lib.nrt_path_workspace_bytes(P), dtype=torch.uint8, device=dev)
+        sh = sdf_handle(shapes.sdf)
+        curr = it
+        for depth in range(self.max_depth):
+            if uniforms is not None:
+                u_comp, u_sel = (u.to(dev).float().reshape(P, -1).contiguous() for u in uniforms[depth])
+            else:
+                draws = [sampler.sample(tuple(lead) + (2,), device=dev).reshape(P, 1, 2)
+                         for _ in range(nc)]
+                u_comp = torch.cat(draws, dim=1).contiguous()
+                u_sel = sampler.sample((P,), device=dev).contiguous()
+            _lib.call("nrt_path_bounce", _bsdf_handle(bsdf), _light_handle(lights), sh,
+                      int(w_isect is True), int(shapes.max_steps), float(shapes.epsilon),
+                      _lib.ptr(curr.p.reshape(P, 3).contiguous()),
+                      _lib.ptr(curr.n.reshape(P, 3).contiguous()),
+                      _lib.ptr(curr.wi.reshape(P, 3).contiguous()), P, _lib.ptr(act),
+                      _lib.ptr(thr), _lib.ptr(res), _lib.ptr(u_comp), _lib.ptr(u_sel),
+                      _lib.ptr(rays_out), _lib.ptr(ws), _lib.precision_code(), _lib.stream())
+            if depth + 1 == self.max_depth or not bool(act.any()):
+                break  # the reference's last spawn is never shaded (:309, :342)
+            curr, hits = shapes.intersect(rays_out.reshape(*lead, 6), primary=False)
+            act &= hits.reshape(-1).to(torch.uint8)
+            if not bool(act.any()):
+                break
+        return result, original_active, it
+
+
 class NeRFReproduce(Integrator):
     """Runs a volumetric NeRF on the rays (integrators.py:260-267): result = nerf(rays, lights)."""
 

@@ -569,6 +569,109 @@ class NeRFIntegratorRef:
         return torch.cat([rgb, alpha], dim=-1), torch.tensor(True), it
 
 
+def square_to_uniform_disk_concentric(sample):
+    """warps.py:10-30, including its (r sin(phi), r cos(phi)) output order."""
+    v = 2 * sample - 1
+    is_zero = (v == 0).all(dim=-1)
+    q13 = (v[..., 0].abs() < v[..., 1].abs()).unsqueeze(-1)
+    x, y = torch.split(v, 1, dim=-1)
+    r = torch.where(q13, y, x)
+    rp = torch.where(q13, x, y)
+    r = r.sign() * r.abs().clamp(min=1e-12)
+    phi = 0.25 * math.pi * rp / r
+    phi = torch.where(q13, 0.5 * math.pi - phi, phi)
+    phi = torch.where(is_zero.unsqueeze(-1), torch.zeros_like(phi), phi)
+    s, c = phi.sin(), phi.cos()
+    return torch.cat([r * s, r * c], dim=-1)
+
+
+def square_to_cos_hemisphere(sample):
+    """warps.py:44-49."""
+    p = square_to_uniform_disk_concentric(sample)
+    z = (1 - (p * p).sum(dim=-1, keepdim=True)).clamp(min=1e-7).sqrt()
+    return torch.cat([p, z], dim=-1)
+
+
+def bsdf_sample_ref(bsdf, it, u_comp, u_sel, active):
+    """ComposeSpatialVarying.sample (bsdfs.py:500-513) with NeuralBSDF.sample (:625-633) and
+    Diffuse.sample (:90-106) components, randomness injected: u_comp[..., c, :] is component c's
+    sampler.sample(shape + (2,)) draw (component order), and the torch.multinomial(k) selection
+    is the inverse CDF of k / sum(k) at u_sel (same distribution; torch's internal draw cannot be
+    replayed).  Returns (wo_local, spectrum) of the selected component."""
+    parts = bsdf.bsdfs if isinstance(bsdf, SpatialMixBSDF) else [bsdf]
+    wos, specs = [], []
+    for c, b in enumerate(parts):
+        wo = F.normalize(square_to_cos_hemisphere(u_comp[..., c, :]), dim=-1)
+        if isinstance(b, NeuralBSDFRef):
+            spec = b.act(b.mlp(rusinkiewicz(it.wi, wo)))
+        elif isinstance(b, DiffuseRef):
+            if not ((it.wi[..., 2] > 0) & active).any():  # bsdfs.py:95-96
+                wo, spec = torch.zeros_like(it.p), torch.zeros_like(it.p)
+            else:
+                spec = b.preproc(b.reflectance).expand(it.p.shape).clone()
+        else:
+            raise NotImplementedError("Conductor.sample crashes in the reference (bsdfs.py:396)")
+        wos.append(wo)
+        specs.append(spec)
+    if isinstance(bsdf, SpatialMixBSDF):
+        k = bsdf.weights(it.p)
+    else:
+        k = torch.ones(it.p.shape[:-1] + (1,))
+    cdf = torch.cumsum(k / k.sum(dim=-1, keepdim=True), dim=-1)
+    sel = (u_sel.unsqueeze(-1) >= cdf).sum(dim=-1).clamp(max=len(parts) - 1)
+    wo = torch.stack(wos, dim=-1).gather(-1, sel[..., None, None].expand(it.p.shape + (1,))).squeeze(-1)
+    spec = torch.stack(specs, dim=-1).gather(-1, sel[..., None, None].expand(it.p.shape + (1,))).squeeze(-1)
+    return F.normalize(wo, dim=-1), spec
+
+
+class PathRef:
+    """Path.sample (integrators.py:275-354), max_depth 2, no Russian roulette (rr_depth 5 is never
+    reached), mis = 1.  ``training`` stays False (set after nn.Module.__init__, :276-278), so the
+    primary intersection runs without the coarse scan.  ``uniforms[depth] = (u_comp, u_sel)``
+    injects the BSDF-sampling randomness (see bsdf_sample_ref)."""
+
+    def __init__(self, max_depth=2):
+        self.max_depth = max_depth
+
+    def dims(self):
+        return 3
+
+    def sample(self, shape, rays, bsdf, lights, w_isect=False, jitter=None, uniforms=None):
+        throughput = torch.ones(*rays.shape[:-1], 3)
+        result = torch.zeros_like(throughput)
+        it, active = shape.intersect(rays, primary=False)
+        if not active.any():
+            return result, active, it
+        original_active = active.clone()
+        curr = it
+        for depth in range(self.max_depth):
+            if active.any():
+                if w_isect is True:
+                    ds, le = emitter_shadow_ray(curr, shape, lights, active)
+                else:
+                    ds, le = emitter_no_shadow(curr, lights, active)
+                ae = active & (torch.as_tensor(ds.pdf) > 0)
+                wo = curr.to_local(ds.d)
+                f, pdf = bsdf.eval_and_pdf(curr, wo, active=ae)
+                mis = torch.ones_like(pdf.reshape(ae.shape))
+                result = result + torch.where(ae.unsqueeze(-1),
+                                              mis.unsqueeze(-1) * throughput * f * le,
+                                              torch.zeros_like(result))
+            u_comp, u_sel = uniforms[depth]
+            wo_l, spec = bsdf_sample_ref(bsdf, curr, u_comp, u_sel, active)
+            throughput = spec.clamp(min=1e-10) * throughput
+            active = active & (throughput > 0).any(-1)
+            if not active.any():
+                break
+            d = curr.from_local(wo_l)
+            rays = torch.cat([curr.p.expand_as(d), d], dim=-1)
+            curr, hits = shape.intersect(rays, primary=False)
+            active = active & hits
+            if not active.any():
+                break
+        return result, original_active, it
+
+
 # ---------------------------------------------------------------------------------------------
 # Cameras  (cameras/cameras.py)
 # ---------------------------------------------------------------------------------------------

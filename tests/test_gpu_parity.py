@@ -749,3 +749,69 @@ def test_nerfle_pathtrace_nerf_reproduce():
             want = ref(rays, torch.tensor([[0.0, 1.0, 0.0]]), jitter=random.random())
         got = img[x0:x0 + 16, y0:y0 + 16].cpu()
         assert (got - want[0, :, :, 0]).abs().max().item() <= 1e-4
+
+
+def _path_pair(seed=31):
+    """path_nerv-like scene (path_nerv.py:42-100): SphereSDF blob with a small learned shift,
+    ComposeSpatialVarying([NeuralBSDF(sigmoid) x 2, Diffuse]), a point light."""
+    from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, Diffuse, NeuralBSDF
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    seeded(seed)
+    ref_sdf = R.SphereBlobSDF(n=16)
+    with torch.no_grad():
+        ref_sdf.radii.add_(0.15)
+    parts = [R.NeuralBSDFRef(), R.NeuralBSDFRef(), R.DiffuseRef()]
+    ref_bsdf = R.SpatialMixBSDF(parts)
+    loc = (0.4, 0.9, 0.8)
+    ref = dict(shape=R.MarchedSDF(sdf=ref_sdf, max_steps=48), bsdf=ref_bsdf,
+               lights=R.PointLightRef(location=loc, scale=5.0))
+    sphere = SphereSDF(n=16, device="cpu")
+    with torch.no_grad():
+        sphere.centers.copy_(ref_sdf.centers)
+        sphere.radii.copy_(ref_sdf.radii)
+    copy_mlp(sphere.shift, ref_sdf.shift)
+    comps = [NeuralBSDF(device="cpu"), NeuralBSDF(device="cpu"), Diffuse(device="cuda")]
+    for c, r in zip(comps[:2], parts[:2]):
+        copy_mlp(c.mlp, r.mlp)
+        c.mlp.cuda()
+    bsdf = ComposeSpatialVarying(comps, device="cpu")
+    copy_mlp(bsdf.sp_var_fn, ref_bsdf.sp_var_fn)
+    bsdf.sp_var_fn.cuda()
+    mine = dict(shape=SDF(sdf=sphere.cuda(), max_steps=48), bsdf=bsdf,
+                lights=PointLights(location=list(loc), scale=5.0, device="cuda"))
+    return ref, mine
+
+
+@pytest.mark.parametrize("prec,w_isect", [("fp32", False), ("fp32", True), ("fp16", True)])
+def test_path_integrator_matches_oracle(prec, w_isect):
+    """Path (integrators.py:275-354), two bounces, with injected BSDF-sampling uniforms: the
+    emitter term per bounce (optionally shadowed), ComposeSpatialVarying.sample, throughput
+    update and the secondary intersection, vs the oracle's PathRef."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    ref, mine = _path_pair()
+    c2w = recipes.look_at_c2w((0.1, 0.5, 0.9)).unsqueeze(0)
+    ocam = R.NeRFCameraRef(c2w, recipes.nerf_focal(48))
+    rays = ocam.sample_positions(R._tile_positions(0, 0, 48), 48)
+    g = torch.Generator().manual_seed(9)
+    lead = rays.shape[:-1]
+    uniforms = [(torch.rand(*lead, 3, 2, generator=g), torch.rand(*lead, generator=g))
+                for _ in range(2)]
+    with torch.no_grad():
+        want, wmask, _ = R.PathRef().sample(ref["shape"], rays, ref["bsdf"], ref["lights"],
+                                            w_isect=w_isect, uniforms=uniforms)
+    assert wmask.float().mean() > 0.2
+    set_precision(prec)
+    with torch.no_grad():
+        got, mask, _ = Path().sample(mine["shape"], rays.cuda(), mine["bsdf"],
+                                     lights=mine["lights"], w_isect=w_isect, uniforms=uniforms)
+    got = got.cpu()
+    assert torch.equal(mask.cpu(), wmask)
+    assert got.shape == want.shape
+    err = (got - want).abs().amax(-1)
+    if prec == "fp32":
+        assert (err <= 1e-4).float().mean() >= 0.99, err.max()
+    else:
+        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
+        assert -10 * math.log10(max(mse, 1e-12)) > 30
