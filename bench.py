@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crop", type=int, default=128, help="side of the CPU-baseline crop")
     ap.add_argument("--no-fp32-check", action="store_true")
+    ap.add_argument("--scene", default="nerf_synthetic",
+                    choices=["nerf_synthetic", "colocate", "dtu", "nerfle"],
+                    help="nerf_synthetic = the BASELINE metric (default); the others are "
+                         "BASELINE.json configs[2..4] as one-GPU workloads")
     return ap.parse_args()
 
 
@@ -126,6 +130,8 @@ def _copy_to_oracle(dst, src):
 
 def main():
     args = parse()
+    if args.scene != "nerf_synthetic":
+        return bench_other(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -262,6 +268,149 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+FLOP_SHIFT_8x128 = 331_200      # SphereSDF shift MLP per evaluation
+FLOP_NERFLE_SAMPLE = 327_840    # NeRFLE first (5x128, out 65) + second (8x64, in 70)
+
+
+def build_other_scene(name, device, samples):
+    """BASELINE.json configs[2..4] as single-GPU workloads (synthetic, seeded random init):
+    colocate (cfg3: FoV camera, SphereSDF(n=64) + 8x128 shift, 4-component BSDF, point light),
+    dtu (cfg4: DTU pinhole, 8x256 MLP SDF, 10 NeuralBSDF + 6 Diffuse, LightField),
+    nerfle (cfg5: NeRFLE, NeRF+PT, `samples` depths per ray)."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import (ComposeSpatialVarying, Conductor, Diffuse,
+                                                        NeuralBSDF)
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator, NeRFReproduce
+    from neural_raytracing_amd.pathtracer.lights import LightField, PointLights
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.shapes import SDF, NeRFLE, SphereSDF
+    torch.manual_seed(0)
+    random.seed(0)
+    if name == "colocate":
+        sphere = SphereSDF(n=64, device="cpu")
+        sphere.shift = SkipConnMLP(num_layers=8, hidden_size=128, in_size=3, out=1, freqs=32,
+                                   activation=F.softplus, device="cpu")
+        with torch.no_grad():
+            sphere.shift.out.weight.mul_(0.1)
+            sphere.shift.out.bias.mul_(0.1)
+        comps = [NeuralBSDF(device="cpu"), NeuralBSDF(device="cpu"),
+                 Diffuse(preprocess=torch.nn.Softplus(), device="cpu").random(),
+                 Conductor(activation=torch.nn.Softplus(), device="cpu").random()]
+        bsdf = ComposeSpatialVarying(comps, device="cpu")
+        for c in comps[:2]:
+            c.mlp.to(device)
+        bsdf.sp_var_fn.to(device)
+        R, T = pt.cameras.look_at_view_transform(dist=1.0, elev=30.0, azim=45.0)
+        cam = pt.cameras.OpenGLPerspectiveCameras(R=R, T=T, device=device)
+        lights = PointLights(location=(cam.get_camera_center()[0] * 1.05).tolist(), scale=5.0,
+                             device=device)
+        return dict(kind="march", shape=SDF(sdf=sphere.to(device), max_steps=samples), bsdf=bsdf,
+                    lights=lights, integrator=Direct(), cameras=cam, flop_eval=FLOP_SHIFT_8x128,
+                    workload="colocate.py-like: OpenGLPerspectiveCameras(look_at dist 1, elev 30, "
+                             "azim 45), SphereSDF(n=64) + 8x128 F32 shift MLP, "
+                             "ComposeSpatialVarying([NeuralBSDF x2, Diffuse, Conductor]), "
+                             "PointLights(scale 5) at 1.05 x camera centre, Direct()")
+    if name == "dtu":
+        sdf = SkipConnMLP(num_layers=8, hidden_size=256, in_size=3, out=1, freqs=16,
+                          activation=F.softplus, device="cpu")
+        with torch.no_grad():
+            sdf.out.weight.mul_(0.1)
+            sdf.out.bias.add_(-0.3)  # a surface inside the unit ball
+        comps = [NeuralBSDF(activation=torch.nn.Sigmoid(), device="cpu") for _ in range(10)] + \
+                [Diffuse(preprocess=torch.sigmoid, device="cpu").random() for _ in range(6)]
+        bsdf = ComposeSpatialVarying(comps, device="cpu")
+        for c in comps[:10]:
+            c.mlp.to(device)
+        bsdf.sp_var_fn.to(device)
+        K = torch.eye(4)
+        K[0, 0], K[1, 1], K[0, 2], K[1, 2] = 2890.0, 2890.0, 800.0, 600.0
+        pose = torch.eye(4)
+        pose[:3, :4] = look_at((0.0, 0.5, 0.866))
+        pose[:3, 1:3] *= -1  # DTU/IDR cameras look down +z
+        cam = pt.cameras.DTUCamera(pose=pose[None].to(device), intrinsic=K[None].to(device),
+                                   device=device)
+        return dict(kind="march", shape=SDF(sdf=sdf.to(device), max_steps=samples), bsdf=bsdf,
+                    lights=LightField(device="cpu").to(device), integrator=NeRFIntegrator(Direct()),
+                    cameras=cam, flop_eval=FLOP_SDF_8x256,
+                    workload="dtu.py-like: DTUCamera (fx=fy=2890, cx=800, cy=600, 1600x1200 "
+                             "sensor), 8x256 F16 MLP SDF, ComposeSpatialVarying([NeuralBSDF x10, "
+                             "Diffuse(sigmoid) x6]), LightField, NeRFIntegrator(Direct())")
+    if name == "nerfle":
+        nerf = NeRFLE(device="cpu", steps=samples).to(device)
+        focal = float(0.5 * 800 / math.tan(0.5 * 0.6911))
+        return dict(kind="nerfle", nerf=nerf, integrator=NeRFReproduce(),
+                    lights=PointLights(location=[0.0, 1.0, 0.0], device=device),
+                    c2w=view_c2w(0, 1), flop_sample=FLOP_NERFLE_SAMPLE,
+                    workload=f"NeRFLE (NeRF+PT, nerf.py:153-214): 5x128 density/latent MLP + "
+                             f"8x64 colour MLP at {samples} depths per ray, point light, "
+                             "NeRFReproduce")
+    raise ValueError(name)
+
+
+def bench_other(args):
+    """Single-GPU bench line for a non-default scene (--scene colocate|dtu|nerfle)."""
+    from neural_raytracing_amd import _lib
+    import neural_raytracing_amd as nra
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.render import RowRenderer
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--scene other than nerf_synthetic runs on one GPU")
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    _lib.load(require_device=True)
+    nra.set_precision(args.precision)
+    size = args.size
+    sc = build_other_scene(args.scene, device, args.samples)
+    if sc["kind"] == "march":
+        rr = RowRenderer(sc["shape"], sc["lights"], sc["cameras"], sc["integrator"], sc["bsdf"],
+                         size, range(size), background=0.0, with_noise=1e-3, device=device)
+        step = rr.render
+        kernel = "k_march16"
+    else:
+        focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+        cam = pt.cameras.NeRFCamera(cam_to_world=sc["c2w"][None].to(device), focal=focal,
+                                    device=device)
+        rays = cam.rays_tile(0, 0, size, size, size)
+
+        def step():
+            return sc["nerf"](rays, sc["lights"])
+        kernel = "k_nerfle"
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        _lib.profile_enable(False)
+        k_ms, k_n = _lib.profile_read(kernel)
+    rays_total = size * size * args.steps
+    if sc["kind"] == "march":
+        flop = rays_total * (args.samples + MARCH_KERNEL_SCAN_EVALS) * sc["flop_eval"]
+    else:
+        flop = rays_total * args.samples * sc["flop_sample"]
+    achieved = flop / (k_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
+    line = {
+        "metric": f"ray-samples/sec/GPU ({args.scene} {size}x{size}x{args.samples})",
+        "value": rays_total * args.samples / elapsed, "unit": "ray-samples/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": args.precision, "data": "synthetic (seeded random-init weights)",
+        "config": {"workload": sc["workload"], "image": [size, size],
+                   "samples_per_ray": args.samples},
+        "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "flop_per_step": flop / args.steps,
+                     "kernel_ms_per_step": k_ms / args.steps, "launches": k_n},
+    }
+    print(json.dumps(line), flush=True)
 
 
 def rr_hit_fraction(rr):

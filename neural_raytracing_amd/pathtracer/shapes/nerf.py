@@ -19,7 +19,10 @@ class NeRFLE(nn.Module):
     HIP path yet.
     """
 
-    def __init__(self, envmap=False, bins=4, device="cuda"):
+    # samples per nrt_nerfle_forward call (bounds the [S*P, 65/70] intermediates to ~2.3 GB)
+    MAX_SAMPLES_PER_CALL = 1 << 22
+
+    def __init__(self, envmap=False, bins=4, device="cuda", steps=64):
         super().__init__()
         self.latent_size = 64
         self.first = SkipConnMLP(num_layers=5, hidden_size=128, in_size=3,
@@ -28,7 +31,7 @@ class NeRFLE(nn.Module):
         self.second = SkipConnMLP(in_size=self.latent_size + (6 if not envmap else 3 + bins * bins * 3),
                                   out=3, device=device).to(device)
         self.envmap = envmap
-        self.steps = 64  # nerf.py:178 hard-codes 64
+        self.steps = steps  # nerf.py:178 hard-codes 64; BASELINE cfg5 asks 256
 
     def forward(self, rays, lights):
         if getattr(self, "envmap", False):
@@ -44,8 +47,13 @@ class NeRFLE(nn.Module):
         light = lights.location.reshape(-1, 3)[0].detach().float().to(dev).contiguous()
         rgb = torch.empty(P, 3, device=dev)
         lib = _lib.load(require_device=True)
-        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(P, self.steps), dtype=torch.uint8, device=dev)
-        _lib.call("nrt_nerfle_forward", self.first.nrt(), self.second.nrt(), _lib.ptr(flat), P,
-                  _lib.ptr(ts), self.steps, _lib.ptr(light), _lib.ptr(rgb), _lib.ptr(ws),
-                  _lib.precision_code(), _lib.stream())
+        chunk = max(1, min(P, self.MAX_SAMPLES_PER_CALL // self.steps))
+        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(chunk, self.steps), dtype=torch.uint8,
+                         device=dev)
+        first, second = self.first.nrt(), self.second.nrt()
+        for r0 in range(0, P, chunk):
+            n = min(chunk, P - r0)
+            _lib.call("nrt_nerfle_forward", first, second, _lib.ptr(flat[r0:r0 + n]), n,
+                      _lib.ptr(ts), self.steps, _lib.ptr(light), _lib.ptr(rgb[r0:r0 + n]),
+                      _lib.ptr(ws), _lib.precision_code(), _lib.stream())
         return rgb.reshape(lead + (3,))
