@@ -185,9 +185,22 @@ int nrt_shade_direct_shadowed(const nrt_bsdf* bsdf, const nrt_light* light, cons
                               int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
                               void* workspace, int precision, void* stream);
 
+/* Direct shading with a LEARNED occlusion term: sample_emitter_dir_w_learned_occ
+ * (scene.py:301-319, selected by Direct/Path when w_isect is a SkipConnMLP,
+ * integrators.py:164-166 and :289-291).  As nrt_shade_direct_shadowed, but an occluded sample keeps
+ * sigmoid(occ([p, dir_to_elev_azim(d)])) * Le instead of 0 (utils.py:490-494 for elev/azim).
+ * occ: an nrt_mlp mapping 5 -> 1 (broadcast over RGB) or 5 -> 3.  Same workspace size. */
+int nrt_shade_direct_learned_occ(const nrt_bsdf* bsdf, const nrt_light* light, const nrt_sdf* sdf,
+                                 const nrt_mlp* occ, int32_t max_steps, float epsilon,
+                                 const float* p, const float* n, const float* wi,
+                                 const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+                                 float* rgb, float* weights_out, uint8_t* visible_out,
+                                 void* workspace, int precision, void* stream);
+
 /* One bounce of Path.sample (integrators.py:309-350) over the rays with active[i] != 0:
  *   result[i] += throughput[i] * f(wi, wo_light) * Le   (the emitter term; shadow rays toward the
- *                point light when shadow != 0, as w_isect=True)
+ *                point light when shadow != 0, as w_isect=True; with occ != NULL as well, an
+ *                occluded Le is scaled by the learned occlusion, as nrt_shade_direct_learned_occ)
  *   BSDF sample (ComposeSpatialVarying.sample, bsdfs.py:500-513; NeuralBSDF / Diffuse components)
  *     from injected uniforms: u_comp [P, n_components, 2] (each component's sampler draw, in
  *     component order) and u_sel [P] (inverse CDF of k / sum k, standing in for multinomial)
@@ -197,8 +210,8 @@ int nrt_shade_direct_shadowed(const nrt_bsdf* bsdf, const nrt_light* light, cons
  * NULL when shadow == 0.  workspace: nrt_path_workspace_bytes(P). */
 size_t nrt_path_workspace_bytes(int64_t P);
 int nrt_path_bounce(const nrt_bsdf* bsdf, const nrt_light* light, const nrt_sdf* sdf,
-                    int32_t shadow, int32_t max_steps, float epsilon, const float* p,
-                    const float* n, const float* wi, int64_t P, uint8_t* active,
+                    int32_t shadow, const nrt_mlp* occ, int32_t max_steps, float epsilon,
+                    const float* p, const float* n, const float* wi, int64_t P, uint8_t* active,
                     float* throughput, float* result, const float* u_comp, const float* u_sel,
                     float* rays_out, void* workspace, int precision, void* stream);
 

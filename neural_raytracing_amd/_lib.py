@@ -79,9 +79,11 @@ _SIGNATURES = {
     "nrt_shadow_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "nrt_shade_direct_shadowed": (_I32, [_P, _P, _P, _I32, _F, _P, _P, _P, _P, _P, _I64, _P, _P,
                                          _P, _P, _I32, _P]),
+    "nrt_shade_direct_learned_occ": (_I32, [_P, _P, _P, _P, _I32, _F, _P, _P, _P, _P, _P, _I64,
+                                            _P, _P, _P, _P, _I32, _P]),
     "nrt_raygen": (_I32, [_P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P, _P, _P]),
     "nrt_path_workspace_bytes": (ctypes.c_size_t, [_I64]),
-    "nrt_path_bounce": (_I32, [_P, _P, _P, _I32, _I32, _F, _P, _P, _P, _I64, _P, _P, _P, _P, _P,
+    "nrt_path_bounce": (_I32, [_P, _P, _P, _I32, _P, _I32, _F, _P, _P, _P, _I64, _P, _P, _P, _P, _P,
                                _P, _P, _I32, _P]),
     "nrt_nerfle_workspace_bytes": (ctypes.c_size_t, [_I64, _I32]),
     "nrt_nerfle_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _P, _P, _I32, _P]),

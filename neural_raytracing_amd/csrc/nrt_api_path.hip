@@ -155,7 +155,7 @@ size_t nrt_path_workspace_bytes(int64_t P) {
 }
 
 int nrt_path_bounce(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s, int32_t shadow,
-                    int32_t max_steps, float eps, const float* p, const float* n, const float* wi,
+                    const nrt_mlp* occ, int32_t max_steps, float eps, const float* p, const float* n, const float* wi,
                     int64_t P, uint8_t* active, float* throughput, float* result,
                     const float* u_comp, const float* u_sel, float* rays_out, void* workspace,
                     int precision, void* stream) {
@@ -185,9 +185,11 @@ int nrt_path_bounce(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s, int
   k_path_default_rays<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(p, P, rays_out);
   if (int rc = check_launch("k_path_default_rays")) return rc;
   // emitter term of this bounce: rgb[i] = f(wi, wo_light) * Le for listed rays
-  int rc = shadow ? nrt_shade_direct_shadowed(b, l, s, max_steps, eps, p, n, wi, list, cnt, P, rgb,
-                                              nullptr, nullptr, shadow_ws, precision, stream)
-                  : nrt_shade_direct(b, l, p, n, wi, list, cnt, P, rgb, nullptr, precision, stream);
+  int rc = !shadow ? nrt_shade_direct(b, l, p, n, wi, list, cnt, P, rgb, nullptr, precision, stream)
+           : occ ? nrt_shade_direct_learned_occ(b, l, s, occ, max_steps, eps, p, n, wi, list, cnt, P,
+                                                rgb, nullptr, nullptr, shadow_ws, precision, stream)
+                 : nrt_shade_direct_shadowed(b, l, s, max_steps, eps, p, n, wi, list, cnt, P, rgb,
+                                             nullptr, nullptr, shadow_ws, precision, stream);
   if (rc) return rc;
   int hidden = 32, ke = 16;
   auto upd = [&](const nrt_mlp* m) {

@@ -97,7 +97,7 @@ int nrt_bsdf_destroy(nrt_bsdf* b) {
 namespace {
 int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                       const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                      const uint8_t* vis, float* rgb, float* weights_out, bool f16, hipStream_t st) {
+                      const float* lscale, float* rgb, float* weights_out, bool f16, hipStream_t st) {
   int hidden = 32, ke = 16;
   auto upd = [&](const nrt_mlp* m) {
     if (!m) return;
@@ -110,7 +110,7 @@ int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, con
   // FP16: light field, spatial weights and NeuralBSDFs on the program engine when compiled for
   // their shapes (NRT_NO_PROGRAM keeps the per-wave register path)
   if (f16 && std::getenv("NRT_NO_PROGRAM") == nullptr) {
-    const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, vis, rgb, weights_out, st);
+    const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out, st);
     if (rc != NRT_EUNSUPPORTED) return rc;
   }
   LdsPlan lp = plan_lds(hidden, ke, 64, f16, false);
@@ -119,11 +119,11 @@ int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, con
   if (f16) {
     if (int rc = set_lds(k_shade_direct<true>, lp.bytes)) return rc;
     k_shade_direct<true><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
-        b->dev, l->dev, p, n, wi, hit_idx, hit_count, vis, rgb, weights_out, lp.RS, lp.per_wave);
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, lscale, rgb, weights_out, lp.RS, lp.per_wave);
   } else {
     if (int rc = set_lds(k_shade_direct<false>, lp.bytes)) return rc;
     k_shade_direct<false><<<dim3(blocks), dim3(64 * lp.waves), lp.bytes, st>>>(
-        b->dev, l->dev, p, n, wi, hit_idx, hit_count, vis, rgb, weights_out, lp.RS, lp.per_wave);
+        b->dev, l->dev, p, n, wi, hit_idx, hit_count, lscale, rgb, weights_out, lp.RS, lp.per_wave);
   }
   return check_launch("k_shade_direct");
 }
@@ -144,23 +144,32 @@ int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, cons
                            precision == NRT_FP16, (hipStream_t)stream);
 }
 
+// workspace: shadow rays [P,6] | max_t [P] | visible [P] | occ inputs [P,5] | occ out [P,3] |
+// Le factors [P,3]
 size_t nrt_shadow_workspace_bytes(int64_t P) {
   P = std::max<int64_t>(P, 1);
-  return align256((size_t)P * 6 * 4) + align256((size_t)P * 4) + align256((size_t)P);
+  return align256((size_t)P * 6 * 4) + align256((size_t)P * 4) + align256((size_t)P) +
+         align256((size_t)P * 5 * 4) + 2 * align256((size_t)P * 3 * 4);
 }
+}  // extern "C"
 
-int nrt_shade_direct_shadowed(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s,
-                              int32_t max_steps, float eps, const float* p, const float* n,
-                              const float* wi, const int32_t* hit_idx, const int32_t* hit_count,
-                              int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
-                              void* workspace, int precision, void* stream) {
+namespace {
+int shade_shadowed_impl(const char* who, const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s,
+                        const nrt_mlp* occ, int32_t max_steps, float eps, const float* p,
+                        const float* n, const float* wi, const int32_t* hit_idx,
+                        const int32_t* hit_count, int64_t P, float* rgb, float* weights_out,
+                        uint8_t* visible_out, void* workspace, int precision, void* stream) {
   if (!b || !l || !s || !p || !n || !wi || !hit_idx || !hit_count || !rgb || P < 0 || !workspace) {
-    set_error("nrt_shade_direct_shadowed: bad argument");
+    set_error(std::string(who) + ": bad argument");
+    return NRT_EINVAL;
+  }
+  if (occ && (occ->desc.in_size != 5 || (occ->desc.out != 1 && occ->desc.out != 3))) {
+    set_error(std::string(who) + ": occlusion MLP must map [p, elev, azim] (5) -> 1 or 3");
     return NRT_EINVAL;
   }
   if (l->host_dev.kind != 1) {
     // the reference's LightField samples carry no distance, so its shadow test cannot run
-    set_error("nrt_shade_direct_shadowed: shadow rays need a point light (LightField samples "
+    set_error(std::string(who) + ": shadow rays need a point light (LightField samples "
               "have no distance, lights.py:175-195)");
     return NRT_EUNSUPPORTED;
   }
@@ -168,14 +177,52 @@ int nrt_shade_direct_shadowed(const nrt_bsdf* b, const nrt_light* l, const nrt_s
   hipStream_t st = (hipStream_t)stream;
   const bool f16 = precision == NRT_FP16;
   char* ws = (char*)workspace;
-  float* rays = (float*)ws;
-  float* max_t = (float*)(ws + align256((size_t)P * 24));
-  uint8_t* vis = visible_out ? visible_out
-                             : (uint8_t*)(ws + align256((size_t)P * 24) + align256((size_t)P * 4));
-  k_point_shadow_rays<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(
-      l->dev, p, hit_idx, hit_count, rays, max_t);
+  size_t off = 0;
+  auto take = [&](size_t bytes) { char* q = ws + off; off += align256(bytes); return q; };
+  float* rays = (float*)take((size_t)P * 24);
+  float* max_t = (float*)take((size_t)P * 4);
+  uint8_t* vis_ws = (uint8_t*)take((size_t)P);
+  float* occ_in = (float*)take((size_t)P * 20);
+  float* occ_out = (float*)take((size_t)P * 12);
+  float* lscale = (float*)take((size_t)P * 12);
+  uint8_t* vis = visible_out ? visible_out : vis_ws;
+  const dim3 grid(std::min<int64_t>(ceil_div64(P, 256), 1024)), block(256);
+  k_point_shadow_rays<><<<grid, block, 0, st>>>(l->dev, p, hit_idx, hit_count, rays, max_t);
   if (int rc = check_launch("k_point_shadow_rays")) return rc;
   if (int rc = launch_occlusion(s, rays, P, hit_count, max_t, max_steps, eps, vis, f16, st)) return rc;
-  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, vis, rgb, weights_out, f16, st);
+  if (occ) {
+    // occ(occ_rays) over the P list slots (rows past *hit_count are never read back)
+    k_occ_inputs<><<<grid, block, 0, st>>>(p, hit_idx, hit_count, rays, occ_in);
+    if (int rc = check_launch("k_occ_inputs")) return rc;
+    if (int rc = nrt_mlp_forward(occ, occ_in, nullptr, P, occ_out, precision, stream)) return rc;
+  }
+  k_light_scale<><<<grid, block, 0, st>>>(hit_count, vis, occ ? occ_out : nullptr,
+                                          occ ? occ->desc.out : 1, lscale);
+  if (int rc = check_launch("k_light_scale")) return rc;
+  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out, f16, st);
+}
+}  // namespace
+
+extern "C" {
+int nrt_shade_direct_shadowed(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s,
+                              int32_t max_steps, float eps, const float* p, const float* n,
+                              const float* wi, const int32_t* hit_idx, const int32_t* hit_count,
+                              int64_t P, float* rgb, float* weights_out, uint8_t* visible_out,
+                              void* workspace, int precision, void* stream) {
+  return shade_shadowed_impl("nrt_shade_direct_shadowed", b, l, s, nullptr, max_steps, eps, p, n,
+                             wi, hit_idx, hit_count, P, rgb, weights_out, visible_out, workspace,
+                             precision, stream);
+}
+
+int nrt_shade_direct_learned_occ(const nrt_bsdf* b, const nrt_light* l, const nrt_sdf* s,
+                                 const nrt_mlp* occ, int32_t max_steps, float eps, const float* p,
+                                 const float* n, const float* wi, const int32_t* hit_idx,
+                                 const int32_t* hit_count, int64_t P, float* rgb,
+                                 float* weights_out, uint8_t* visible_out, void* workspace,
+                                 int precision, void* stream) {
+  if (!occ) { set_error("nrt_shade_direct_learned_occ: null occlusion MLP"); return NRT_EINVAL; }
+  return shade_shadowed_impl("nrt_shade_direct_learned_occ", b, l, s, occ, max_steps, eps, p, n,
+                             wi, hit_idx, hit_count, P, rgb, weights_out, visible_out, workspace,
+                             precision, stream);
 }
 }  // extern "C"

@@ -663,6 +663,48 @@ __global__ void k_point_shadow_rays(const LightDev* __restrict__ lp, const float
   }
 }
 
+// dir_to_elev_azim (utils.py:490-494)
+__device__ __forceinline__ void dir_elev_azim(float x, float y, float z, float& elev, float& azim) {
+  normalize3(x, y, z, 1e-12f);
+  const float lo = -1.f + 1e-7f, hi = 1.f - 1e-7f;
+  x = fminf(fmaxf(x, lo), hi);
+  z = fminf(fmaxf(z, lo), hi);
+  elev = asinf(z);
+  azim = atan2f(x, sqrtf(fmaxf((1.f - x * x) - z * z, 1e-10f)));
+}
+
+// occ_rays = [p, dir_to_elev_azim(ds.d)] per listed ray (scene.py:309-312); d from the shadow rays
+template <int = 0>
+__global__ void k_occ_inputs(const float* __restrict__ P_, const int32_t* __restrict__ hit_idx,
+                             const int32_t* __restrict__ hit_count, const float* __restrict__ rays,
+                             float* __restrict__ x) {
+  const int64_t total = *hit_count;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t idx = hit_idx[i];
+    float* o = x + i * 5;
+    o[0] = P_[idx * 3]; o[1] = P_[idx * 3 + 1]; o[2] = P_[idx * 3 + 2];
+    dir_elev_azim(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5], o[3], o[4]);
+  }
+}
+
+// per listed ray, the factor on Le: visible -> 1; occluded -> 0 (scene.py:297) or
+// sigmoid(occ(occ_rays)) (scene.py:313-317; occ_out 1 broadcasts over RGB, 3 is per channel)
+template <int = 0>
+__global__ void k_light_scale(const int32_t* __restrict__ hit_count, const uint8_t* __restrict__ vis,
+                              const float* __restrict__ occ, int occ_out, float* __restrict__ ls) {
+  const int64_t total = *hit_count;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool v = vis[i] != 0;
+    for (int q = 0; q < 3; ++q) {
+      float s = 1.f;
+      if (!v) s = occ ? 1.f / (1.f + expf(-occ[i * occ_out + (occ_out == 3 ? q : 0)])) : 0.f;
+      ls[i * 3 + q] = s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // shading
 // ------------------------------------------------------------------------------------------
@@ -716,7 +758,7 @@ template <bool F16>
 __global__ void __launch_bounds__(256) k_shade_direct(
     const BsdfDev* __restrict__ bp, const LightDev* __restrict__ lp, const float* __restrict__ P_,
     const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
-    const int32_t* __restrict__ hit_count, const uint8_t* __restrict__ vis,
+    const int32_t* __restrict__ hit_count, const float* __restrict__ lscale,
     float* __restrict__ rgb, float* __restrict__ wout, int RS, int per_wave) {
   extern __shared__ float smem[];
   const BsdfDev& bs = *bp;
@@ -808,7 +850,10 @@ __global__ void __launch_bounds__(256) k_shade_direct(
       }
       wave_lds_fence();
     }
-    if (vis && !vis[valid ? i : total - 1]) le[0] = le[1] = le[2] = 0.f;  // scene.py:297
+    if (lscale) {  // shadow test (scene.py:297) or learned occlusion (scene.py:313-318)
+      const float* sc = lscale + (valid ? i : total - 1) * 3;
+      le[0] *= sc[0]; le[1] *= sc[1]; le[2] *= sc[2];
+    }
     if (valid && lane < 32) {
       // integrators.py:186-189: mis(=1) * bsdf_val * emitter_val, / emitter_samples(=1)
       rgb[idx * 3] = (1.f * f[0]) * le[0];
@@ -849,7 +894,7 @@ template <int WV, bool FIELD>
 __global__ void __launch_bounds__(64 * WV, 1) k_light16(
     const ProgDev prog, const LightDev* __restrict__ lp, const float* __restrict__ P_,
     const float* __restrict__ N_, const float* __restrict__ WI, const int32_t* __restrict__ hit_idx,
-    const int32_t* __restrict__ hit_count, const uint8_t* __restrict__ vis, float* __restrict__ LS) {
+    const int32_t* __restrict__ hit_count, const float* __restrict__ lscale, float* __restrict__ LS) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const LightDev& lt = *lp;
   const int64_t total = *(const NRT_GLOBAL int32_t*)hit_count;
@@ -883,7 +928,10 @@ __global__ void __launch_bounds__(64 * WV, 1) k_light16(
       to_local(fr, ldx, ldy, ldz, wo);
       rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
     }
-    if (vis && !vis[valid ? i : total - 1]) le[0] = le[1] = le[2] = 0.f;  // scene.py:297
+    if (lscale) {  // shadow test (scene.py:297) or learned occlusion (scene.py:313-318)
+      const float* sc = lscale + (valid ? i : total - 1) * 3;
+      le[0] *= sc[0]; le[1] *= sc[1]; le[2] *= sc[2];
+    }
     if (valid && lane < 32) {
       float* o = LS + i * kLsStride;
       o[0] = le[0]; o[1] = le[1]; o[2] = le[2];

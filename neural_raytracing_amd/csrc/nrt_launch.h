@@ -132,6 +132,6 @@ int build_light_program(nrt_light* l);
 int build_bsdf_program(nrt_bsdf* b);
 int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                   const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                  const uint8_t* vis, float* rgb, float* weights_out, hipStream_t st);
+                  const float* lscale, float* rgb, float* weights_out, hipStream_t st);
 
 }  // namespace nrt

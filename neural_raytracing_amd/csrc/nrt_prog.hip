@@ -119,7 +119,7 @@ int persistent_blocks(K kern, int threads, size_t lds, int64_t want) {
 // NRT_EUNSUPPORTED when the program path does not cover this light / BSDF pair
 int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                   const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                  const uint8_t* vis, float* rgb, float* weights_out, hipStream_t st) {
+                  const float* lscale, float* rgb, float* weights_out, hipStream_t st) {
   const bool field = l->host_dev.kind == 0;
   if ((field && !l->prog.ok) || !b->prog.ok) return NRT_EUNSUPPORTED;
   constexpr int WV = kShadeWaves;
@@ -134,13 +134,13 @@ int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const f
       const size_t lds = ring::KEngine<WV>::lds_bytes(l->prog.d);
       if (!(rc = set_lds(kern, lds))) {
         kern<<<dim3(persistent_blocks(kern, 64 * WV, lds, want)), dim3(64 * WV), lds, st>>>(
-            l->prog.d, l->dev, p, n, wi, hit_idx, hit_count, vis, ls);
+            l->prog.d, l->dev, p, n, wi, hit_idx, hit_count, lscale, ls);
         rc = check_launch("k_light16");
       }
     } else {
       auto kern = k_light16<WV, false>;
       kern<<<dim3(persistent_blocks(kern, 64 * WV, 0, want)), dim3(64 * WV), 0, st>>>(
-          l->prog.d, l->dev, p, n, wi, hit_idx, hit_count, vis, ls);
+          l->prog.d, l->dev, p, n, wi, hit_idx, hit_count, lscale, ls);
       rc = check_launch("k_light16");
     }
   }

@@ -96,6 +96,18 @@ def _bsdf_handle(bsdf):
     return nrt()
 
 
+def _emitter_mode(w_isect):
+    """Which sample_emitter_dir_* the reference picks (integrators.py:161-166, :287-291):
+    True -> shadow ray (w_isect); a SkipConnMLP -> learned occlusion; anything else -> none.
+    Returns (shadow, occlusion-MLP handle or None)."""
+    from ..neural_blocks import SkipConnMLP
+    if w_isect is True:
+        return 1, None
+    if type(w_isect) is SkipConnMLP:
+        return 1, w_isect.nrt()
+    return 0, None
+
+
 class Direct(Integrator):
     """Direct lighting, one emitter sample, no BSDF sampling (integrators.py:139-206).
 
@@ -117,10 +129,7 @@ class Direct(Integrator):
 
     def sample(self, shapes, rays, bsdf, **kwargs):
         lights = kwargs.get("lights", self.lights)
-        w_isect = kwargs.get("w_isect")
-        if w_isect not in (None, False, True):
-            raise _lib.NrtError("Direct(w_isect=<occlusion MLP>) (learned occlusion, "
-                                "scene.py:301-319) is not on the HIP path yet")
+        shadow, occ = _emitter_mode(kwargs.get("w_isect"))
         if self.emitter_samples != 1 or self.bsdf_samples != 0:
             raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
         result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
@@ -133,16 +142,22 @@ class Direct(Integrator):
         args = (_lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
                 _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
                 _lib.ptr(rgb), _lib.ptr(weights))
-        if w_isect is True:
+        if shadow:
             # sample_emitter_dir_w_isect (scene.py:290-298): shadow ray to the point light,
-            # marched like SDF.intersect_test (sdfs.py:162-181)
+            # marched like SDF.intersect_test (sdfs.py:162-181); with an occlusion MLP,
+            # sample_emitter_dir_w_learned_occ (scene.py:301-319)
             from ..shapes.sdfs import sdf_handle
             lib = _lib.load(require_device=True)
             ws = torch.empty(lib.nrt_shadow_workspace_bytes(P), dtype=torch.uint8,
                              device=rays.device)
-            _lib.call("nrt_shade_direct_shadowed", _bsdf_handle(bsdf), _light_handle(lights),
-                      sdf_handle(shapes.sdf), int(shapes.max_steps), float(shapes.epsilon),
-                      *args, None, _lib.ptr(ws), _lib.precision_code(), _lib.stream())
+            head = (_bsdf_handle(bsdf), _light_handle(lights), sdf_handle(shapes.sdf))
+            steps = (int(shapes.max_steps), float(shapes.epsilon))
+            if occ is None:
+                _lib.call("nrt_shade_direct_shadowed", *head, *steps, *args, None, _lib.ptr(ws),
+                          _lib.precision_code(), _lib.stream())
+            else:
+                _lib.call("nrt_shade_direct_learned_occ", *head, occ, *steps, *args, None,
+                          _lib.ptr(ws), _lib.precision_code(), _lib.stream())
         else:
             _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), *args,
                       _lib.precision_code(), _lib.stream())
@@ -174,10 +189,8 @@ class Path(Integrator):
         from ..shapes.sdfs import sdf_handle
         sampler = kwargs.get("sampler", self.sampler)
         lights = kwargs.get("lights", self.lights)
-        w_isect = kwargs.get("w_isect", False)
+        shadow, occ = _emitter_mode(kwargs.get("w_isect", False))
         uniforms = kwargs.get("uniforms")
-        if w_isect not in (None, False, True):
-            raise _lib.NrtError("Path(w_isect=<occlusion MLP>) is not on the HIP path yet")
         dev = rays.device
         lead = rays.shape[:-1]
         it, active = shapes.intersect(rays, primary=self.training)
@@ -204,7 +217,7 @@ class Path(Integrator):
                 u_comp = torch.cat(draws, dim=1).contiguous()
                 u_sel = sampler.sample((P,), device=dev).contiguous()
             _lib.call("nrt_path_bounce", _bsdf_handle(bsdf), _light_handle(lights), sh,
-                      int(w_isect is True), int(shapes.max_steps), float(shapes.epsilon),
+                      shadow, occ, int(shapes.max_steps), float(shapes.epsilon),
                       _lib.ptr(curr.p.reshape(P, 3).contiguous()),
                       _lib.ptr(curr.n.reshape(P, 3).contiguous()),
                       _lib.ptr(curr.wi.reshape(P, 3).contiguous()), P, _lib.ptr(act),

@@ -519,6 +519,34 @@ def emitter_shadow_ray(it, shape, lights, active):
     return ds, le
 
 
+def dir_to_elev_azim(direc):
+    """utils.py:490-494."""
+    x, y, z = F.normalize(direc, dim=-1).clamp(min=-1 + 1e-7, max=1 - 1e-7).split(1, dim=-1)
+    elev = z.asin()
+    azim = torch.atan2(x, (1 - x.square() - z.square()).clamp(min=1e-10).sqrt())
+    return torch.cat([elev, azim], dim=-1)
+
+
+def emitter_learned_occ(it, shape, lights, occ, active):
+    """sample_emitter_dir_w_learned_occ, scene.py:301-319."""
+    ds, le = lights.sample_direction(it, active)
+    rays = torch.cat([it.p, ds.d], dim=-1)
+    visible = shape.intersect_test(rays, max_t=ds.dist.reshape_as(active)[..., None],
+                                   active=active)
+    occ_rays = torch.cat([it.p, dir_to_elev_azim(ds.d)], dim=-1)
+    le = torch.where((~visible)[..., None], occ(occ_rays).sigmoid() * le, le)
+    return ds, active[..., None] * le
+
+
+def emitter(it, shape, lights, active, w_isect):
+    """The sample_emitter choice of integrators.py:161-166 / :287-291."""
+    if w_isect is True:
+        return emitter_shadow_ray(it, shape, lights, active)
+    if isinstance(w_isect, SkipMLP):
+        return emitter_learned_occ(it, shape, lights, w_isect, active)
+    return emitter_no_shadow(it, lights, active)
+
+
 # ---------------------------------------------------------------------------------------------
 # Integrators  (integrators/integrators.py)
 # ---------------------------------------------------------------------------------------------
@@ -538,10 +566,7 @@ class DirectRef:
         it, active = shape.intersect(rays, primary=True, jitter=jitter)
         if not active.any():
             return result, active, it
-        if w_isect is True:
-            ds, le = emitter_shadow_ray(it, shape, lights, active)
-        else:
-            ds, le = emitter_no_shadow(it, lights, active)
+        ds, le = emitter(it, shape, lights, active, w_isect)
         ae = active & (torch.as_tensor(ds.pdf) > 0)
         wo = it.to_local(ds.d)
         f, pdf = bsdf.eval_and_pdf(it, wo, active=ae)
@@ -646,10 +671,7 @@ class PathRef:
         curr = it
         for depth in range(self.max_depth):
             if active.any():
-                if w_isect is True:
-                    ds, le = emitter_shadow_ray(curr, shape, lights, active)
-                else:
-                    ds, le = emitter_no_shadow(curr, lights, active)
+                ds, le = emitter(curr, shape, lights, active, w_isect)
                 ae = active & (torch.as_tensor(ds.pdf) > 0)
                 wo = curr.to_local(ds.d)
                 f, pdf = bsdf.eval_and_pdf(curr, wo, active=ae)

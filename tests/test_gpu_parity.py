@@ -584,6 +584,69 @@ def test_direct_shadow_rays_match_oracle(prec):
         assert -10 * math.log10(max(mse, 1e-12)) > 40
 
 
+def _occ_pair(out=1, seed=21):
+    """An occlusion MLP (SkipConnMLP 5 -> out, as w_isect takes it, scene.py:301-319): oracle
+    and product copies with the same weights."""
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    seeded(seed)
+    ref = R.SkipMLP(num_layers=4, hidden_size=64, in_size=5, out=out)
+    mine = SkipConnMLP(num_layers=4, hidden_size=64, in_size=5, out=out, device="cpu")
+    copy_mlp(mine, ref)
+    return ref, mine.cuda()
+
+
+@pytest.mark.parametrize("prec,out", [("fp32", 1), ("fp32", 3), ("fp16", 1)])
+def test_direct_learned_occlusion_matches_oracle(prec, out):
+    """Direct with w_isect=<SkipConnMLP> (sample_emitter_dir_w_learned_occ, scene.py:301-319):
+    shadow march, occ([p, dir_to_elev_azim(d)]) on the HIP MLP, sigmoid-scaled Le where occluded.
+    FP32 within 1e-4 except shadow-boundary flips (<= 0.5 % of pixels); FP16 by PSNR."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    ref, mine = _shadow_scene()
+    occ_ref, occ_mine = _occ_pair(out)
+    random.seed(8)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref["lights"], ref["camera"], R.DirectRef(), ref["bsdf"],
+                        size=64, chunk_size=64, background=0.0, with_noise=0.0, w_isect=occ_ref)
+        hard = R.render(ref["shape"], ref["lights"], ref["camera"], R.DirectRef(), ref["bsdf"],
+                        size=64, chunk_size=64, background=0.0, with_noise=0.0, w_isect=True)
+    # the learned term must light up pixels the hard shadow leaves black
+    lit = (want - hard).abs().amax(-1) > 1e-3
+    assert lit.sum() > 40
+    set_precision(prec)
+    random.seed(8)
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                                     bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
+                                     crop_size=64, uv=(0, 0), background=0, with_noise=0.0,
+                                     w_isect=occ_mine)
+    got = got.cpu()
+    assert got.shape == want.shape
+    if prec == "fp32":
+        close = (got - want).abs().amax(-1) <= 1e-4
+        assert close.float().mean() >= 0.995, (got - want).abs().max()
+    else:
+        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
+        assert -10 * math.log10(max(mse, 1e-12)) > 40
+
+
+def test_learned_occlusion_needs_5_inputs():
+    """nrt_shade_direct_learned_occ refuses an occlusion MLP that is not 5 -> 1|3."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import NrtError
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    _, mine = _shadow_scene()
+    bad = SkipConnMLP(num_layers=2, hidden_size=32, in_size=5, out=2, device="cuda")
+    with pytest.raises(NrtError):
+        with torch.no_grad():
+            pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                                bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
+                                crop_size=32, uv=(0, 0), background=0, with_noise=0.0,
+                                w_isect=bad)
+
+
 def test_direct_shadow_rays_need_point_light():
     """The reference's LightField samples carry no distance (lights.py:175-195), so
     w_isect=True cannot run with it there; the HIP path refuses it loudly."""
@@ -783,11 +846,17 @@ def _path_pair(seed=31):
     return ref, mine
 
 
-@pytest.mark.parametrize("prec,w_isect", [("fp32", False), ("fp32", True), ("fp16", True)])
+@pytest.mark.parametrize("prec,w_isect", [("fp32", False), ("fp32", True), ("fp16", True),
+                                          ("fp32", "occ")])
 def test_path_integrator_matches_oracle(prec, w_isect):
     """Path (integrators.py:275-354), two bounces, with injected BSDF-sampling uniforms: the
     emitter term per bounce (optionally shadowed), ComposeSpatialVarying.sample, throughput
     update and the secondary intersection, vs the oracle's PathRef."""
+    if w_isect == "occ":
+        occ_ref, occ_mine = _occ_pair(1, seed=23)
+        w_ref, w_mine = occ_ref, occ_mine
+    else:
+        w_ref = w_mine = w_isect
     from neural_raytracing_amd import set_precision
     from neural_raytracing_amd.pathtracer.integrators import Path
     ref, mine = _path_pair()
@@ -800,12 +869,12 @@ def test_path_integrator_matches_oracle(prec, w_isect):
                 for _ in range(2)]
     with torch.no_grad():
         want, wmask, _ = R.PathRef().sample(ref["shape"], rays, ref["bsdf"], ref["lights"],
-                                            w_isect=w_isect, uniforms=uniforms)
+                                            w_isect=w_ref, uniforms=uniforms)
     assert wmask.float().mean() > 0.2
     set_precision(prec)
     with torch.no_grad():
         got, mask, _ = Path().sample(mine["shape"], rays.cuda(), mine["bsdf"],
-                                     lights=mine["lights"], w_isect=w_isect, uniforms=uniforms)
+                                     lights=mine["lights"], w_isect=w_mine, uniforms=uniforms)
     got = got.cpu()
     assert torch.equal(mask.cpu(), wmask)
     assert got.shape == want.shape
