@@ -1,6 +1,8 @@
 // nrt_api_nerf.hip -- NeRFLE (NeRF + point-light, shapes/nerf.py:153-214) volume rendering:
 // sample points, first MLP (density + 64-d latent), second MLP (rgb from latent, direction and
 // light position), and the reference's front-to-back compositing with its quirks.
+#include <array>
+
 #include "nrt_launch.h"
 
 namespace nrt {
@@ -40,16 +42,17 @@ __global__ void k_nerf_second_in(const float* __restrict__ first_out, const floa
 // nerf.py:203-214: rgb = sigmoid(second), sigma = relu(alpha_raw), a_s = 1 - exp(-sigma t_s)
 // (absolute depth t, not a spacing), cp = cumprod(clamp(1 - a, 1e-10)) rolled by one with the
 // LAST entry set to 1: w_0 = a_0 cp_{S-1}, w_s = a_s cp_{s-1} (1 <= s <= S-2), w_{S-1} = a_{S-1}.
+// alpha_raw[i * astride] is the first MLP's output 0 of sample i, rgb_raw[i * 3 + k] the second's.
 template <int = 0>
-__global__ void k_nerf_composite(const float* __restrict__ first_out, const float* __restrict__ rgb_raw,
-                                 const float* __restrict__ ts, int64_t P, int S,
-                                 float* __restrict__ out) {
+__global__ void k_nerf_composite(const float* __restrict__ first_out, int astride,
+                                 const float* __restrict__ rgb_raw, const float* __restrict__ ts,
+                                 int64_t P, int S, float* __restrict__ out) {
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
        p += (int64_t)gridDim.x * blockDim.x) {
     // pass 1: cp_{S-1} (the product over every sample), needed by w_0
     float cp = 1.f;
     for (int s = 0; s < S; ++s) {
-      const float sig = fmaxf(first_out[((int64_t)s * P + p) * 65], 0.f);
+      const float sig = fmaxf(first_out[((int64_t)s * P + p) * astride], 0.f);
       const float a = 1.f - expf(-(sig * ts[s]));
       cp = cp * fmaxf(1.f - a, 1e-10f);
     }
@@ -58,7 +61,7 @@ __global__ void k_nerf_composite(const float* __restrict__ first_out, const floa
     float prev = 1.f;  // cp_{s-1}
     for (int s = 0; s < S; ++s) {
       const int64_t i = (int64_t)s * P + p;
-      const float sig = fmaxf(first_out[i * 65], 0.f);
+      const float sig = fmaxf(first_out[i * astride], 0.f);
       const float a = 1.f - expf(-(sig * ts[s]));
       const float w = s == S - 1 ? a * 1.f : (s == 0 ? a * cp_last : a * prev);
       prev = prev * fmaxf(1.f - a, 1e-10f);
@@ -70,6 +73,320 @@ __global__ void k_nerf_composite(const float* __restrict__ first_out, const floa
 }
 
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// ------------------------------------------------------------------------------------------
+// Fused FP16 NeRFLE sample kernel on the k-outer program engine (ring::KEngine): per wave 32
+// samples (columns); both MLPs, the second MLP's Fourier projection and its input assembly stay
+// in registers; only alpha_raw and rgb_raw (16 B per sample) reach HBM.
+//
+// Program chunk order (build_nerf_program, consumed in exactly this order per batch):
+//   first MLP (hidden 128 = 4 row blocks, F = 16, 3 -> 65): init enc [3 k-steps];
+//     per hidden layer: hidden [4][4] k-steps, + enc [3] on skip layers;
+//     out (3 row blocks): k-steps [0..4], [5..7]
+//   projection: A_hi (7 k-steps) then A_lo (7) of basis^T (16 x 70) in one chunk
+//   second MLP (hidden 64 = 2 row blocks, 70 -> 3): init enc [8][1]; per hidden layer hidden
+//     [4] or, on skip layers, hidden + enc [8][5]; out [4] (1 row block)
+// Second-MLP encoding k-steps (9): e0, e1 = sin/cos of projections q = 8e + 4h + jj (the usual
+// pair order); e2..e7 = the first MLP's output tiles in accumulator order (row 1 + k = latent k;
+// row 0 and rows > 64 have zero weight); e8 = (r_d, light) in half 0.
+// ------------------------------------------------------------------------------------------
+constexpr int kNerfWaves = 8;
+
+// acc[ib] += W[ib] * [b1[0..KS1), b2[0..KS2)] over chunks of KC k-steps
+template <int NB, int KS1, int KS2, int KC, int WV, int N1, int N2>
+__device__ __forceinline__ void nerf_layer(ring::KEngine<WV>& E, f16v (&acc)[NB],
+                                           const h8 (&b1)[N1], const h8 (&b2)[N2]) {
+  static_assert(KS1 <= N1 && KS2 <= N2, "fragment arrays too short");
+  constexpr int KS = KS1 + KS2;
+  constexpr int NCH = (KS + KC - 1) / KC;
+#pragma unroll
+  for (int cc = 0; cc < NCH; ++cc) {
+    const h8* A = E.begin();
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int s = cc * KC + j;
+      if (s < KS) {
+        const h8 b = s < KS1 ? b1[s < KS1 ? s : 0] : b2[s >= KS1 ? s - KS1 : 0];
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(j * NB + ib) * 64], b, acc[ib]);
+      }
+    }
+    E.end();
+  }
+}
+
+// the first MLP (nerf.py:162-163: 5 x 128, F = 16, 3 -> 65) with its 3 output row blocks
+template <int WV>
+__device__ __forceinline__ void nerf_first(ring::KEngine<WV>& E, const ProgMlp& pm, float x0,
+                                           float x1, float x2, f16v (&o)[3]) {
+  constexpr int NB = 4, NE = 3;
+  const int h = E.lane >> 5;
+  const float4* basis = E.lbasis + pm.basis_off;
+  f16v acc[NB];
+  h8 hv[2 * NB];
+  h8 enc[NE];
+#pragma unroll
+  for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<-1>(basis, s, NE - 1, h, x0, x1, x2);
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
+  nerf_layer<NB, NE, 0, 4>(E, acc, enc, enc);
+#pragma unroll
+  for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<ACT_LEAKY>(basis, s, NE - 1, h, x0, x1, x2);
+  for (int i = 0; i < pm.L; ++i) {
+    ring::kact<NB, ACT_LEAKY>(acc, hv);
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 1 + i, ib, h);
+    nerf_layer<NB, 2 * NB, 0, 4>(E, acc, hv, hv);
+    if (i != pm.L - 1 && (i % pm.skip) == 0) nerf_layer<NB, NE, 0, 4>(E, acc, enc, enc);
+  }
+  ring::kact<NB, ACT_LEAKY>(acc, hv);
+#pragma unroll
+  for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(pm, pm.L + 1, ob, h);
+  nerf_layer<3, 2 * NB, 0, 5>(E, o, hv, hv);
+}
+
+__device__ __forceinline__ h8 h8_of(const float (&v)[8]) {
+  h8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (_Float16)v[j];
+  return f;
+}
+
+template <int WV>
+__global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
+    const ProgDev prog, const float* __restrict__ rays, int64_t P, const float* __restrict__ ts,
+    int S, const float* __restrict__ light, float* __restrict__ alpha_raw,
+    float* __restrict__ rgb_raw) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int64_t n = (int64_t)S * P;
+  const int64_t per_block = 32 * WV;
+  if ((int64_t)blockIdx.x * per_block >= n) return;
+  ring::KEngine<WV> E;
+  E.init(prog, smem_c);
+  const int lane = lane_id(), h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const ProgMlp& m1 = prog.mlp[0];
+  const ProgMlp& m2 = prog.mlp[1];
+  const float lx = light[0], ly = light[1], lz = light[2];
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < n; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t g = b0 + 32 * wv + (lane & 31);
+    const bool valid = g < n;
+    const int64_t gg = valid ? g : n - 1;
+    const int64_t s = gg / P, p = gg - s * P;
+    const float t = ts[s];
+    const float* r = rays + p * 6;
+    const float dx = r[3], dy = r[4], dz = r[5];
+    // pts = r_o + t r_d (nerf.py:179, no FMA contraction)
+    const float x0 = __fadd_rn(r[0], __fmul_rn(t, dx));
+    const float x1 = __fadd_rn(r[1], __fmul_rn(t, dy));
+    const float x2 = __fadd_rn(r[2], __fmul_rn(t, dz));
+    f16v o[3];
+    nerf_first<WV>(E, m1, x0, x1, x2, o);
+    // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
+    h8 e[9], ea[9], lo[7];
+#pragma unroll
+    for (int tt = 0; tt < 6; ++tt) {
+      float v[8], va[8], vl[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[j] = o[tt >> 1][8 * (tt & 1) + j];
+        va[j] = act_fwd<true>(v[j], ACT_LEAKY);
+        vl[j] = v[j] - (float)(_Float16)v[j];
+      }
+      e[2 + tt] = h8_of(v); ea[2 + tt] = h8_of(va); lo[tt] = h8_of(vl);
+    }
+    {
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, va[8], vl[8];
+      if (h == 0) { v[0] = dx; v[1] = dy; v[2] = dz; v[3] = lx; v[4] = ly; v[5] = lz; }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        va[j] = act_fwd<true>(v[j], ACT_LEAKY);
+        vl[j] = v[j] - (float)(_Float16)v[j];
+      }
+      e[8] = h8_of(v); ea[8] = h8_of(va); lo[6] = h8_of(vl);
+    }
+    // projections x @ B (utils.py:37-40) as hi*hi + lo(A)*hi + hi*lo(x): FP32-accurate
+    f16v pq;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pq[k] = 0.f;
+    {
+      const h8* A = E.begin();
+#pragma unroll
+      for (int tt = 0; tt < 7; ++tt) {
+        pq = mfma16(A[tt * 64], e[2 + tt], pq);
+        pq = mfma16(A[(7 + tt) * 64], e[2 + tt], pq);
+        pq = mfma16(A[tt * 64], lo[tt], pq);
+      }
+      E.end();
+    }
+    // rows q = (reg & 3) + 8 (reg >> 2) + 4h: regs 0..3 -> q = 4h + jj, regs 4..7 -> 8 + 4h + jj
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      float v[8], va[8];
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        v[2 * jj] = __sinf(pq[4 * s2 + jj]);
+        v[2 * jj + 1] = __cosf(pq[4 * s2 + jj]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) va[j] = act_fwd<true>(v[j], ACT_LEAKY);
+      e[s2] = h8_of(v); ea[s2] = h8_of(va);
+    }
+    // the second MLP (nerf.py:168-172: 8 x 64, 70 -> 3)
+    constexpr int NB = 2;
+    f16v acc[NB];
+    h8 hv[2 * NB];
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
+    nerf_layer<NB, 9, 0, 8>(E, acc, e, e);
+    for (int i = 0; i < m2.L; ++i) {
+      ring::kact<NB, ACT_LEAKY>(acc, hv);
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 1 + i, ib, h);
+      if (i != m2.L - 1 && (i % m2.skip) == 0) nerf_layer<NB, 2 * NB, 9, 8>(E, acc, hv, ea);
+      else nerf_layer<NB, 2 * NB, 0, 8>(E, acc, hv, hv);
+    }
+    ring::kact<NB, ACT_LEAKY>(acc, hv);
+    f16v out[1] = {E.bias_at(m2, m2.L + 1, 0, h)};
+    nerf_layer<1, 2 * NB, 0, 8>(E, out, hv, hv);
+    if (valid && h == 0) {
+      alpha_raw[g] = o[0][0];
+      rgb_raw[g * 3] = out[0][0]; rgb_raw[g * 3 + 1] = out[0][1]; rgb_raw[g * 3 + 2] = out[0][2];
+    }
+  }
+}
+
+// first: 3 -> 65, hidden 128, F 16; second: 70 -> 3, hidden 64, F 16; both leaky_relu, no latent
+static bool nerf_fusable(const nrt_mlp* f, const nrt_mlp* s) {
+  const MlpDev& a = f->host_dev;
+  const MlpDev& b = s->host_dev;
+  return a.in_size == 3 && a.nb == 4 && a.freqs == 16 && a.out == 65 && a.latent == 0 &&
+         a.act == ACT_LEAKY && b.in_size == 70 && b.nb == 2 && b.freqs == 16 && b.out == 3 &&
+         b.latent == 0 && b.act == ACT_LEAKY && (int)f->host_w.size() == a.n_hidden + 2 &&
+         (int)s->host_w.size() == b.n_hidden + 2 && a.ke == 48;
+}
+
+// the program stream of k_nerfle16 (chunk order in the kernel's header comment)
+static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out) {
+  out.ok = false;
+  const MlpDev& a = f->host_dev;
+  const MlpDev& b = s->host_dev;
+  typedef std::array<_Float16, 512> Frag;  // [lane][8]
+  std::vector<Frag> frags;
+  std::vector<int> coff;
+  // first MLP: its own k-outer stream, out layer split into k-steps [0..4] and [5..7]
+  frags.resize(a.nk_frags);
+  NRT_HIP(hipMemcpy(frags.data(), a.streamk16, (size_t)a.nk_frags * 1024, hipMemcpyDeviceToHost));
+  for (size_t c = 0; c + 1 < f->host_chunkk.size(); ++c) coff.push_back(f->host_chunkk[c]);
+  coff.push_back(f->host_chunkk.back());
+  coff.push_back(f->host_chunkk.back() + 5 * 3);
+  // element (h, j) of second-MLP encoding k-step e -> reference input column (-1: none)
+  const int IN = 70, F = 16;
+  auto enc_col = [&](int e, int hf, int j) -> int {
+    if (e < 2) {
+      const int q = 8 * e + 4 * hf + (j >> 1);
+      return (j & 1) ? IN + F + q : IN + q;
+    }
+    if (e < 8) {
+      const int t = e - 2;
+      const int r = 32 * (t >> 1) + 16 * (t & 1) + 8 * (j >> 2) + 4 * hf + (j & 3);
+      return (r >= 1 && r <= 64) ? r - 1 : -1;
+    }
+    return (hf == 0 && j < 6) ? 64 + j : -1;
+  };
+  // projection chunk: A[q][k] = basis[x index of k][q] split into hi and lo halves
+  coff.push_back((int)frags.size());
+  for (int part = 0; part < 2; ++part)
+    for (int tt = 0; tt < 7; ++tt) {
+      Frag fr;
+      for (int lane = 0; lane < 64; ++lane) {
+        const int q = lane & 31, hf = lane >> 5;
+        for (int j = 0; j < 8; ++j) {
+          const int col = enc_col(2 + tt, hf, j);
+          const float v = (q < F && col >= 0) ? s->host_basis[(size_t)col * F + q] : 0.f;
+          const _Float16 hi = (_Float16)v;
+          fr[lane * 8 + j] = part == 0 ? hi : (_Float16)(v - (float)hi);
+        }
+      }
+      frags.push_back(fr);
+    }
+  // second MLP: k-steps per layer (hidden, then the 9 encoding steps), chunks of 8 k-steps
+  const int H = 64, NB = 2, L = b.n_hidden;
+  for (int l = 0; l < L + 2; ++l) {
+    const bool init = l == 0, outl = l == L + 1;
+    const int i = l - 1;
+    const bool skip = !init && !outl && i != L - 1 && (i % b.skip) == 0;
+    const bool hid = !init;
+    const bool enc = init || skip;
+    const int R = outl ? 3 : H, C = (hid ? H : 0) + (enc ? IN + 2 * F : 0);
+    const std::vector<float>& W = s->host_w[l];
+    const int nrb = outl ? 1 : NB;
+    const int ks = (hid ? 2 * NB : 0) + (enc ? 9 : 0);
+    const int base = (int)frags.size();
+    for (int st = 0; st < ks; ++st)
+      for (int ib = 0; ib < nrb; ++ib) {
+        Frag fr;
+        for (int lane = 0; lane < 64; ++lane) {
+          const int row = 32 * ib + (lane & 31), hf = lane >> 5;
+          for (int j = 0; j < 8; ++j) {
+            int col;
+            if (hid && st < 2 * NB)
+              col = 32 * (st >> 1) + 16 * (st & 1) + 8 * (j >> 2) + 4 * hf + (j & 3);
+            else {
+              const int c = enc_col(st - (hid ? 2 * NB : 0), hf, j);
+              col = c < 0 ? -1 : (hid ? H : 0) + c;
+            }
+            const float v = (row < R && col >= 0 && col < C) ? W[(size_t)row * C + col] : 0.f;
+            fr[lane * 8 + j] = (_Float16)v;
+          }
+        }
+        frags.push_back(fr);
+      }
+    for (int st = 0; st < ks; st += 8) coff.push_back(base + st * nrb);
+  }
+  const size_t nfr = frags.size();
+  frags.resize(nfr + 64);
+  for (size_t q = nfr; q < frags.size(); ++q) frags[q].fill((_Float16)0.f);
+  // biases [first: L1 + 2 layers x 128][second: L2 + 2 layers x 64]; first basis as float4
+  std::vector<float> bias(f->host_bias);
+  const int boff2 = (int)bias.size();
+  bias.insert(bias.end(), s->host_bias.begin(), s->host_bias.end());
+  std::vector<float4> basis;
+  for (int q = 0; q < a.freqs; ++q)
+    basis.push_back(make_float4(f->host_basis[q], f->host_basis[a.freqs + q],
+                                f->host_basis[2 * a.freqs + q], 0.f));
+  ProgDev& d = out.d;
+  std::memset(&d, 0, sizeof(d));
+  d.n_mlp = 2;
+  d.n_chunks = (int)coff.size();
+  d.bias_floats = (int)bias.size();
+  d.basis_q = (int)basis.size();
+  ProgMlp& p1 = d.mlp[0];
+  p1.nb = 4; p1.ne = 3; p1.ob = 3; p1.L = a.n_hidden; p1.skip = a.skip; p1.out = a.out;
+  p1.act = a.act; p1.F = a.freqs; p1.bias_off = 0; p1.bstride = a.bias16_stride; p1.basis_off = 0;
+  ProgMlp& p2 = d.mlp[1];
+  p2.nb = 2; p2.ne = 9; p2.ob = 1; p2.L = b.n_hidden; p2.skip = b.skip; p2.out = b.out;
+  p2.act = b.act; p2.F = b.freqs; p2.bias_off = boff2; p2.bstride = b.bias16_stride;
+  p2.basis_off = 0;
+  const size_t stream_bytes = frags.size() * 1024;
+  const size_t o_coff = a256(stream_bytes);
+  const size_t o_bias = a256(o_coff + coff.size() * 4);
+  const size_t o_basis = a256(o_bias + bias.size() * 4);
+  const size_t total = a256(o_basis + basis.size() * 16);
+  char* buf = nullptr;
+  NRT_HIP(hipMalloc((void**)&buf, total));
+  out.buf = buf;
+  NRT_HIP(hipMemcpy(buf, frags.data(), stream_bytes, hipMemcpyHostToDevice));
+  NRT_HIP(hipMemcpy(buf + o_coff, coff.data(), coff.size() * 4, hipMemcpyHostToDevice));
+  NRT_HIP(hipMemcpy(buf + o_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
+  NRT_HIP(hipMemcpy(buf + o_basis, basis.data(), basis.size() * 16, hipMemcpyHostToDevice));
+  d.stream = reinterpret_cast<const h8*>(buf);
+  d.coff = reinterpret_cast<const int*>(buf + o_coff);
+  d.bias = reinterpret_cast<const float*>(buf + o_bias);
+  d.basis = reinterpret_cast<const float4*>(buf + o_basis);
+  out.ok = true;
+  return NRT_OK;
+}
 
 }  // namespace nrt
 
@@ -96,6 +413,35 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   hipStream_t st = (hipStream_t)stream;
   const size_t n = (size_t)P * S;
   char* ws = (char*)workspace;
+  if (precision == NRT_FP16 && std::getenv("NRT_NERF_UNFUSED") == nullptr &&
+      nerf_fusable(first, second)) {
+    if (!second->nerf_prog || second->nerf_first_serial != first->serial) {
+      std::unique_ptr<nrt_prog> pr(new nrt_prog());
+      if (int rc = build_nerf_program(first, second, *pr)) return rc;
+      second->nerf_prog = std::move(pr);
+      second->nerf_first_serial = first->serial;
+    }
+    const ProgDev& pd = second->nerf_prog->d;
+    float* alpha = (float*)ws;
+    float* rgb_raw = (float*)(ws + a256(n * 4));
+    auto kern = k_nerfle16<kNerfWaves>;
+    const size_t lds = ring::KEngine<kNerfWaves>::lds_bytes(pd);
+    if (int rc = set_lds(kern, lds)) return rc;
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    const int64_t want = ceil_div64((int64_t)n, 32 * kNerfWaves);
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, cus));
+    ProfScope prof("k_nerfle", st);
+    kern<<<dim3(blocks), dim3(64 * kNerfWaves), lds, st>>>(pd, rays, P, ts, S, light, alpha, rgb_raw);
+    if (int rc = check_launch("k_nerfle16")) return rc;
+    k_nerf_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(
+        alpha, 1, rgb_raw, ts, P, S, rgb);
+    return check_launch("k_nerf_composite");
+  }
   float* pts = (float*)ws;
   float* f1 = (float*)(ws + a256(n * 12));
   float* x2 = (float*)(ws + a256(n * 12) + a256(n * 260));
@@ -109,7 +455,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   if (int rc = check_launch("k_nerf_second_in")) return rc;
   if (int rc = nrt_mlp_forward(second, x2, nullptr, (int64_t)n, c2, precision, stream)) return rc;
   k_nerf_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(
-      f1, c2, ts, P, S, rgb);
+      f1, 65, c2, ts, P, S, rgb);
   return check_launch("k_nerf_composite");
 }
 

@@ -2,11 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/nrt.h"
 #include "nrt_device.h"
+
+struct nrt_prog;
 
 struct nrt_mlp {
   nrt_mlp_desc desc;
@@ -18,6 +22,12 @@ struct nrt_mlp {
   std::vector<int> host_chunkk;  // k-outer chunk offsets
   std::vector<float> host_bias;  // unfolded biases [layer][bias16_stride]
   std::vector<float> host_basis; // [in][F]
+  std::vector<std::vector<float>> host_w;  // original weights per linear (init, hidden..., out)
+  // fused NeRFLE program built for (nerf_first, this) on first use (nrt_api_nerf.hip)
+  mutable std::unique_ptr<nrt_prog> nerf_prog;
+  mutable uint64_t nerf_first_serial = 0;
+  uint64_t serial = 0;  // unique per created MLP (cache key; addresses can be reused)
+  ~nrt_mlp();
 };
 
 // A device program (ProgDev) and the buffer holding its stream, chunk table, biases and basis.

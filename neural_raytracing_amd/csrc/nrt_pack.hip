@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -247,12 +248,15 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
 
   std::unique_ptr<nrt_mlp> m(new nrt_mlp());
   m->desc = *d;
+  static std::atomic<uint64_t> next_serial{1};
+  m->serial = next_serial.fetch_add(1);
   m->blob_bytes = blob.bytes.size();
   m->host_chunkk = chunkk_off;
   m->host_bias.assign(layers.size() * (size_t)bstride, 0.f);
   for (size_t l = 0; l < layers.size(); ++l)
     for (int r = 0; r < layers[l].R; ++r) m->host_bias[l * bstride + r] = layers[l].b[r];
   m->host_basis.assign(basis, basis + (size_t)in * F);
+  for (const Layer& ly : layers) m->host_w.emplace_back(ly.W, ly.W + (size_t)ly.R * ly.C);
   NRT_HIP(hipMalloc(&m->blob, m->blob_bytes));
   NRT_HIP(hipMemcpy(m->blob, blob.bytes.data(), m->blob_bytes, hipMemcpyHostToDevice));
   char* base = static_cast<char*>(m->blob);
@@ -282,6 +286,8 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   *out = m.release();
   return NRT_OK;
 }
+
+nrt_mlp::~nrt_mlp() = default;  // nrt_prog is complete here
 
 extern "C" int nrt_mlp_destroy(nrt_mlp* m) {
   if (!m) return NRT_OK;

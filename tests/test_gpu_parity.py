@@ -763,11 +763,17 @@ def _nerfle_pair(seed=19):
     return ref, mine.cuda()
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
-def test_nerfle_matches_oracle(prec):
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16-unfused"])
+def test_nerfle_matches_oracle(prec, monkeypatch):
     """NeRFLE (nerf.py:153-214): 64 samples per ray through both MLPs and the reference's
-    rolled-cumprod compositing, on nrt_nerfle_forward, vs the oracle; ragged ray count."""
+    rolled-cumprod compositing, on nrt_nerfle_forward, vs the oracle; ragged ray count.
+    "fp16" runs the fused k_nerfle16 program kernel, "fp16-unfused" the per-MLP kernels."""
     from neural_raytracing_amd import set_precision
+    if prec == "fp16-unfused":
+        monkeypatch.setenv("NRT_NERF_UNFUSED", "1")
+        prec = "fp16"
+    else:
+        monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
     from neural_raytracing_amd.pathtracer.lights import PointLights
     ref, mine = _nerfle_pair()
     g = torch.Generator().manual_seed(4)
