@@ -259,18 +259,26 @@ int nrt_composite(const float* rgb, const float* throughput, const uint8_t* hit,
                   int32_t channels, int32_t X0, int32_t Y0, void* stream);
 
 /* ---------------------------------------------------------------------------------------
- * NeRFLE (shapes/nerf.py:153-214, envmap=False), driven by NeRFReproduce.sample
- * (integrators.py:260-267): for each ray and each depth ts[s] (the caller's
- * linspace(0, 2 + random()*0.1, S)), first = MLP_5x128(o + ts[s] d) -> (alpha_raw, latent[64]),
+ * NeRFLE (shapes/nerf.py:153-214), driven by NeRFReproduce.sample (integrators.py:260-267):
+ * for each ray and each depth ts[s] (the caller's linspace(0, 2 + random()*0.1, S)),
+ * first = MLP_5x128(o + ts[s] d) -> (alpha_raw, latent[64]),
  * rgb_s = sigmoid(MLP_8x64([latent, d, light])), composited with the reference's weights
  * (alpha = 1 - exp(-relu(alpha_raw) t), rolled cumprod with the last entry 1).
- * first: 3 -> 65, second: 70 -> 3.  ts[S] and light[3] are device arrays; rgb [P,3].
- * workspace: nrt_nerfle_workspace_bytes(P, S) bytes of device memory.
+ * light[light_dim] (device) is the point light's location (envmap=False, light_dim 3) or
+ * its envmap encoding from nrt_light_envmap (envmap=True, light_dim 3 bins^2).
+ * first: 3 -> 65, second: (67 + light_dim) -> 3.  ts[S] device; rgb [P,3].  FP16 with the
+ * default shapes (light_dim 3) runs the fused k_nerfle16 kernel.
+ * workspace: nrt_nerfle_workspace_bytes(P, S, light_dim) bytes of device memory.
  * ------------------------------------------------------------------------------------- */
-size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S);
+size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim);
 int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays, int64_t P,
-                       const float* ts, int32_t S, const float* light, float* rgb,
-                       void* workspace, int precision, void* stream);
+                       const float* ts, int32_t S, const float* light, int32_t light_dim,
+                       float* rgb, void* workspace, int precision, void* stream);
+
+/* NeRFLE's envmap light encoding (nerf.py:183-191): PointLights.envmap (lights.py:81-88) at
+ * elev_azim_to_dir (utils.py:478-486) of meshgrid(linspace(0, 180, bins), linspace(0, 45, bins))
+ * -> out[bins^2 * 3] (device).  Point lights only (NRT_EUNSUPPORTED otherwise). */
+int nrt_light_envmap(const nrt_light* light, int32_t bins, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Kernel timing (bench / profiling aid; no reference counterpart)

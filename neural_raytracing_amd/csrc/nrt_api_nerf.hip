@@ -22,21 +22,47 @@ __global__ void k_nerf_points(const float* __restrict__ rays, int64_t P, const f
   }
 }
 
-// second MLP input [latent (64) | r_d (3) | light location (3)]   (nerf.py:197-203)
+// second MLP input [latent (64) | r_d (3) | light encoding (LK)]   (nerf.py:182-203): the point
+// light's location (LK = 3) or its envmap over bins^2 directions (LK = 3 bins^2)
 template <int = 0>
 __global__ void k_nerf_second_in(const float* __restrict__ first_out, const float* __restrict__ rays,
-                                 int64_t P, int S, const float* __restrict__ light,
+                                 int64_t P, int S, const float* __restrict__ light, int LK,
                                  float* __restrict__ x2) {
   const int64_t n = (int64_t)S * P;
+  const int in2 = 67 + LK;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = i % P;
     const float* f = first_out + i * 65;
-    float* o = x2 + i * 70;
+    float* o = x2 + i * in2;
     for (int k = 0; k < 64; ++k) o[k] = f[1 + k];
     o[64] = rays[p * 6 + 3]; o[65] = rays[p * 6 + 4]; o[66] = rays[p * 6 + 5];
-    o[67] = light[0]; o[68] = light[1]; o[69] = light[2];
+    for (int k = 0; k < LK; ++k) o[67 + k] = light[k];
   }
+}
+
+// torch.linspace(start, end, steps)[k] (float32, symmetric two-sided formula)
+__device__ __forceinline__ float linspace_at(float start, float end, int steps, int k) {
+  if (steps == 1) return start;
+  const float step = (end - start) / (float)(steps - 1);
+  return k < steps / 2 ? start + step * (float)k : end - step * (float)(steps - k - 1);
+}
+
+// PointLights.envmap(elev_azim_to_dir(meshgrid(linspace(0, 180, bins), linspace(0, 45, bins))))
+// (nerf.py:183-191, utils.py:478-486, lights.py:81-88); the degrees go in as radians, as there.
+template <int = 0>
+__global__ void k_light_envmap(const LightDev* __restrict__ lp, int bins, float* __restrict__ out) {
+  const LightDev& lt = *lp;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= bins * bins) return;
+  const float limit = 3.14159265358979f - 1e-7f;
+  const float elev = fminf(fmaxf(linspace_at(0.f, 180.f, bins, i / bins), -limit), limit);
+  const float azim = fminf(fmaxf(linspace_at(0.f, 45.f, bins, i % bins), -limit), limit);
+  const float dx = sinf(azim) * cosf(elev), dy = cosf(azim) * cosf(elev), dz = sinf(elev);
+  const float vx = dx - lt.loc[0], vy = dy - lt.loc[1], vz = dz - lt.loc[2];
+  const float dist = sqrtf(vx * vx + vy * vy + vz * vz);
+  const float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
+  for (int k = 0; k < 3; ++k) out[i * 3 + k] = lt.scaled_dir[k] / fall;
 }
 
 // nerf.py:203-214: rgb = sigmoid(second), sigma = relu(alpha_raw), a_s = 1 - exp(-sigma t_s)
@@ -394,20 +420,32 @@ using namespace nrt;
 
 extern "C" {
 
-size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S) {
+size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim) {
   const size_t n = (size_t)std::max<int64_t>(P, 1) * (size_t)std::max(S, 1);
-  return a256(n * 3 * 4) + a256(n * 65 * 4) + a256(n * 70 * 4) + a256(n * 3 * 4);
+  const size_t in2 = 67 + (size_t)std::max(light_dim, 3);
+  return a256(n * 3 * 4) + a256(n * 65 * 4) + a256(n * in2 * 4) + a256(n * 3 * 4);
+}
+
+int nrt_light_envmap(const nrt_light* l, int32_t bins, float* out, void* stream) {
+  if (!l || bins < 1 || !out) { set_error("nrt_light_envmap: bad argument"); return NRT_EINVAL; }
+  if (l->host_dev.kind != 1) {
+    set_error("nrt_light_envmap: envmap is defined for PointLights only (lights.py:81-88)");
+    return NRT_EUNSUPPORTED;
+  }
+  k_light_envmap<><<<dim3(ceil_div64(bins * bins, 64)), dim3(64), 0, (hipStream_t)stream>>>(l->dev, bins, out);
+  return check_launch("k_light_envmap");
 }
 
 int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays, int64_t P,
-                       const float* ts, int32_t S, const float* light, float* rgb, void* workspace,
-                       int precision, void* stream) {
+                       const float* ts, int32_t S, const float* light, int32_t light_dim,
+                       float* rgb, void* workspace, int precision, void* stream) {
   if (!first || !second || P < 0 || S < 1) { set_error("nrt_nerfle_forward: bad argument"); return NRT_EINVAL; }
   if (P == 0) return NRT_OK;
   if (!rays || !ts || !light || !rgb || !workspace) { set_error("nrt_nerfle_forward: null argument"); return NRT_EINVAL; }
-  if (first->desc.in_size != 3 || first->desc.out != 65 || second->desc.in_size != 70 ||
-      second->desc.out != 3) {
-    set_error("nrt_nerfle_forward: expects first 3 -> 65 and second 70 -> 3 (nerf.py:162-172)");
+  if (first->desc.in_size != 3 || first->desc.out != 65 || light_dim < 3 ||
+      second->desc.in_size != 67 + light_dim || second->desc.out != 3) {
+    set_error("nrt_nerfle_forward: expects first 3 -> 65 and second (67 + light_dim) -> 3 "
+              "(nerf.py:162-172)");
     return NRT_EINVAL;
   }
   hipStream_t st = (hipStream_t)stream;
@@ -445,13 +483,14 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   float* pts = (float*)ws;
   float* f1 = (float*)(ws + a256(n * 12));
   float* x2 = (float*)(ws + a256(n * 12) + a256(n * 260));
-  float* c2 = (float*)(ws + a256(n * 12) + a256(n * 260) + a256(n * 280));
+  const size_t in2 = 67 + (size_t)light_dim;
+  float* c2 = (float*)(ws + a256(n * 12) + a256(n * 260) + a256(n * in2 * 4));
   const int blocks = (int)std::min<int64_t>(ceil_div64((int64_t)n, 256), 4096);
   ProfScope prof("k_nerfle", st);
   k_nerf_points<><<<dim3(blocks), dim3(256), 0, st>>>(rays, P, ts, S, pts);
   if (int rc = check_launch("k_nerf_points")) return rc;
   if (int rc = nrt_mlp_forward(first, pts, nullptr, (int64_t)n, f1, precision, stream)) return rc;
-  k_nerf_second_in<><<<dim3(blocks), dim3(256), 0, st>>>(f1, rays, P, S, light, x2);
+  k_nerf_second_in<><<<dim3(blocks), dim3(256), 0, st>>>(f1, rays, P, S, light, light_dim, x2);
   if (int rc = check_launch("k_nerf_second_in")) return rc;
   if (int rc = nrt_mlp_forward(second, x2, nullptr, (int64_t)n, c2, precision, stream)) return rc;
   k_nerf_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(

@@ -1,6 +1,6 @@
-"""Volumetric NeRF shapes (shapes/nerf.py).  ``NeRFLE`` (NeRF + point light, envmap=False) renders
-through ``nrt_nerfle_forward``: sample points, both MLPs and the reference's compositing on the
-GPU.  Constructor and RNG consumption follow nerf.py:153-172."""
+"""Volumetric NeRF shapes (shapes/nerf.py).  ``NeRFLE`` (NeRF + point light, or NeRF + envmap
+light with envmap=True) renders through ``nrt_nerfle_forward``: sample points, both MLPs and the
+reference's compositing on the GPU.  Constructor and RNG consumption follow nerf.py:153-172."""
 import random
 
 import torch
@@ -15,8 +15,8 @@ class NeRFLE(nn.Module):
 
     forward(rays [..., 6], lights) -> rgb [..., 3] with 64 samples at
     ts = linspace(0, 2 + random.random() * 0.1, 64) (nerf.py:178; one ``random.random()`` draw per
-    call, as in the reference).  ``envmap=True`` (light encoded by ``lights.envmap``) is not on the
-    HIP path yet.
+    call, as in the reference).  The colour MLP sees the point light's location, or with
+    ``envmap=True`` its envmap over bins^2 directions (``nrt_light_envmap``, nerf.py:183-191).
     """
 
     # samples per nrt_nerfle_forward call (bounds the [S*P, 65/70] intermediates to ~2.3 GB)
@@ -34,8 +34,6 @@ class NeRFLE(nn.Module):
         self.steps = steps  # nerf.py:178 hard-codes 64; BASELINE cfg5 asks 256
 
     def forward(self, rays, lights):
-        if getattr(self, "envmap", False):
-            raise _lib.NrtError("NeRFLE(envmap=True) is not on the HIP path yet")
         if not rays.is_cuda:
             raise _lib.NrtError("NeRFLE renders on the HIP path only: move it and the rays to the GPU")
         lead = rays.shape[:-1]
@@ -44,16 +42,25 @@ class NeRFLE(nn.Module):
         dev = flat.device
         # torch.linspace on the host: the same float32 sequence the CPU reference computes
         ts = torch.linspace(0, 2 + random.random() * 0.1, self.steps).to(dev)
-        light = lights.location.reshape(-1, 3)[0].detach().float().to(dev).contiguous()
-        rgb = torch.empty(P, 3, device=dev)
         lib = _lib.load(require_device=True)
+        if getattr(self, "envmap", False):
+            handle = getattr(lights, "nrt", None)
+            if handle is None or not hasattr(lights, "envmap"):
+                raise _lib.NrtError("NeRFLE(envmap=True) needs PointLights (lights.envmap, "
+                                    "lights.py:81-88)")
+            light = torch.empty(3 * self.bins * self.bins, device=dev)
+            _lib.call("nrt_light_envmap", handle(), self.bins, _lib.ptr(light), _lib.stream())
+        else:
+            light = lights.location.reshape(-1, 3)[0].detach().float().to(dev).contiguous()
+        rgb = torch.empty(P, 3, device=dev)
         chunk = max(1, min(P, self.MAX_SAMPLES_PER_CALL // self.steps))
-        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(chunk, self.steps), dtype=torch.uint8,
-                         device=dev)
+        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(chunk, self.steps, light.numel()),
+                         dtype=torch.uint8, device=dev)
         first, second = self.first.nrt(), self.second.nrt()
         for r0 in range(0, P, chunk):
             n = min(chunk, P - r0)
             _lib.call("nrt_nerfle_forward", first, second, _lib.ptr(flat[r0:r0 + n]), n,
-                      _lib.ptr(ts), self.steps, _lib.ptr(light), _lib.ptr(rgb[r0:r0 + n]),
+                      _lib.ptr(ts), self.steps, _lib.ptr(light), light.numel(),
+                      _lib.ptr(rgb[r0:r0 + n]),
                       _lib.ptr(ws), _lib.precision_code(), _lib.stream())
         return rgb.reshape(lead + (3,))

@@ -502,6 +502,22 @@ class PointLightRef(nn.Module):
         return LightSample(d, 1, dist), le
 
 
+def elev_azim_to_dir(elev_azim):
+    """utils.py:478-486."""
+    limit = math.pi - 1e-7
+    elev, azim = elev_azim.clamp(min=-limit, max=limit).split(1, dim=-1)
+    return torch.cat([azim.sin() * elev.cos(), azim.cos() * elev.cos(), elev.sin()], dim=-1)
+
+
+def point_light_envmap(light, p):
+    """PointLights.envmap, lights.py:81-88."""
+    d = p[None, ...] - light.location[:, None, None, :]
+    dist = torch.linalg.norm(d, dim=-1, keepdim=True)
+    fall = light.const.clamp(min=1e-6) + light.linear.clamp(min=1e-6) * dist \
+        + light.square.clamp(min=1e-6) * dist.square()
+    return light.scale * F.normalize(light.intensity, dim=-1) / fall.clamp(min=1e-6)
+
+
 def emitter_no_shadow(it, lights, active):
     """sample_emitter_dir_wo_isect, scene.py:321-324."""
     ds, le = lights.sample_direction(it, active)
@@ -925,20 +941,25 @@ def render(shape, lights, camera, integrator, bsdf, size, chunk_size, background
 # ---------------------------------------------------------------------------------------------
 
 class NeRFLERef(nn.Module):
-    """NeRFLE (envmap=False, NeRF+PT), nerf.py:153-214.
+    """NeRFLE, nerf.py:153-214 (envmap=False: NeRF+PT; envmap=True: NeRF+LE).
 
     Reproduces the reference's compositing quirks: ``alpha = 1-exp(-sigma * t)`` with the
-    absolute depth, and ``roll(cumprod, 1)`` with the LAST entry set to 1.
+    absolute depth, and ``roll(cumprod, 1)`` with the LAST entry set to 1.  With envmap the
+    colour MLP sees ``lights.envmap`` at ``bins^2`` directions built from degree values passed
+    as radians (:183-191).
     """
 
-    def __init__(self, steps=64):
+    def __init__(self, steps=64, envmap=False, bins=4):
         super().__init__()
         self.latent_size = 64
         self.first = SkipMLP(num_layers=5, hidden_size=128, in_size=3, out=1 + self.latent_size)
-        self.second = SkipMLP(in_size=self.latent_size + 6, out=3)
+        self.bins = bins
+        self.second = SkipMLP(in_size=self.latent_size + (6 if not envmap else 3 + bins * bins * 3),
+                              out=3)
+        self.envmap = envmap
         self.steps = steps
 
-    def forward(self, rays, light_location, jitter=None):
+    def forward(self, rays, light_location, jitter=None, light=None):
         r_o, r_d = rays.split([3, 3], dim=-1)
         if jitter is None:
             jitter = random.random()
@@ -947,9 +968,18 @@ class NeRFLERef(nn.Module):
         first = self.first(pts)
         latent = first[..., 1:]
         alpha = first[..., 0, None]
-        light = light_location[None, :, None, None, None, :].expand(latent.shape[:-1] + (3,))
+        if self.envmap:
+            points = torch.stack(torch.meshgrid(torch.linspace(0, 180, self.bins),
+                                                torch.linspace(0, 45, self.bins), indexing="ij"),
+                                 dim=-1).reshape(-1, 2)
+            enc = point_light_envmap(light, elev_azim_to_dir(points))
+            B = latent.shape[1]
+            light_enc = enc.reshape(1, B, 1, 1, 1, -1).expand(latent.shape[:-1] + (-1,))
+        else:
+            light_enc = light_location[None, :, None, None, None, :].expand(
+                latent.shape[:-1] + (3,))
         rgb = self.second(torch.cat([latent, r_d[None, ...].expand(latent.shape[:-1] + (3,)),
-                                     light], dim=-1)).sigmoid()
+                                     light_enc], dim=-1)).sigmoid()
         sigma = F.relu(alpha).squeeze(-1)
         alpha = 1 - torch.exp(-sigma * ts[:, None, None, None, None].expand_as(sigma))
         cp = torch.cumprod((1 - alpha).clamp(min=1e-10), dim=0)
