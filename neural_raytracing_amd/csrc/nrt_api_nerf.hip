@@ -107,34 +107,44 @@ static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 //
 // Program chunk order (build_nerf_program, consumed in exactly this order per batch):
 //   first MLP (hidden 128 = 4 row blocks, F = 16, 3 -> 65): init enc [3 k-steps];
-//     per hidden layer: hidden [4][4] k-steps, + enc [3] on skip layers;
-//     out (3 row blocks): k-steps [0..4], [5..7]
+//     per hidden layer: hidden [8] k-steps, + enc [3] on skip layers; out (3 row blocks) [8]
 //   projection: A_hi (7 k-steps) then A_lo (7) of basis^T (16 x 70) in one chunk
-//   second MLP (hidden 64 = 2 row blocks, 70 -> 3): init enc [8][1]; per hidden layer hidden
-//     [4] or, on skip layers, hidden + enc [8][5]; out [4] (1 row block)
+//   second MLP (hidden 64 = 2 row blocks, 70 -> 3): init enc [9]; per hidden layer hidden
+//     [4] or, on skip layers, hidden + enc [13]; out [4] (1 row block)
+// (chunks of at most kNerfMaxF fragments; one barrier per chunk)
 // Second-MLP encoding k-steps (9): e0, e1 = sin/cos of projections q = 8e + 4h + jj (the usual
 // pair order); e2..e7 = the first MLP's output tiles in accumulator order (row 1 + k = latent k;
 // row 0 and rows > 64 have zero weight); e8 = (r_d, light) in half 0.
 // ------------------------------------------------------------------------------------------
 constexpr int kNerfWaves = 8;
+constexpr int kNerfMaxF = 32;  // fragments per ring slot (3 slots: 96 KiB of LDS)
+constexpr int kNerfL1 = 5, kNerfL2 = 8, kNerfSkip = 3;  // nerf.py:162-172 (SkipConnMLP skip 3)
 
 // acc[ib] += W[ib] * [b1[0..KS1), b2[0..KS2)] over chunks of KC k-steps
-template <int NB, int KS1, int KS2, int KC, int WV, int N1, int N2>
-__device__ __forceinline__ void nerf_layer(ring::KEngine<WV>& E, f16v (&acc)[NB],
+template <int NB, int KS1, int KS2, int KC, class Eng, int N1, int N2>
+__device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
                                            const h8 (&b1)[N1], const h8 (&b2)[N2]) {
   static_assert(KS1 <= N1 && KS2 <= N2, "fragment arrays too short");
+  static_assert(KC * NB <= Eng::MAXF, "chunk larger than a ring slot");
   constexpr int KS = KS1 + KS2;
   constexpr int NCH = (KS + KC - 1) / KC;
+  constexpr int W = 4;  // A fragments in flight (LDS latency cover)
 #pragma unroll
   for (int cc = 0; cc < NCH; ++cc) {
     const h8* A = E.begin();
+    const int nf = ((KS - cc * KC) < KC ? (KS - cc * KC) : KC) * NB;  // fragments of this chunk
+    h8 a[W];
 #pragma unroll
-    for (int j = 0; j < KC; ++j) {
-      const int s = cc * KC + j;
-      if (s < KS) {
+    for (int w = 0; w < W; ++w)
+      if (w < nf) a[w] = A[w * 64];
+#pragma unroll
+    for (int m = 0; m < KC * NB; ++m) {
+      if (m < nf) {
+        const int s = cc * KC + m / NB, ib = m % NB;
         const h8 b = s < KS1 ? b1[s < KS1 ? s : 0] : b2[s >= KS1 ? s - KS1 : 0];
-#pragma unroll
-        for (int ib = 0; ib < NB; ++ib) acc[ib] = mfma16(A[(j * NB + ib) * 64], b, acc[ib]);
+        acc[ib] = mfma16(a[m % W], b, acc[ib]);
+        if (m + W < nf) a[m % W] = A[(m + W) * 64];
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     E.end();
@@ -142,8 +152,8 @@ __device__ __forceinline__ void nerf_layer(ring::KEngine<WV>& E, f16v (&acc)[NB]
 }
 
 // the first MLP (nerf.py:162-163: 5 x 128, F = 16, 3 -> 65) with its 3 output row blocks
-template <int WV>
-__device__ __forceinline__ void nerf_first(ring::KEngine<WV>& E, const ProgMlp& pm, float x0,
+template <int L, int SKIP, class Eng>
+__device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, float x0,
                                            float x1, float x2, f16v (&o)[3]) {
   constexpr int NB = 4, NE = 3;
   const int h = E.lane >> 5;
@@ -155,20 +165,21 @@ __device__ __forceinline__ void nerf_first(ring::KEngine<WV>& E, const ProgMlp& 
   for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<-1>(basis, s, NE - 1, h, x0, x1, x2);
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
-  nerf_layer<NB, NE, 0, 4>(E, acc, enc, enc);
+  nerf_layer<NB, NE, 0, 8>(E, acc, enc, enc);
 #pragma unroll
   for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<ACT_LEAKY>(basis, s, NE - 1, h, x0, x1, x2);
-  for (int i = 0; i < pm.L; ++i) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
     ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 1 + i, ib, h);
-    nerf_layer<NB, 2 * NB, 0, 4>(E, acc, hv, hv);
-    if (i != pm.L - 1 && (i % pm.skip) == 0) nerf_layer<NB, NE, 0, 4>(E, acc, enc, enc);
+    nerf_layer<NB, 2 * NB, 0, 8>(E, acc, hv, hv);
+    if (i != L - 1 && (i % SKIP) == 0) nerf_layer<NB, NE, 0, 8>(E, acc, enc, enc);
   }
   ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
-  for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(pm, pm.L + 1, ob, h);
-  nerf_layer<3, 2 * NB, 0, 5>(E, o, hv, hv);
+  for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(pm, L + 1, ob, h);
+  nerf_layer<3, 2 * NB, 0, 8>(E, o, hv, hv);
 }
 
 __device__ __forceinline__ h8 h8_of(const float (&v)[8]) {
@@ -187,7 +198,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
   const int64_t n = (int64_t)S * P;
   const int64_t per_block = 32 * WV;
   if ((int64_t)blockIdx.x * per_block >= n) return;
-  ring::KEngine<WV> E;
+  ring::KEngine<WV, kNerfMaxF> E;
   E.init(prog, smem_c);
   const int lane = lane_id(), h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -207,7 +218,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     const float x1 = __fadd_rn(r[1], __fmul_rn(t, dy));
     const float x2 = __fadd_rn(r[2], __fmul_rn(t, dz));
     f16v o[3];
-    nerf_first<WV>(E, m1, x0, x1, x2, o);
+    nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
     // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
     h8 e[9], ea[9], lo[7];
 #pragma unroll
@@ -264,17 +275,18 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     h8 hv[2 * NB];
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
-    nerf_layer<NB, 9, 0, 8>(E, acc, e, e);
-    for (int i = 0; i < m2.L; ++i) {
+    nerf_layer<NB, 9, 0, 16>(E, acc, e, e);
+#pragma unroll
+    for (int i = 0; i < kNerfL2; ++i) {
       ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 1 + i, ib, h);
-      if (i != m2.L - 1 && (i % m2.skip) == 0) nerf_layer<NB, 2 * NB, 9, 8>(E, acc, hv, ea);
-      else nerf_layer<NB, 2 * NB, 0, 8>(E, acc, hv, hv);
+      if (i != kNerfL2 - 1 && (i % kNerfSkip) == 0) nerf_layer<NB, 2 * NB, 9, 16>(E, acc, hv, ea);
+      else nerf_layer<NB, 2 * NB, 0, 16>(E, acc, hv, hv);
     }
     ring::kact<NB, ACT_LEAKY>(acc, hv);
-    f16v out[1] = {E.bias_at(m2, m2.L + 1, 0, h)};
-    nerf_layer<1, 2 * NB, 0, 8>(E, out, hv, hv);
+    f16v out[1] = {E.bias_at(m2, kNerfL2 + 1, 0, h)};
+    nerf_layer<1, 2 * NB, 0, 16>(E, out, hv, hv);
     if (valid && h == 0) {
       alpha_raw[g] = o[0][0];
       rgb_raw[g * 3] = out[0][0]; rgb_raw[g * 3 + 1] = out[0][1]; rgb_raw[g * 3 + 2] = out[0][2];
@@ -288,7 +300,8 @@ static bool nerf_fusable(const nrt_mlp* f, const nrt_mlp* s) {
   const MlpDev& b = s->host_dev;
   return a.in_size == 3 && a.nb == 4 && a.freqs == 16 && a.out == 65 && a.latent == 0 &&
          a.act == ACT_LEAKY && b.in_size == 70 && b.nb == 2 && b.freqs == 16 && b.out == 3 &&
-         b.latent == 0 && b.act == ACT_LEAKY && (int)f->host_w.size() == a.n_hidden + 2 &&
+         b.latent == 0 && b.act == ACT_LEAKY && a.n_hidden == kNerfL1 && b.n_hidden == kNerfL2 &&
+         a.skip == kNerfSkip && b.skip == kNerfSkip && (int)f->host_w.size() == a.n_hidden + 2 &&
          (int)s->host_w.size() == b.n_hidden + 2 && a.ke == 48;
 }
 
@@ -300,12 +313,26 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
   typedef std::array<_Float16, 512> Frag;  // [lane][8]
   std::vector<Frag> frags;
   std::vector<int> coff;
-  // first MLP: its own k-outer stream, out layer split into k-steps [0..4] and [5..7]
+  // first MLP: its own k-outer stream ([layer][k-step][row block]); one chunk per layer part
   frags.resize(a.nk_frags);
   NRT_HIP(hipMemcpy(frags.data(), a.streamk16, (size_t)a.nk_frags * 1024, hipMemcpyDeviceToHost));
-  for (size_t c = 0; c + 1 < f->host_chunkk.size(); ++c) coff.push_back(f->host_chunkk[c]);
-  coff.push_back(f->host_chunkk.back());
-  coff.push_back(f->host_chunkk.back() + 5 * 3);
+  {
+    int base = 0;
+    coff.push_back(base);  // init: 3 encoding k-steps x 4 row blocks
+    base += 3 * 4;
+    for (int i = 0; i < a.n_hidden; ++i) {
+      const bool skip = i != a.n_hidden - 1 && (i % a.skip) == 0;
+      coff.push_back(base);  // 8 hidden k-steps
+      if (skip) coff.push_back(base + 8 * 4);  // + 3 encoding k-steps
+      base += (8 + (skip ? 3 : 0)) * 4;
+    }
+    coff.push_back(base);  // out: 8 k-steps x 3 row blocks
+    base += 8 * 3;
+    if (base != a.nk_frags) {
+      set_error("build_nerf_program: unexpected first-MLP stream layout");
+      return NRT_EUNSUPPORTED;
+    }
+  }
   // element (h, j) of second-MLP encoding k-step e -> reference input column (-1: none)
   const int IN = 70, F = 16;
   auto enc_col = [&](int e, int hf, int j) -> int {
@@ -336,7 +363,7 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
       }
       frags.push_back(fr);
     }
-  // second MLP: k-steps per layer (hidden, then the 9 encoding steps), chunks of 8 k-steps
+  // second MLP: k-steps per layer (hidden, then the 9 encoding steps), chunks of 16 k-steps
   const int H = 64, NB = 2, L = b.n_hidden;
   for (int l = 0; l < L + 2; ++l) {
     const bool init = l == 0, outl = l == L + 1;
@@ -368,7 +395,7 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
         }
         frags.push_back(fr);
       }
-    for (int st = 0; st < ks; st += 8) coff.push_back(base + st * nrb);
+    for (int st = 0; st < ks; st += 16) coff.push_back(base + st * nrb);
   }
   const size_t nfr = frags.size();
   frags.resize(nfr + 64);
@@ -463,7 +490,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     float* alpha = (float*)ws;
     float* rgb_raw = (float*)(ws + a256(n * 4));
     auto kern = k_nerfle16<kNerfWaves>;
-    const size_t lds = ring::KEngine<kNerfWaves>::lds_bytes(pd);
+    const size_t lds = ring::KEngine<kNerfWaves, kNerfMaxF>::lds_bytes(pd);
     if (int rc = set_lds(kern, lds)) return rc;
     static int cus = 0;
     if (!cus) {

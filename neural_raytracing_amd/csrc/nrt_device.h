@@ -950,9 +950,9 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
 // per layer), which keeps wide encodings (F = 64 / 128) out of the register file.  The layer
 // count and skip period are runtime values.
 // ------------------------------------------------------------------------------------------
-template <int WV>
+template <int WV, int MAXF_ = 16>
 struct KEngine {
-  static constexpr int MAXF = 16;  // fragments per chunk: KC * NB <= 16 (out layer: KC)
+  static constexpr int MAXF = MAXF_;  // fragments per chunk: KC * NB <= MAXF (out layer: KC)
   static constexpr int MAXL = (MAXF + WV - 1) / WV;
   static constexpr int SLOTF = MAXL * WV;
   static constexpr int RING_BYTES = 3 * SLOTF * 1024;
@@ -1054,6 +1054,8 @@ __device__ __forceinline__ h8 enc_frag_k(const float4* basis, int s, int last, i
   return f;
 }
 
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
 template <int NB, int ACT>
 __device__ __forceinline__ void kact(const f16v (&acc)[NB], h8 (&hv)[2 * NB]) {
 #pragma unroll
@@ -1061,8 +1063,21 @@ __device__ __forceinline__ void kact(const f16v (&acc)[NB], h8 (&hv)[2 * NB]) {
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       h8 f;
+      if (ACT == ACT_LEAKY) {
+        // leaky_relu(x) = max(x, 0.01 x) on packed halves: cvt_pk + pk_mul + pk_max per pair
+        // (1.5 VALU per element instead of cmp + mul + cndmask + cvt)
+        const h2 k = {(_Float16)0.01f, (_Float16)0.01f};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = (_Float16)act_fwd<true>(acc[ib][8 * s2 + j], ACT);
+        for (int j = 0; j < 8; j += 2) {
+          const h2 v = {(_Float16)acc[ib][8 * s2 + j], (_Float16)acc[ib][8 * s2 + j + 1]};
+          const h2 r = __builtin_elementwise_max(v, v * k);
+          f[j] = r[0];
+          f[j + 1] = r[1];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] = (_Float16)act_fwd<true>(acc[ib][8 * s2 + j], ACT);
+      }
       hv[2 * ib + s2] = f;
     }
 }
