@@ -39,8 +39,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=800)
-    ap.add_argument("--samples", type=int, default=64, help="march steps per ray (max_steps)")
+    ap.add_argument("--size", type=int, default=None,
+                    help="image side (default 800; 1600 for --scene nerfle, BASELINE cfg5)")
+    ap.add_argument("--samples", type=int, default=None,
+                    help="march steps per ray (max_steps) or NeRF depths per ray "
+                         "(default 64; 256 for --scene nerfle, BASELINE cfg5)")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     ap.add_argument("--tile-rows", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,7 +53,13 @@ def parse():
                     choices=["nerf_synthetic", "colocate", "dtu", "nerfle"],
                     help="nerf_synthetic = the BASELINE metric (default); the others are "
                          "BASELINE.json configs[2..4] as one-GPU workloads")
-    return ap.parse_args()
+    args = ap.parse_args()
+    big = args.scene == "nerfle"
+    if args.size is None:
+        args.size = 1600 if big else 800
+    if args.samples is None:
+        args.samples = 256 if big else 64
+    return args
 
 
 def look_at(eye):

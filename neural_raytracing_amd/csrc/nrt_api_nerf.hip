@@ -98,12 +98,73 @@ __global__ void k_nerf_composite(const float* __restrict__ first_out, int astrid
   }
 }
 
+// The same compositing for the fused path's ray-major samples (alpha_raw[p * S + s],
+// rgb_raw[(p * S + s) * 3 + k]): one wave per ray, 64 depths per step, the cumulative product as
+// a wave prefix product carried across steps (the sequential product reassociated: FP32
+// rounding differences only).
+template <int = 0>
+__global__ void k_nerf_composite_rm(const float* __restrict__ alpha_raw,
+                                    const float* __restrict__ rgb_raw,
+                                    const float* __restrict__ ts, int64_t P, int S,
+                                    float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; p < P; p += nw) {
+    const float* al = alpha_raw + p * S;
+    const float* rg = rgb_raw + p * S * 3;
+    float carry = 1.f;  // cp_{c0 - 1}
+    float acc[3] = {0.f, 0.f, 0.f};
+    float a_first = 0.f, c_first[3] = {0.f, 0.f, 0.f};
+    for (int c0 = 0; c0 < S; c0 += 64) {
+      const int s = c0 + lane;
+      const bool v = s < S;
+      float a = 0.f, q = 1.f, col[3] = {0.f, 0.f, 0.f};
+      if (v) {
+        const float sig = fmaxf(al[s], 0.f);
+        a = 1.f - expf(-(sig * ts[s]));
+        q = fmaxf(1.f - a, 1e-10f);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) col[k] = 1.f / (1.f + expf(-rg[s * 3 + k]));
+      }
+      float inc = q;  // inclusive prefix product of q over the step's lanes
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const float o = __shfl_up(inc, d);
+        if (lane >= d) inc *= o;
+      }
+      const float up = __shfl_up(inc, 1);
+      const float prev = carry * (lane == 0 ? 1.f : up);  // cp_{s-1}
+      if (s == 0) {
+        a_first = a;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) c_first[k] = col[k];
+      }
+      const float w = !v ? 0.f : (s == S - 1 ? a : (s == 0 ? 0.f : a * prev));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc[k] += w * col[k];
+      carry = carry * __shfl(inc, 63);
+    }
+    // w_0 = a_0 cp_{S-1} (the roll), unless S == 1 where w_0 = a_0
+    if (lane == 0 && S > 1)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc[k] += (a_first * carry) * c_first[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) acc[k] += __shfl_xor(acc[k], d);
+    if (lane == 0) {
+      out[p * 3] = acc[0]; out[p * 3 + 1] = acc[1]; out[p * 3 + 2] = acc[2];
+    }
+  }
+}
+
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------------------------------------
 // Fused FP16 NeRFLE sample kernel on the k-outer program engine (ring::KEngine): per wave 32
-// samples (columns); both MLPs, the second MLP's Fourier projection and its input assembly stay
-// in registers; only alpha_raw and rgb_raw (16 B per sample) reach HBM.
+// samples (columns, ray-major: sample g = p * S + s); both MLPs, the second MLP's Fourier
+// projection and its input assembly stay in registers; only alpha_raw and rgb_raw (16 B per
+// sample) reach HBM.
 //
 // Program chunk order (build_nerf_program, consumed in exactly this order per batch):
 //   first MLP (hidden 128 = 4 row blocks, F = 16, 3 -> 65): init enc [3 k-steps];
@@ -209,7 +270,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     const int64_t g = b0 + 32 * wv + (lane & 31);
     const bool valid = g < n;
     const int64_t gg = valid ? g : n - 1;
-    const int64_t s = gg / P, p = gg - s * P;
+    const int64_t p = gg / S, s = gg - p * S;  // ray-major: a wave's columns share a ray
     const float t = ts[s];
     const float* r = rays + p * 6;
     const float dx = r[3], dy = r[4], dz = r[5];
@@ -503,9 +564,9 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     ProfScope prof("k_nerfle", st);
     kern<<<dim3(blocks), dim3(64 * kNerfWaves), lds, st>>>(pd, rays, P, ts, S, light, alpha, rgb_raw);
     if (int rc = check_launch("k_nerfle16")) return rc;
-    k_nerf_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(
-        alpha, 1, rgb_raw, ts, P, S, rgb);
-    return check_launch("k_nerf_composite");
+    k_nerf_composite_rm<><<<dim3(std::min<int64_t>(ceil_div64(P, 4), 16384)), dim3(256), 0, st>>>(
+        alpha, rgb_raw, ts, P, S, rgb);
+    return check_launch("k_nerf_composite_rm");
   }
   float* pts = (float*)ws;
   float* f1 = (float*)(ws + a256(n * 12));

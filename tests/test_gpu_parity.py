@@ -795,6 +795,39 @@ def test_nerfle_matches_oracle(prec, monkeypatch):
     assert (got - want).abs().max().item() <= tol, (got - want).abs().max()
 
 
+@pytest.mark.parametrize("prec,steps", [("fp32", 37), ("fp16", 1), ("fp16", 37), ("fp16", 200)])
+def test_nerfle_depth_counts(prec, steps, monkeypatch):
+    """NeRFLE with depth counts other than 64 (BASELINE cfg5 asks 256): the fused kernel's
+    ray-major sample order and the wave-scan compositing across partial 64-depth steps, and the
+    S == 1 roll edge case, vs the oracle."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.shapes import NeRFLE
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
+    seeded(31)
+    ref = R.NeRFLERef(steps=steps)
+    mine = NeRFLE(device="cpu", steps=steps)
+    copy_mlp(mine.first, ref.first)
+    copy_mlp(mine.second, ref.second)
+    mine = mine.cuda()
+    g = torch.Generator().manual_seed(8)
+    o = torch.tensor([0.0, 0.1, 1.1]) + 0.1 * torch.randn(1, 7, 5, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, 7, 5, 1, 2, generator=g) - 0.5,
+                               -torch.ones(1, 7, 5, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    loc = torch.tensor([[0.2, 1.0, 0.4]])
+    lights = PointLights(location=loc.cuda(), device="cuda")
+    set_precision(prec)
+    random.seed(3)
+    with torch.no_grad():
+        got = mine(rays.cuda(), lights).cpu()
+    random.seed(3)
+    with torch.no_grad():
+        want = ref(rays, loc, jitter=random.random())
+    tol = 1e-4 if prec == "fp32" else 2e-2
+    assert (got - want).abs().max().item() <= tol, (got - want).abs().max()
+
+
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
 def test_nerfle_envmap_matches_oracle(prec):
     """NeRFLE(envmap=True) (NeRF+LE, nerf.py:183-191): the colour MLP's light input is the point

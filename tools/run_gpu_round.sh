@@ -1,5 +1,5 @@
 # GPU round script: tests, smoke, bench, rocprof, PMC traffic (each step time-limited; stop at
-# the first failure).  bash tools/run_gpu_round.sh [all|tests|bench|prof|pmc]
+# the first failure).  bash tools/run_gpu_round.sh [all|tests|bench|prof|pmc|scenes]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -22,4 +22,13 @@ fi
 if [ "$STEP" = all ] || [ "$STEP" = pmc ]; then
   rm -rf gpurun_out/pmc
   SIZE=800 bash tools/pmc.sh k_march16 "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" || exit 1
+fi
+if [ "$STEP" = all ] || [ "$STEP" = scenes ]; then
+  rm -f gpurun_out/scenes.jsonl
+  for SC in colocate dtu nerfle; do
+    timeout -k 10 300 python -u bench.py --scene $SC --steps 3 --warmup 1 >> gpurun_out/scenes.jsonl 2> gpurun_out/scene_$SC.err
+    rc=$?; echo "SCENE $SC EXIT $rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nerfle -o run --output-format csv -- python3 bench.py --scene nerfle --steps 2 --warmup 1 > gpurun_out/prof_nerfle.log 2>&1
+  rc=$?; echo "PROF NERFLE EXIT $rc"; [ $rc -eq 0 ] || exit $rc
 fi
