@@ -80,6 +80,18 @@ int nrt_mlp_destroy(nrt_mlp* mlp);
 int nrt_mlp_forward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,
                     float* y, int precision, void* stream);
 
+/* Backward of nrt_mlp_forward in FP32 (torch autograd through
+ * SkipConnMLP.forward, neural_blocks.py:75-86): given dy [M, out] = dL/dy, writes
+ *   dx [M, in] and dlatent [M, latent] (each may be NULL),
+ *   dweights[l] [R_l, C_l] and dbiases[l] [R_l] for l = 0 (init), 1..num_layers (hidden),
+ *   num_layers + 1 (out), in the torch nn.Linear layouts (host arrays of device pointers; the
+ *   arrays or single entries may be NULL).  Gradients are overwritten, not accumulated.
+ * workspace: nrt_mlp_backward_workspace_bytes(mlp, M) bytes of device memory. */
+size_t nrt_mlp_backward_workspace_bytes(const nrt_mlp* mlp, int64_t M);
+int nrt_mlp_backward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,
+                     const float* dy, float* dx, float* dlatent, float* const* dweights,
+                     float* const* dbiases, void* workspace, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Signed distance fields (shapes/sdfs.py)
  * ------------------------------------------------------------------------------------- */

@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libnrt_hip.so")
 SOURCES = ["nrt_common.hip", "nrt_pack.hip", "nrt_api_mlp.hip", "nrt_api_sdf.hip",
            "nrt_api_shade.hip", "nrt_api_cam.hip", "nrt_ring_march.hip", "nrt_ring_normal.hip", "nrt_prog.hip", "nrt_api_nerf.hip",
-           "nrt_api_path.hip"]
+           "nrt_api_path.hip", "nrt_api_train.hip"]
 HEADERS = ["nrt_kernels.h", "nrt_device.h", "nrt_internal.h", "nrt_launch.h"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nrt.h")
 
@@ -53,7 +53,9 @@ def build(force=False, verbose=True, jobs=None):
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 8)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
+    # rocBLAS: the batch-reduction GEMMs of the MLP weight gradients (nrt_api_train.hip)
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs,
+           "-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(OUT + ".tmp", OUT)
     return OUT

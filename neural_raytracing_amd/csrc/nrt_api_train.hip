@@ -1,0 +1,309 @@
+// nrt_api_train.hip -- SkipConnMLP backward (first slice): the gradients
+// torch autograd produces for `y = mlp(x, latent)` (neural_blocks.py:75-86) given dL/dy.
+//
+//   k_mlp_backward32  per wave 32 rows, FP32 MFMA (v_mfma_f32_32x32x2_f32) on the LDS slab:
+//                     forward with saved pre-activations Z_l and activations A_l = act(Z_l),
+//                     the encoding (raw and activated) in the reference's column order, then the
+//                     row-local backward chain dZ_l = (dZ_{l+1} W_{l+1}) * act'(Z_l) with the W^T
+//                     fragments, the encoding gradient, and dL/dx, dL/dlatent.
+//   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M): rocBLAS sgemm on the saved
+//                     activations; bias gradients = column sums of dZ_l (rocBLAS sgemv with ones).
+#include <rocblas/rocblas.h>
+
+#include <mutex>
+
+#include "nrt_launch.h"
+
+namespace nrt {
+
+// reference encoding column of slot s ([x, sin(xB), cos(xB), latent], utils.py:37-40); -1 = pad
+__device__ __forceinline__ int enc_col(const MlpDev& m, int s) {
+  const int F = m.freqs, in = m.in_size;
+  if (s < 2 * F) return (s & 1) ? in + F + (s >> 1) : in + (s >> 1);
+  if (s < 2 * F + in) return s - 2 * F;
+  if (s < 2 * F + in + m.latent) return in + 2 * F + (s - 2 * F - in);
+  return -1;
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) k_mlp_backward32(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
+    float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
+    float* __restrict__ Eact, float* __restrict__ dZg, int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const MlpDev& m = *mp;
+  float* X = smem + (size_t)(threadIdx.x >> 6) * per_wave;
+  const int lane = lane_id(), r = lane & 31, h = lane >> 5;
+  const int64_t row0 = wave_global() * 32;
+  if (row0 >= M) return;  // whole wave exits together
+  const int64_t row = row0 + r;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  const int H = m.hidden, L = m.n_hidden, ke = m.ke, dp = m.dp, in = m.in_size;
+  EncIn e;
+  if (in <= 4) {
+    for (int i = 0; i < 4; ++i) e.x[i] = (i < in) ? x[rr * in + i] : 0.f;
+    e.xg = nullptr;
+  } else {
+    e.x[0] = e.x[1] = e.x[2] = e.x[3] = 0.f;
+    e.xg = x + rr * in;
+  }
+  e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
+  float* rowp = X + r * RS;
+  // ---- forward (mlp32_forward's order of operations), saving Z_l, A_l and the encoding
+  write_enc_slab<false>(m, e, X, RS);
+  wave_lds_fence();
+  if (valid)
+    for (int s = h; s < ke; s += 2) {
+      const int c = enc_col(m, s);
+      if (c < 0) continue;
+      const float v = rowp[H + s];
+      Eraw[row * dp + c] = v;
+      Eact[row * dp + c] = act_fwd<false>(v, m.act);
+    }
+  f16v acc[NB];
+  for (int l = 0; l <= L; ++l) {
+    bias32<NB>(acc, m.bias[l], 0, NB, h);
+    if (l == 0) {
+      gemm32<NB>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, H, -1);
+    } else {
+      const int i = l - 1;
+      gemm32<NB>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
+      if (i != L - 1 && (i % m.skip) == 0)
+        gemm32<NB>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, H, m.act);
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const float z = acc[ib][reg];
+        const float a = act_fwd<false>(z, m.act);
+        if (valid) {
+          Zg[((int64_t)l * M + row) * H + k] = z;
+          Ag[((int64_t)l * M + row) * H + k] = a;
+        }
+        rowp[k] = a;
+      }
+    wave_lds_fence();
+  }
+  // ---- backward seed: dZ_L = (dY W_out) * act'(Z_L)
+  float* egrad = rowp + H + ke;
+  for (int s = h; s < ke; s += 2) egrad[s] = 0.f;
+  const float* Ao = m.w32[L + 1];
+  const int out = m.out;
+  for (int k = h; k < H; k += 2) {
+    float g = 0.f;
+    for (int o = 0; o < out; ++o)
+      g = fmaf(dY[rr * out + o], Ao[((k >> 1) * m.ob + (o >> 5)) * 64 + (k & 1) * 32 + (o & 31)], g);
+    rowp[k] = g * act_bwd(Zg[((int64_t)L * M + rr) * H + k], m.act);
+  }
+  wave_lds_fence();
+  for (int l = L; l >= 0; --l) {
+    if (valid)
+      for (int k = h; k < H; k += 2) dZg[((int64_t)l * M + row) * H + k] = rowp[k];
+    const float* At = m.wt32[l];
+    const int nrb = m.nbt[l];
+    const bool has_hidden_in = (l != 0);
+    const bool has_enc_in = (l == 0) || ((l - 1) != L - 1 && ((l - 1) % m.skip) == 0);
+    const int hid_rb = has_hidden_in ? NB : 0;
+    if (has_enc_in) {
+      const int enc_pos0 = has_hidden_in ? H : 0;
+      for (int rb0 = hid_rb; rb0 < nrb; rb0 += NB) {
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+        gemm32<NB>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+          if (rb0 + ib >= nrb) continue;
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int slot = pos - enc_pos0;
+            if (slot >= 0 && slot < ke) {
+              float v = acc[ib][reg];
+              if (l != 0) v *= act_bwd(rowp[H + slot], m.act);  // skip inputs are act(enc)
+              egrad[slot] += v;
+            }
+          }
+        }
+      }
+      wave_lds_fence();
+    }
+    if (has_hidden_in) {
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+      gemm32<NB>(acc, At, nrb, 0, H >> 1, X, RS, 0, -1);
+      wave_lds_fence();
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+          const int pos = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+          rowp[pos] = acc[ib][reg] * act_bwd(Zg[((int64_t)(l - 1) * M + rr) * H + pos], m.act);
+        }
+      wave_lds_fence();
+    }
+  }
+  // ---- encoding -> inputs: d sin(p_q) = cos(p_q) B_iq, d cos(p_q) = -sin(p_q) B_iq, x_i direct
+  const int F = m.freqs;
+  for (int i = 0; i < in; ++i) {
+    float g = 0.f;
+    for (int q = h; q < F; q += 2) {
+      float s, c;
+      sincosf(proj<false>(m, e, q), &s, &c);
+      g = fmaf(egrad[2 * q] * c - egrad[2 * q + 1] * s, m.basis[i * F + q], g);
+    }
+    if (h == 0) g += egrad[2 * F + i];
+    g += __shfl_xor(g, 32);
+    if (dX && valid && h == 0) dX[row * in + i] = g;
+  }
+  if (dLat && valid)
+    for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[2 * F + in + j];
+}
+
+template <int = 0>
+__global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+namespace {
+size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct TrainWs {
+  float *Z, *A, *dZ, *Eraw, *Eact, *ones;
+};
+
+TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
+  const MlpDev& d = m->host_dev;
+  const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
+  const size_t enc = (size_t)M * d.dp * 4;
+  char* p = (char*)base;
+  TrainWs w;
+  w.Z = (float*)p; p += a256(lay);
+  w.A = (float*)p; p += a256(lay);
+  w.dZ = (float*)p; p += a256(lay);
+  w.Eraw = (float*)p; p += a256(enc);
+  w.Eact = (float*)p; p += a256(enc);
+  w.ones = (float*)p;
+  return w;
+}
+
+rocblas_handle blas() {
+  static rocblas_handle h = nullptr;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> g(mu);
+  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
+  return h;
+}
+
+int blas_fail(rocblas_status s, const char* what) {
+  set_error(std::string(what) + ": rocBLAS status " + std::to_string((int)s));
+  return NRT_EHIP;
+}
+
+// row-major dW[R][ldw] (columns c0 .. c0+C) = dZ[M][R]^T @ In[M][C]
+int grad_gemm(rocblas_handle hb, const float* dZ, int R, const float* In, int C, int64_t M,
+              float* dW, int ldw, int c0) {
+  const float one = 1.f, zero = 0.f;
+  // column-major view: dW^T (C x R, ld ldw) = In^T (C x M, ld C) * dZ (M x R = (R x M, ld R)^T)
+  rocblas_status s = rocblas_sgemm(hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
+                                   (rocblas_int)M, &one, In, C, dZ, R, &zero, dW + c0, ldw);
+  return s == rocblas_status_success ? NRT_OK : blas_fail(s, "rocblas_sgemm");
+}
+
+int grad_bias(rocblas_handle hb, const float* dZ, int R, int64_t M, const float* ones, float* db) {
+  const float one = 1.f, zero = 0.f;
+  // db (R) = dZ^T (R x M, ld R) @ ones (M)
+  rocblas_status s = rocblas_sgemv(hb, rocblas_operation_none, R, (rocblas_int)M, &one, dZ, R,
+                                   ones, 1, &zero, db, 1);
+  return s == rocblas_status_success ? NRT_OK : blas_fail(s, "rocblas_sgemv");
+}
+}  // namespace
+
+}  // namespace nrt
+
+using namespace nrt;
+
+extern "C" {
+
+size_t nrt_mlp_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
+  if (!m) return 0;
+  M = std::max<int64_t>(M, 1);
+  const MlpDev& d = m->host_dev;
+  const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
+  const size_t enc = (size_t)M * d.dp * 4;
+  return 3 * a256(lay) + 2 * a256(enc) + a256((size_t)M * 4);
+}
+
+int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int64_t M,
+                     const float* dy, float* dx, float* dlatent, float* const* dweights,
+                     float* const* dbiases, void* workspace, void* stream) {
+  if (!m || M < 0 || (M > 0 && (!x || !dy || !workspace))) {
+    set_error("nrt_mlp_backward: bad argument");
+    return NRT_EINVAL;
+  }
+  const MlpDev& d = m->host_dev;
+  if (d.latent > 0 && !latent) { set_error("nrt_mlp_backward: latent required"); return NRT_EINVAL; }
+  if (M > INT32_MAX) { set_error("nrt_mlp_backward: at most 2^31-1 rows per call"); return NRT_EINVAL; }
+  hipStream_t st = (hipStream_t)stream;
+  const int L = d.n_hidden, H = d.hidden;
+  if (M == 0) {  // zero gradients
+    for (int l = 0; l < L + 2; ++l) {
+      const int R = l == L + 1 ? d.out : H;
+      const int C = m->host_w[l].size() / (size_t)R;
+      if (dweights && dweights[l]) NRT_HIP(hipMemsetAsync(dweights[l], 0, (size_t)R * C * 4, st));
+      if (dbiases && dbiases[l]) NRT_HIP(hipMemsetAsync(dbiases[l], 0, (size_t)R * 4, st));
+    }
+    return NRT_OK;
+  }
+  TrainWs w = carve(m, M, workspace);
+  LdsPlan lp = plan_lds(H, d.ke, 1, false, true);
+  const int waves = ceil_div64(M, 32);
+  dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
+  int rc = NRT_OK;
+  {
+    ProfScope prof("k_mlp_backward32", st);
+    NRT_NB_SWITCH(d.nb, {
+      if (!(rc = set_lds(k_mlp_backward32<NB>, lp.bytes)))
+        k_mlp_backward32<NB><<<grid, block, lp.bytes, st>>>(m->dev, x, latent, M, dy, dx, dlatent,
+                                                            w.Z, w.A, w.Eraw, w.Eact, w.dZ, lp.RS,
+                                                            lp.per_wave);
+    });
+    if (rc) return rc;
+    if ((rc = check_launch("k_mlp_backward32"))) return rc;
+  }
+  if (!dweights && !dbiases) return NRT_OK;
+  k_fill<><<<dim3(std::min<int64_t>(ceil_div64(M, 256), 1024)), dim3(256), 0, st>>>(w.ones, M, 1.f);
+  if ((rc = check_launch("k_fill"))) return rc;
+  rocblas_handle hb = blas();
+  if (!hb) { set_error("nrt_mlp_backward: rocblas_create_handle failed"); return NRT_EHIP; }
+  rocblas_status s = rocblas_set_stream(hb, st);
+  if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
+  const size_t lay = (size_t)M * H;
+  for (int l = 0; l <= L + 1; ++l) {
+    const bool outl = l == L + 1;
+    const int R = outl ? d.out : H;
+    const float* dZ = outl ? dy : w.dZ + (size_t)l * lay;
+    if (dweights && dweights[l]) {
+      if (l == 0) {
+        rc = grad_gemm(hb, dZ, R, w.Eraw, d.dp, M, dweights[0], d.dp, 0);
+      } else {
+        const int i = l - 1;
+        const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
+        const int C = H + (skip ? d.dp : 0);
+        rc = grad_gemm(hb, dZ, R, w.A + (size_t)(l - 1) * lay, H, M, dweights[l], C, 0);
+        if (!rc && skip) rc = grad_gemm(hb, dZ, R, w.Eact, d.dp, M, dweights[l], C, H);
+      }
+      if (rc) return rc;
+    }
+    if (dbiases && dbiases[l] && (rc = grad_bias(hb, dZ, R, M, w.ones, dbiases[l]))) return rc;
+  }
+  return NRT_OK;
+}
+
+}  // extern "C"

@@ -89,16 +89,69 @@ class SkipConnMLP(nn.Module):
         if not p.is_cuda:
             raise _lib.NrtError("SkipConnMLP evaluates on the HIP path only: move it and its "
                                 "inputs to the GPU")
-        if torch.is_grad_enabled() and (p.requires_grad or any(q.requires_grad for q in self.parameters())):
-            raise NotImplementedError(
-                "backward through the fused MLP is not implemented yet (SURVEY §8f row 1); "
-                "call under torch.no_grad()")
         batches = p.shape[:-1]
         x = p.reshape(-1, self.in_size).float().contiguous()
         lat = None
         if latent is not None:
             lat = latent.reshape(-1, self.latent_size).float().contiguous()
-        y = torch.empty(x.shape[0], self.out.out_features, device=p.device)
-        _lib.call("nrt_mlp_forward", self.nrt(), _lib.ptr(x), _lib.ptr(lat), x.shape[0],
-                  _lib.ptr(y), _lib.precision_code(), _lib.stream())
+        params = [t for lin in self._linears() for t in (lin.weight, lin.bias)]
+        needs_grad = torch.is_grad_enabled() and (
+            x.requires_grad or (lat is not None and lat.requires_grad) or
+            any(q.requires_grad for q in params))
+        if needs_grad:
+            if any(t.device != p.device for t in params):
+                # as nn.Linear would: the HIP backward writes gradients next to the parameters
+                raise _lib.NrtError("SkipConnMLP parameters and inputs are on different devices: "
+                                    "move the module to the GPU (.to(device)) to train it")
+            # autograd through the HIP MLP: nrt_mlp_forward, then nrt_mlp_backward (FP32)
+            y = _MlpFn.apply(self, x, lat, *params)
+        else:
+            y = _mlp_forward(self, x, lat)
         return y.reshape(batches + (self.out.out_features,))
+
+
+def _mlp_forward(mlp, x, lat):
+    y = torch.empty(x.shape[0], mlp.out.out_features, device=x.device)
+    _lib.call("nrt_mlp_forward", mlp.nrt(), _lib.ptr(x), _lib.ptr(lat), x.shape[0],
+              _lib.ptr(y), _lib.precision_code(), _lib.stream())
+    return y
+
+
+class _MlpFn(torch.autograd.Function):
+    """y = SkipConnMLP(x, latent) with gradients for x, latent and every nn.Linear weight and
+    bias from nrt_mlp_backward.  basis_p is a plain tensor attribute in the
+    reference (no gradient), as here."""
+
+    @staticmethod
+    def forward(ctx, mlp, x, lat, *params):
+        with torch.no_grad():
+            y = _mlp_forward(mlp, x.detach(), None if lat is None else lat.detach())
+        ctx.mlp = mlp
+        ctx.handle = mlp_handle(mlp)  # the packed weights this forward used
+        ctx.has_lat = lat is not None
+        ctx.save_for_backward(x, lat if lat is not None else x.new_empty(0))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        import ctypes
+        x, lat = ctx.saved_tensors
+        lat = lat if ctx.has_lat else None
+        mlp = ctx.mlp
+        lib = _lib.load(require_device=True)
+        M = x.shape[0]
+        dy = dy.float().contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
+        dlat = torch.empty_like(lat) if (lat is not None and ctx.needs_input_grad[2]) else None
+        lins = mlp._linears()
+        dws = [torch.empty_like(lin.weight) if lin.weight.requires_grad else None for lin in lins]
+        dbs = [torch.empty_like(lin.bias) if lin.bias.requires_grad else None for lin in lins]
+        wp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dws])
+        bp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dbs])
+        ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(ctx.handle.value, M),
+                         dtype=torch.uint8, device=x.device)
+        _lib.call("nrt_mlp_backward", ctx.handle.value, _lib.ptr(x), _lib.ptr(lat), M,
+                  _lib.ptr(dy), _lib.ptr(dx), _lib.ptr(dlat), wp, bp, _lib.ptr(ws),
+                  _lib.stream())
+        grads = [g for pair in zip(dws, dbs) for g in pair]
+        return (None, dx, dlat, *grads)

@@ -1,0 +1,119 @@
+"""Autograd through the HIP SkipConnMLP (first slice): nrt_mlp_backward vs
+torch autograd of the oracle's SkipMLP (neural_blocks.py:12-86 restated) in float64 on the CPU.
+Tolerance per tensor: max|got - want64| <= max(1e-4 * max(1, max|want64|), 4 * e32), where e32 is
+the error of the same oracle run in float32 (the reference's own precision): gradients through
+sigma-32 Fourier features of 70 inputs are ill-conditioned in FP32 for any implementation."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import pathtracer_ref as R
+from tests.helpers import copy_mlp, seeded
+
+SHAPES = {
+    "8x64_leaky": dict(num_layers=8, hidden_size=64, in_size=3, out=3, freqs=16),
+    "sdf_shift_8x128_softplus": dict(num_layers=8, hidden_size=128, in_size=3, out=1, freqs=32,
+                                     activation="softplus"),
+    "nerfle_second_70in": dict(num_layers=8, hidden_size=64, in_size=70, out=3, freqs=16),
+    "latent_4x32": dict(num_layers=4, hidden_size=32, in_size=3, out=4, freqs=8, latent_size=8),
+}
+
+
+def _pair(kw, seed):
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    seeded(seed)
+    act = kw.get("activation", "leaky_relu")
+    ref = R.SkipMLP(**kw)
+    pkw = {k: v for k, v in kw.items() if k != "activation"}
+    if act == "softplus":
+        pkw["activation"] = F.softplus
+    mine = SkipConnMLP(device="cpu", **pkw)
+    copy_mlp(mine, ref)
+    return ref, mine.cuda()
+
+
+def _close(got, want, ref32, what):
+    scale = max(1.0, want.abs().max().item())
+    err = (got.detach().cpu().double() - want).abs().max().item()
+    e32 = (ref32.detach().double() - want).abs().max().item()
+    tol = max(1e-4 * scale, 4 * e32)
+    assert err <= tol, f"{what}: max|diff| {err:.3g} > {tol:.3g} (scale {scale:.3g}, fp32 ref {e32:.3g})"
+
+
+def _grads(ref, x, lat, dy, dtype):
+    import copy
+    m = copy.deepcopy(ref).to(dtype)
+    m.basis_p = ref.basis_p.to(dtype)
+    xr = x.detach().clone().to(dtype).requires_grad_(True)
+    lr = lat.detach().clone().to(dtype).requires_grad_(True) if lat is not None else None
+    (m(xr, lr) * dy.to(dtype)).sum().backward()
+    out = {"dx": xr.grad}
+    if lr is not None:
+        out["dlatent"] = lr.grad
+    for i, lin in enumerate([m.init, *m.layers, m.out]):
+        out[f"dW[{i}]"] = lin.weight.grad
+        out[f"db[{i}]"] = lin.bias.grad
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 33, 1000])
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_mlp_backward_matches_autograd(name, M):
+    from neural_raytracing_amd import set_precision
+    kw = SHAPES[name]
+    ref, mine = _pair(kw, 40 + M)
+    set_precision("fp32")
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, kw["in_size"], generator=g) - 0.5)
+    lat = torch.randn(M, kw["latent_size"], generator=g) if kw.get("latent_size") else None
+    dy = torch.randn(M, kw["out"], generator=g)
+    want = _grads(ref, x, lat, dy, torch.float64)
+    ref32 = _grads(ref, x, lat, dy, torch.float32)
+    # HIP
+    xm = x.cuda().requires_grad_(True)
+    lm = lat.cuda().requires_grad_(True) if lat is not None else None
+    y = mine(xm, lm)
+    (y * dy.cuda()).sum().backward()
+    got = {"dx": xm.grad}
+    if lat is not None:
+        got["dlatent"] = lm.grad
+    for i, a in enumerate(mine._linears()):
+        got[f"dW[{i}]"] = a.weight.grad
+        got[f"db[{i}]"] = a.bias.grad
+    assert set(got) == set(want)
+    for k in want:
+        _close(got[k], want[k], ref32[k], k)
+
+
+@pytest.mark.gpu
+def test_mlp_training_steps_reduce_loss():
+    """A few Adam steps of an 8x64 SkipConnMLP fitting a smooth target on the HIP path."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    set_precision("fp32")
+    seeded(3)
+    mlp = SkipConnMLP(num_layers=4, hidden_size=64, in_size=3, out=1, freqs=8, sigma=2,
+                      device="cuda").to("cuda")
+    x = torch.rand(4096, 3, device="cuda") * 2 - 1
+    t = (x.norm(dim=-1, keepdim=True) - 0.5)
+    opt = torch.optim.Adam(mlp.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        loss = (mlp(x) - t).square().mean()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0], losses
+
+
+@pytest.mark.gpu
+def test_mlp_parameters_on_another_device_are_refused():
+    """Parameters left on the CPU with GPU inputs fail loudly (as nn.Linear does), before any
+    HIP launch could be handed host pointers."""
+    from neural_raytracing_amd import NrtError
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    mlp = SkipConnMLP(num_layers=2, hidden_size=32, in_size=3, out=1, freqs=4, device="cuda")
+    with pytest.raises(NrtError):
+        mlp(torch.rand(8, 3, device="cuda"))
