@@ -92,6 +92,17 @@ int nrt_mlp_backward(const nrt_mlp* mlp, const float* x, const float* latent, in
                      const float* dy, float* dx, float* dlatent, float* const* dweights,
                      float* const* dbiases, void* workspace, void* stream);
 
+/* Double backward of the input gradient (SDF.autograd_diff with
+ * create_graph=True, sdfs.py:184-197, differentiated again by loss.backward()): for
+ * g(x) = d(sum_o y_o)/dx [M, in] (torch.autograd.grad with grad_outputs = ones) and v [M, in] =
+ * dL/dg, writes dweights[l], dbiases[l] = d(sum_rows v . g)/dW_l, /db_l in the nn.Linear layouts
+ * (FP32; latent is held constant; x is not differentiated).  Gradients are overwritten.
+ * workspace: nrt_mlp_grad_backward_workspace_bytes(mlp, M) bytes of device memory. */
+size_t nrt_mlp_grad_backward_workspace_bytes(const nrt_mlp* mlp, int64_t M);
+int nrt_mlp_grad_backward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,
+                          const float* v, float* const* dweights, float* const* dbiases,
+                          void* workspace, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Signed distance fields (shapes/sdfs.py)
  * ------------------------------------------------------------------------------------- */
@@ -121,6 +132,8 @@ typedef struct {
   int32_t primary;     /* 1: run the 128-step coarse scan (SDF.throughput, sdfs.py:232)     */
   double scan_max_t;   /* dist + random.random()*(2/128), computed by the caller           */
   int32_t precision;   /* NRT_FP32 / NRT_FP16                                               */
+  int32_t* scan_index; /* optional [P] output: the coarse-scan argmin idxs (sdfs.py:243-246), so a
+                          training caller can rebuild best_pos = o + idx*step*d; NULL = unused  */
 } nrt_march_params;
 
 /* SDF.intersect (sdfs.py:111-160) for P rays.  Outputs (each [P] or [P,3]):

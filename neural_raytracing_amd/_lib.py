@@ -34,7 +34,8 @@ class MlpDesc(ctypes.Structure):
 class MarchParams(ctypes.Structure):
     _fields_ = [("max_steps", ctypes.c_int32), ("epsilon", ctypes.c_float),
                 ("max_t", ctypes.c_float), ("primary", ctypes.c_int32),
-                ("scan_max_t", ctypes.c_double), ("precision", ctypes.c_int32)]
+                ("scan_max_t", ctypes.c_double), ("precision", ctypes.c_int32),
+                ("scan_index", ctypes.c_void_p)]
 
 
 class BsdfComponent(ctypes.Structure):
@@ -90,6 +91,8 @@ _SIGNATURES = {
     "nrt_light_envmap": (_I32, [_P, _I32, _P, _P]),
     "nrt_mlp_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_mlp_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "nrt_mlp_grad_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
+    "nrt_mlp_grad_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "nrt_frames": (_I32, [_P, _P, _I64, _P, _P, _P]),
     "nrt_profile_enable": (None, [_I32]),
     "nrt_profile_reset": (None, []),

@@ -175,6 +175,7 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   ma.max_t = a->max_t;
   ma.primary = a->primary;
   ma.step = a->scan_max_t / 128.0;
+  ma.scan_idx = a->primary ? a->scan_index : nullptr;
   // the normal pass needs the list of hit rays; use the caller's or a workspace-backed one
   int32_t* idx = hit_idx;
   int32_t* cnt = hit_count;
@@ -197,6 +198,10 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
     ProfScope prof("k_intersect", st);
     auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
     rc0 = ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
+    if (!rc0 && ma.scan_idx) {
+      k_keys_index<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, st>>>(keys, P, ma.scan_idx);
+      rc0 = check_launch("k_keys_index");
+    }
   } else {
     ProfScope prof("k_intersect", st);
     NRT_NB_SWITCH(s->host_dev.nb, {

@@ -164,6 +164,184 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
     for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[2 * F + in + j];
 }
 
+// second derivative of act at pre-activation x (torch double-backward formulas:
+// softplus_double_backward = s(1-s) where x < threshold, sigmoid: s(1-s)(1-2s), piecewise-linear: 0)
+__device__ __forceinline__ float act_bwd2(float x, int act) {
+  switch (act) {
+    case ACT_SOFTPLUS: {
+      if (!(x < 20.f)) return 0.f;
+      const float s = 1.f / (1.f + expf(-x));
+      return s * (1.f - s);
+    }
+    case ACT_SIGMOID: {
+      const float s = 1.f / (1.f + expf(-x));
+      return s * (1.f - s) * (1.f - 2.f * s);
+    }
+    default: return 0.f;
+  }
+}
+
+// Double backward of the input gradient g(x) = d(sum_o y_o)/dx (SDF.autograd_diff with
+// create_graph=True, sdfs.py:184-197): the parameter gradients of J = sum_rows v . g(x) for a
+// given v = dL/dg.  J is the forward-mode derivative of sum_o y_o along v, so one pass runs the
+// MLP forward with a tangent (z_l, zt_l = W_l tangent-inputs), then the reverse of both chains:
+//   zt_bar = at_bar act'(z),   z_bar = a_bar act'(z) + at_bar act''(z) zt,
+//   a_bar(l-1) = W_l^T z_bar,   at_bar(l-1) = W_l^T zt_bar     (hidden inputs; at_bar_L = W_out^T 1)
+// and dW_l = z_bar^T In_l + zt_bar^T InT_l, db_l = sum z_bar, done afterwards as one GEMM over the
+// stacked [primal; tangent] rows.  Slab row: [a | enc | enc tangent | a tangent].
+template <int NB>
+__global__ void __launch_bounds__(256) k_mlp_grad_backward32(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    const float* __restrict__ v, int64_t M, float* __restrict__ Zg, float* __restrict__ Tg,
+    float* __restrict__ Ag, float* __restrict__ E0, float* __restrict__ E1,
+    float* __restrict__ dZg, int RS, int per_wave) {
+  extern __shared__ float smem[];
+  const MlpDev& m = *mp;
+  float* X = smem + (size_t)(threadIdx.x >> 6) * per_wave;
+  const int lane = lane_id(), r = lane & 31, h = lane >> 5;
+  const int64_t row0 = wave_global() * 32;
+  if (row0 >= M) return;  // whole wave exits together
+  const int64_t row = row0 + r;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  const int H = m.hidden, L = m.n_hidden, ke = m.ke, dp = m.dp, in = m.in_size, F = m.freqs;
+  const int EE = H, ET = H + ke, PT = H + 2 * ke;
+  const int64_t M2 = 2 * M;
+  EncIn e;
+  if (in <= 4) {
+    for (int i = 0; i < 4; ++i) e.x[i] = (i < in) ? x[rr * in + i] : 0.f;
+    e.xg = nullptr;
+  } else {
+    e.x[0] = e.x[1] = e.x[2] = e.x[3] = 0.f;
+    e.xg = x + rr * in;
+  }
+  e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
+  float* rowp = X + r * RS;
+  const float* vr = v + rr * in;
+  // ---- encoding and its tangent along v: d sin(xB_q) = cos(xB_q) (vB)_q, d cos = -sin (vB)_q
+  write_enc_slab<false>(m, e, X, RS);
+  for (int s = h; s < ke; s += 2) {
+    float tv = 0.f;
+    if (s < 2 * F) {
+      const int q = s >> 1;
+      float vb = vr[0] * m.basis[q];
+      for (int i = 1; i < in; ++i) vb = fmaf(vr[i], m.basis[i * F + q], vb);
+      float sn, cs;
+      sincosf(proj<false>(m, e, q), &sn, &cs);
+      tv = (s & 1) ? -sn * vb : cs * vb;
+    } else if (s < 2 * F + in) {
+      tv = vr[s - 2 * F];
+    }
+    rowp[ET + s] = tv;
+  }
+  wave_lds_fence();
+  if (valid)
+    for (int s = h; s < ke; s += 2) {
+      const int c = enc_col(m, s);
+      if (c < 0) continue;
+      const float ev = rowp[EE + s], tv = rowp[ET + s];
+      E0[row * dp + c] = ev;
+      E0[(M + row) * dp + c] = tv;
+      E1[row * dp + c] = act_fwd<false>(ev, m.act);
+      E1[(M + row) * dp + c] = act_bwd(ev, m.act) * tv;
+    }
+  // ---- forward: primal then tangent per layer
+  f16v acc[NB];
+  for (int l = 0; l <= L; ++l) {
+    const bool skip = l > 0 && (l - 1) != L - 1 && ((l - 1) % m.skip) == 0;
+    bias32<NB>(acc, m.bias[l], 0, NB, h);
+    if (l == 0) {
+      gemm32<NB>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, EE, -1);
+    } else {
+      gemm32<NB>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
+      if (skip) gemm32<NB>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, EE, m.act);
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const float z = acc[ib][reg];
+        const float a = act_fwd<false>(z, m.act);
+        if (valid) {
+          Zg[((int64_t)l * M + row) * H + k] = z;
+          Ag[((int64_t)l * M2 + row) * H + k] = a;
+        }
+        rowp[k] = a;
+      }
+    wave_lds_fence();
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+    if (l == 0) {
+      gemm32<NB>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, ET, -1);
+    } else {
+      gemm32<NB>(acc, m.w32[l], NB, 0, H >> 1, X, RS, PT, -1);
+      if (skip) gemm32<NB>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, ET, -1);
+    }
+    wave_lds_fence();
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const int k = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+        const float zt = acc[ib][reg];
+        const float z = valid ? Zg[((int64_t)l * M + row) * H + k] : 0.f;
+        const float at = act_bwd(z, m.act) * zt;
+        if (valid) {
+          Tg[((int64_t)l * M + row) * H + k] = zt;
+          Ag[((int64_t)l * M2 + M + row) * H + k] = at;
+        }
+        rowp[PT + k] = at;
+      }
+    if (l == 0)  // skip layers consume act(enc): tangent act'(enc) * enc tangent
+      for (int s = h; s < ke; s += 2) rowp[ET + s] = act_bwd(rowp[EE + s], m.act) * rowp[ET + s];
+    wave_lds_fence();
+  }
+  // ---- reverse: seed a_bar_L = 0, at_bar_L = W_out^T 1
+  const float* Ao = m.w32[L + 1];
+  for (int k = h; k < H; k += 2) {
+    float g = 0.f;
+    for (int o = 0; o < m.out; ++o) g += Ao[((k >> 1) * m.ob + (o >> 5)) * 64 + (k & 1) * 32 + (o & 31)];
+    rowp[k] = 0.f;
+    rowp[PT + k] = g;
+  }
+  wave_lds_fence();
+  for (int l = L; l >= 0; --l) {
+    for (int k = h; k < H; k += 2) {
+      const float z = valid ? Zg[((int64_t)l * M + row) * H + k] : 0.f;
+      const float zt = valid ? Tg[((int64_t)l * M + row) * H + k] : 0.f;
+      const float d1 = act_bwd(z, m.act);
+      const float ab = rowp[k], atb = rowp[PT + k];
+      const float zb = ab * d1 + atb * act_bwd2(z, m.act) * zt;
+      const float ztb = atb * d1;
+      rowp[k] = zb;
+      rowp[PT + k] = ztb;
+      if (valid) {
+        dZg[((int64_t)l * M2 + row) * H + k] = zb;
+        dZg[((int64_t)l * M2 + M + row) * H + k] = ztb;
+      }
+    }
+    wave_lds_fence();
+    if (l == 0) break;
+    const float* At = m.wt32[l];
+    const int nrb = m.nbt[l];
+    for (int pass = 0; pass < 2; ++pass) {
+      const int col = pass ? PT : 0;
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
+      gemm32<NB>(acc, At, nrb, 0, H >> 1, X, RS, col, -1);
+      wave_lds_fence();
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg)
+          rowp[col + 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[ib][reg];
+      wave_lds_fence();
+    }
+  }
+}
+
 template <int = 0>
 __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -302,6 +480,112 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
       if (rc) return rc;
     }
     if (dbiases && dbiases[l] && (rc = grad_bias(hb, dZ, R, M, w.ones, dbiases[l]))) return rc;
+  }
+  return NRT_OK;
+}
+
+static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[8]) {
+  const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
+  sz[0] = lay;          // Z
+  sz[1] = lay;          // Z tangent
+  sz[2] = 2 * lay;      // A stacked
+  sz[3] = 2 * lay;      // dZ stacked
+  sz[4] = (size_t)2 * M * d.dp * 4;   // E0
+  sz[5] = sz[4];                      // E1
+  sz[6] = (size_t)2 * M * d.out * 4;  // output seed
+  sz[7] = (size_t)M * 4;              // ones
+  size_t tot = 0;
+  for (int i = 0; i < 8; ++i) tot += a256(sz[i]);
+  return tot;
+}
+
+size_t nrt_mlp_grad_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
+  if (!m) return 0;
+  size_t sz[8];
+  return gb_sizes(m->host_dev, std::max<int64_t>(M, 1), sz);
+}
+
+int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent, int64_t M,
+                          const float* v, float* const* dweights, float* const* dbiases,
+                          void* workspace, void* stream) {
+  if (!m || M < 0 || (M > 0 && (!x || !v || !workspace))) {
+    set_error("nrt_mlp_grad_backward: bad argument");
+    return NRT_EINVAL;
+  }
+  const MlpDev& d = m->host_dev;
+  if (d.latent > 0 && !latent) { set_error("nrt_mlp_grad_backward: latent required"); return NRT_EINVAL; }
+  if (M > INT32_MAX / 2) { set_error("nrt_mlp_grad_backward: at most 2^30-1 rows per call"); return NRT_EINVAL; }
+  hipStream_t st = (hipStream_t)stream;
+  const int L = d.n_hidden, H = d.hidden;
+  auto zero_all = [&]() -> int {
+    for (int l = 0; l < L + 2; ++l) {
+      const int R = l == L + 1 ? d.out : H;
+      const int C = m->host_w[l].size() / (size_t)R;
+      if (dweights && dweights[l]) NRT_HIP(hipMemsetAsync(dweights[l], 0, (size_t)R * C * 4, st));
+      if (dbiases && dbiases[l]) NRT_HIP(hipMemsetAsync(dbiases[l], 0, (size_t)R * 4, st));
+    }
+    return NRT_OK;
+  };
+  if (M == 0) return zero_all();
+  if (!dweights && !dbiases) return NRT_OK;
+  size_t sz[8];
+  gb_sizes(d, M, sz);
+  float* buf[8];
+  char* p = (char*)workspace;
+  for (int i = 0; i < 8; ++i) { buf[i] = (float*)p; p += a256(sz[i]); }
+  // slab row: primal activations | encoding | encoding tangent | tangent activations
+  const int RS = (2 * std::max(H, 32) + 2 * std::max(d.ke, 16)) | 1;
+  const int per_wave = 32 * RS;
+  const int waves = std::max(1, std::min(4, kLdsBytes / (per_wave * 4)));
+  const size_t bytes = (size_t)waves * per_wave * 4;
+  if (bytes > (size_t)kLdsBytes) { set_error("nrt_mlp_grad_backward: MLP too wide for LDS"); return NRT_EINVAL; }
+  const int nwaves = ceil_div64(M, 32);
+  dim3 grid(ceil_div64(nwaves, waves)), block(64 * waves);
+  int rc = NRT_OK;
+  {
+    ProfScope prof("k_mlp_grad_backward32", st);
+    NRT_NB_SWITCH(d.nb, {
+      if (!(rc = set_lds(k_mlp_grad_backward32<NB>, bytes)))
+        k_mlp_grad_backward32<NB><<<grid, block, bytes, st>>>(m->dev, x, latent, v, M, buf[0], buf[1],
+                                                             buf[2], buf[4], buf[5], buf[3], RS,
+                                                             per_wave);
+    });
+    if (rc) return rc;
+    if ((rc = check_launch("k_mlp_grad_backward32"))) return rc;
+  }
+  const int64_t M2 = 2 * M;
+  float* seed = buf[6];
+  float* ones = buf[7];
+  NRT_HIP(hipMemsetAsync(seed, 0, (size_t)M * d.out * 4, st));
+  k_fill<><<<dim3(std::min<int64_t>(ceil_div64(M * d.out, 256), 1024)), dim3(256), 0, st>>>(
+      seed + (size_t)M * d.out, M * d.out, 1.f);
+  k_fill<><<<dim3(std::min<int64_t>(ceil_div64(M, 256), 1024)), dim3(256), 0, st>>>(ones, M, 1.f);
+  if ((rc = check_launch("k_fill"))) return rc;
+  rocblas_handle hb = blas();
+  if (!hb) { set_error("nrt_mlp_grad_backward: rocblas_create_handle failed"); return NRT_EHIP; }
+  rocblas_status s = rocblas_set_stream(hb, st);
+  if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
+  const size_t lay2 = (size_t)M2 * H;
+  for (int l = 0; l <= L + 1; ++l) {
+    const bool outl = l == L + 1;
+    const int R = outl ? d.out : H;
+    const float* dZ = outl ? seed : buf[3] + (size_t)l * lay2;
+    if (dweights && dweights[l]) {
+      if (l == 0) {
+        rc = grad_gemm(hb, dZ, R, buf[4], d.dp, M2, dweights[0], d.dp, 0);
+      } else {
+        const int i = l - 1;
+        const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
+        const int C = H + (skip ? d.dp : 0);
+        rc = grad_gemm(hb, dZ, R, buf[2] + (size_t)(l - 1) * lay2, H, M2, dweights[l], C, 0);
+        if (!rc && skip) rc = grad_gemm(hb, dZ, R, buf[5], d.dp, M2, dweights[l], C, H);
+      }
+      if (rc) return rc;
+    }
+    if (dbiases && dbiases[l]) {
+      if (outl) NRT_HIP(hipMemsetAsync(dbiases[l], 0, (size_t)R * 4, st));
+      else if ((rc = grad_bias(hb, dZ, R, M, ones, dbiases[l]))) return rc;
+    }
   }
   return NRT_OK;
 }

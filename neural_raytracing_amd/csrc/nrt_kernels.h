@@ -248,6 +248,7 @@ struct MarchArgs {
   float max_t;
   int primary;
   double step;  // scan step = scan_max_t / 128 (python float)
+  int32_t* scan_idx;  // optional [P] coarse-scan argmin output
 };
 
 template <bool F16, int NB>
@@ -328,6 +329,7 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
     n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
     if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
     if (a.primary) thr_out[ray] = thr;
+    if (a.primary && a.scan_idx) a.scan_idx[ray] = idx;
   }
   if (hit_idx) {
     // wave-aggregated append of the hit rays (order is irrelevant downstream)
@@ -504,6 +506,14 @@ __global__ void __launch_bounds__(64 * WV, 2) k_scan_best16(NRT_MARCH_ARGS) {
   march16_body<NB, NE, WV, FOLD, 1>(s, m, rays, P, a, t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys);
 }
 #undef NRT_MARCH_ARGS
+
+// coarse-scan argmin index of each ray from the ring march's 64-bit keys ([ordered min | idx])
+template <int = 0>
+__global__ void k_keys_index(const unsigned long long* __restrict__ keys, int64_t P,
+                             int32_t* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P) idx[i] = (int32_t)(uint32_t)keys[i];
+}
 
 // hit list of a finished march (order is irrelevant downstream): wave-aggregated appends
 template <int = 0>

@@ -36,8 +36,8 @@ def _host(t):
     return t.detach().to("cpu", torch.float32).contiguous()
 
 
-def _cache(owner, tensors, build):
-    key = _key(tensors)
+def _cache(owner, tensors, build, extra=()):
+    key = (_key(tensors), tuple(extra))
     cached = getattr(owner, "_nrt_cache", None)
     if cached is not None and cached[0] == key:
         return cached[1]
@@ -65,4 +65,5 @@ def mlp_handle(mlp):
                                       ctypes.byref(out)), "nrt_mlp_create")
         return _Handle(out, "nrt_mlp_destroy")
 
-    return _cache(mlp, params, build)
+    # the activation is packed too (and folded into the FP16 ring stream): re-pack on a change
+    return _cache(mlp, params, build, extra=(mlp.activation_code(),))

@@ -1,0 +1,238 @@
+"""Training through the fused path: the differentiable pieces of
+``SDF.intersect`` and ``Direct.sample`` for ``loss.backward()``.
+
+Rendering with gradients keeps the reference's split: the march and the 128-step coarse scan
+run without gradients (``torch.no_grad`` in sdfs.py:118-131, :239-247) on the fused HIP
+kernels; what carries gradients is recomputed at the points they found:
+
+* ``throughput = -1000 * sdf(best_pos)`` (sdfs.py:134-137, :248) -- the SDF MLP forward and
+  backward on ``nrt_mlp_forward`` / ``nrt_mlp_backward``;
+* ``raw_normals = d sdf / d p`` with ``create_graph=True`` (sdfs.py:184-197) --
+  ``nrt_mlp_backward`` for the value, ``nrt_mlp_grad_backward`` for its parameter gradients;
+* the shading MLPs (spatial weights, NeuralBSDFs, LightField) -- ``SkipConnMLP`` autograd.
+
+The glue between the MLPs (frames, Rusinkiewicz angles, Fresnel, light falloff, the 128-sphere
+smooth-min of ``SphereSDF``) is a few element-wise tensor ops per ray, written here in the
+reference's op order so autograd reproduces its gradients.
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from .. import _lib
+
+
+# ---- interaction frames (interaction.py:9-51) -------------------------------------------------
+
+def coordinate_system(n):
+    """Shading frame columns [s, t, n] (interaction.py:9-27), differentiable."""
+    n = F.normalize(n, eps=1e-7, dim=-1)
+    x, y, z = n.split(1, dim=-1)
+    sign = torch.where(z >= 0, 1., -1.)
+    s_z = sign + z
+    a = -torch.where(s_z.abs() < 1e-6, torch.tensor(1e-6, device=z.device), s_z).reciprocal()
+    b = x * y * a
+    s = torch.cat([(x * x * a * sign) + 1, b * sign, x * -sign], dim=-1)
+    s = F.normalize(s, eps=1e-7, dim=-1)
+    t = F.normalize(s.cross(n, dim=-1), eps=1e-7, dim=-1)
+    s = F.normalize(n.cross(t, dim=-1), eps=1e-7, dim=-1)
+    return torch.stack([s, t, n], dim=-1)
+
+
+# ---- BSDF helpers (utils.py:43-51, 152-155, 234-258; bsdfs.py:127-129, 327-343) --------------
+
+def nonzero_eps(v, eps: float = 1e-7):
+    return torch.where(v.abs() < eps, torch.tensor(eps, device=v.device), v)
+
+
+def rotate_vector(v, axis, c, s):
+    return v * c + axis * (v * axis).sum(dim=-1, keepdim=True) * (1 - c) + \
+        torch.cross(axis, v, dim=-1) * s
+
+
+def param_rusin2(wo, wi):
+    """[cos phi_d, cos theta_h, cos theta_d] (utils.py:234-258)."""
+    wo = F.normalize(wo, dim=-1)
+    wi = F.normalize(wi, dim=-1)
+    e_1 = torch.tensor([0, 1, 0], device=wo.device, dtype=torch.float).expand_as(wo)
+    e_2 = torch.tensor([0, 0, 1], device=wo.device, dtype=torch.float).expand_as(wo)
+    H = F.normalize(wo + wi, dim=-1)
+    cos_theta_h = H[..., 2]
+    r = nonzero_eps(H[..., 1]).hypot(nonzero_eps(H[..., 0])).clamp(min=1e-6)
+    c = (H[..., 0] / r).unsqueeze(-1)
+    s = -(H[..., 1] / r).unsqueeze(-1)
+    tmp = F.normalize(rotate_vector(wi, e_2, c, s), dim=-1)
+    c = H[..., 2].unsqueeze(-1)
+    s = -(1 - H[..., 2]).clamp(min=1e-6).sqrt().unsqueeze(-1)
+    diff = F.normalize(rotate_vector(tmp, e_1, c, s), dim=-1)
+    cos_theta_d = diff[..., 2]
+    cos_phi_d = torch.atan2(nonzero_eps(diff[..., 1]), nonzero_eps(diff[..., 0])).cos()
+    return torch.stack([cos_phi_d, cos_theta_h, cos_theta_d], dim=-1)
+
+
+def local_reflect(v):
+    x, y, z = v.split(1, dim=-1)
+    return torch.cat([-x, -y, z], dim=-1)
+
+
+def fresnel_conductor(cos_t, eta_r: float, eta_i: float):
+    ct2 = cos_t * cos_t
+    st2 = (1 - ct2).clamp(min=1e-10)
+    st4 = st2 * st2
+    tmp = eta_r * eta_r - eta_i * eta_i - st2
+    a_2_pb_2 = (tmp * tmp + 4 * eta_i * eta_i * eta_r * eta_r).clamp(min=1e-10).sqrt()
+    a = (0.5 * (a_2_pb_2 + tmp)).clamp(min=1e-10).sqrt()
+    t1 = a_2_pb_2 + ct2
+    t2 = 2 * cos_t * a
+    r_s = (t1 - t2) / (t1 + t2)
+    t3 = a_2_pb_2 * ct2 + st4
+    t4 = t2 * st2
+    r_p = r_s * (t3 - t4) / (t3 + t4)
+    return 0.5 * (r_s + r_p)
+
+
+# ---- SDF values and gradients with autograd ---------------------------------------------------
+
+def needs_grad(*modules):
+    """True when autograd is on and any parameter of the given objects requires a gradient."""
+    if not torch.is_grad_enabled():
+        return False
+    for m in modules:
+        params = getattr(m, "parameters", None)
+        if params is None:
+            continue
+        try:
+            if any(getattr(q, "requires_grad", False) for q in params()):
+                return True
+        except (TypeError, AttributeError):
+            continue
+    return False
+
+
+def sphere_part(sdf, p):
+    """The smooth-min of the transformed spheres of SphereSDF (sdfs.py:37-43, utils.py:386-387)."""
+    flat = p.reshape(-1, 3).unsqueeze(0)
+    tfs = sdf.tfs + torch.eye(3, device=p.device).unsqueeze(0)
+    q = torch.einsum("ijk,ibk->ibj", tfs, flat.expand(tfs.shape[0], -1, -1)) - \
+        sdf.centers.unsqueeze(1)
+    sd = q.norm(p=2, dim=-1) - sdf.radii.unsqueeze(-1)
+    return (-(-32. * sd).exp().sum(dim=0).clamp(min=1e-4).log() / 32.).reshape(p.shape[:-1])
+
+
+def sdf_value(sdf, p):
+    """sdf(p) with gradients for the SDF's parameters."""
+    from .neural_blocks import SkipConnMLP
+    from .shapes.sdfs import SPHERE_SDF, _is_sphere_sdf
+    if sdf is SPHERE_SDF:
+        return torch.norm(p, dim=-1) - 1
+    if isinstance(sdf, SkipConnMLP):
+        return sdf(p).reshape(p.shape[:-1])
+    if _is_sphere_sdf(sdf):
+        out = sphere_part(sdf, p)
+        return out + sdf.shift(p).reshape_as(out)
+    raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP training path")
+
+
+def sdf_gradient(sdf, p):
+    """SDF.autograd_diff (sdfs.py:184-197): d sdf / d p, differentiable with respect to the
+    SDF's parameters (create_graph=True).  ``p`` itself is not differentiated (the reference's
+    hit points come from the no-grad march)."""
+    from .neural_blocks import SkipConnMLP, input_gradient
+    from .shapes.sdfs import SPHERE_SDF, _is_sphere_sdf
+    p = p.detach()
+    if sdf is SPHERE_SDF:
+        return p / torch.norm(p, dim=-1, keepdim=True)
+    if isinstance(sdf, SkipConnMLP):
+        return input_gradient(sdf, p)
+    if _is_sphere_sdf(sdf):
+        with torch.enable_grad():
+            q = p.clone().requires_grad_(True)
+            out = sphere_part(sdf, q)
+            (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+        return g + input_gradient(sdf.shift, p)
+    raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP training path")
+
+
+# ---- shading (integrators.py:139-206 with emitter_samples=1, bsdf_samples=0) -----------------
+
+def light_sample(lights, it, active):
+    """sample_emitter_dir_wo_isect (scene.py:321-324) -> (d, Le, pdf)."""
+    from .lights.lights import LightField, PointLights
+    p = it.p
+    if isinstance(lights, LightField):
+        # lights.py:175-195
+        v = lights.light_field_approx(p[active])
+        d = torch.zeros_like(p)
+        d[active] = F.normalize(v, eps=1e-6, dim=-1).clamp(min=1e-6, max=1)
+        le = torch.zeros_like(p)
+        le[active] = torch.linalg.norm(v, ord=2, dim=-1, keepdim=True) * lights.color.sigmoid()
+        pdf = torch.ones(p.shape[:-1], device=p.device)
+    elif isinstance(lights, PointLights):
+        # lights.py:89-110
+        loc = lights.location.reshape(-1, 3)[0]
+        d = loc - p
+        dist = torch.linalg.norm(d, dim=-1, keepdim=True)
+        d = F.normalize(d, eps=1e-6, dim=-1)
+        fall = lights.const.clamp(min=1e-6).to(p.device) + \
+            lights.linear.clamp(min=1e-6).to(p.device) * dist + \
+            lights.square.clamp(min=1e-6).to(p.device) * dist.square()
+        color = lights.intensity.reshape(-1, 3)[0]
+        le = lights.scale.to(p.device) * F.normalize(color, dim=-1) / fall.clamp(min=1e-6)
+        pdf = torch.ones(p.shape[:-1], device=p.device)
+    else:
+        raise _lib.NrtError(f"light {type(lights).__name__} has no HIP training path")
+    le = torch.where(active.unsqueeze(-1), le, torch.zeros_like(le))
+    return d, le, pdf
+
+
+def bsdf_eval(bsdf, it, wo, active):
+    """eval_and_pdf of the supported BSDFs (bsdfs.py:108-118, 364-388, 515-536, 634-637)."""
+    from .bsdf.bsdfs import ComposeSpatialVarying, Conductor, Diffuse, NeuralBSDF, identity_div_pi
+    if isinstance(bsdf, ComposeSpatialVarying):
+        k = bsdf.sp_var_fn(bsdf.preprocess(it.p)).reshape(it.p.shape[:-1] + (len(bsdf.bsdfs),))
+        setattr(it, "nonnormalized_weights", k)
+        k = k.sigmoid()
+        parts = []
+        for b in bsdf.bsdfs:
+            f, pdf = bsdf_eval(b, it, wo, active)
+            parts.append(torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1))
+        spec_pdf = torch.stack(parts, dim=-1)
+        setattr(it, "normalized_weights", k)
+        spec_pdf = torch.where(active[..., None, None], spec_pdf * k.unsqueeze(-2),
+                               torch.zeros_like(spec_pdf))
+        f, pdf = spec_pdf.sum(dim=-1).split([3, 1], dim=-1)
+        return f, pdf.squeeze(-1)
+    if isinstance(bsdf, NeuralBSDF):
+        f = bsdf.act(bsdf.mlp(param_rusin2(it.wi, wo)))
+        return f, torch.ones(f.shape[:-1], device=f.device)
+    if isinstance(bsdf, Diffuse):
+        refl = bsdf.reflectance.to(wo.device)
+        x = wo[..., 2].unsqueeze(-1) * refl
+        f = x / math.pi if bsdf.preproc is identity_div_pi else bsdf.preproc(x)
+        return f, wo[..., 2] / math.pi
+    if isinstance(bsdf, Conductor):
+        refl = local_reflect(it.wi)
+        thresh = (refl * wo).sum(dim=-1, keepdim=True) > 0.94
+        fres = fresnel_conductor(it.wi[..., 2], float(F.softplus(bsdf.eta.detach())), 0.0)
+        fres = fres.reshape_as(thresh)
+        f = torch.where(thresh, fres * bsdf.act(bsdf.specular.to(wo.device)),
+                        torch.zeros_like(it.p))
+        pdf = torch.where(thresh.reshape(it.p.shape[:-1]), 1.0, 0.0)
+        f = torch.where(active.unsqueeze(-1), f, torch.zeros_like(f))
+        return f, pdf
+    raise _lib.NrtError(f"BSDF {type(bsdf).__name__} has no HIP training path")
+
+
+def direct_sample(it, active, bsdf, lights, lead, device):
+    """Direct.sample's shading with autograd (integrators.py:167-189)."""
+    result = torch.zeros(*lead, 3, device=device)
+    if not bool(active.any()):
+        return result
+    d, le, pdf = light_sample(lights, it, active)
+    ae = active & (pdf > 0)
+    wo = it.to_local(d)
+    f, _ = bsdf_eval(bsdf, it, wo, ae)
+    result = result.clone()
+    result[ae] = result[ae] + f[ae] * le[ae]
+    return result

@@ -5,6 +5,7 @@ import torch
 import torch.nn as nn
 
 from ... import _lib
+from ..differentiable import direct_sample, needs_grad
 
 
 class Integrator(nn.Module):
@@ -132,8 +133,13 @@ class Direct(Integrator):
         shadow, occ = _emitter_mode(kwargs.get("w_isect"))
         if self.emitter_samples != 1 or self.bsdf_samples != 0:
             raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
-        result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
         it, active = shapes.intersect(rays, primary=self.training)
+        if getattr(it, "_nrt_train", False) or needs_grad(bsdf, lights):
+            # training: shading with autograd through the HIP MLPs
+            if shadow:
+                raise _lib.NrtError("Direct with w_isect is not on the HIP training path")
+            return direct_sample(it, active, bsdf, lights, rays.shape[:-1], rays.device), active, it
+        result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
         hit_idx, hit_count, flat = it._nrt_hits
         P = flat.shape[0]
         rgb = result.reshape(P, 3)

@@ -8,6 +8,7 @@ import random
 
 import torch
 
+from .differentiable import needs_grad
 from .render import fused_integrator, render_tile
 from .samplers import Sampler
 
@@ -66,6 +67,8 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     ys = list(range(0, height, chunk_size))
     it = None
     fused = _fused(integrator, cameras, w_isect, addition)
+    if needs_grad(shapes, bsdf, lights):
+        fused = None  # training: integrator.sample carries the gradients
     for ij in range(len(xs) * len(ys)):
         i, j = divmod(ij, len(ys))
         x0, y0 = xs[j], ys[i]

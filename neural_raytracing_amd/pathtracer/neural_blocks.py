@@ -155,3 +155,76 @@ class _MlpFn(torch.autograd.Function):
                   _lib.stream())
         grads = [g for pair in zip(dws, dbs) for g in pair]
         return (None, dx, dlat, *grads)
+
+
+def input_gradient(mlp, x):
+    """d(sum_o mlp(x)_o)/dx -- torch.autograd.grad(mlp(x), x, ones, create_graph=True), the SDF
+    normal of SDF.autograd_diff (sdfs.py:184-197) -- on the HIP path: nrt_mlp_backward for the
+    value, nrt_mlp_grad_backward for its gradients with respect to every nn.Linear.  ``x`` is
+    not differentiated (second derivatives in x are not on the HIP path)."""
+    if not x.is_cuda:
+        raise _lib.NrtError("SkipConnMLP evaluates on the HIP path only: move it and its "
+                            "inputs to the GPU")
+    if mlp.latent_size:
+        raise _lib.NrtError("input_gradient: latent MLPs are not supported")
+    if torch.is_grad_enabled() and x.requires_grad:
+        raise _lib.NrtError("input_gradient: second derivatives with respect to the inputs are "
+                            "not on the HIP path (detach the points)")
+    lead = x.shape[:-1]
+    flat = x.reshape(-1, mlp.in_size).float().contiguous()
+    params = [t for lin in mlp._linears() for t in (lin.weight, lin.bias)]
+    if torch.is_grad_enabled() and any(q.requires_grad for q in params):
+        if any(t.device != x.device for t in params):
+            raise _lib.NrtError("SkipConnMLP parameters and inputs are on different devices: "
+                                "move the module to the GPU (.to(device)) to train it")
+        g = _InputGradFn.apply(mlp, flat, *params)
+    else:
+        g = _input_grad(mlp, flat)
+    return g.reshape(lead + (mlp.in_size,))
+
+
+def _input_grad(mlp, x):
+    lib = _lib.load(require_device=True)
+    M = x.shape[0]
+    g = torch.empty_like(x)
+    if M == 0:
+        return g
+    dy = torch.ones(M, mlp.out.out_features, device=x.device)
+    ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(mlp.nrt(), M), dtype=torch.uint8,
+                     device=x.device)
+    _lib.call("nrt_mlp_backward", mlp.nrt(), _lib.ptr(x), None, M, _lib.ptr(dy), _lib.ptr(g),
+              None, None, None, _lib.ptr(ws), _lib.stream())
+    return g
+
+
+class _InputGradFn(torch.autograd.Function):
+    """g = d(sum_o y_o)/dx with parameter gradients of <dL/dg, g> from nrt_mlp_grad_backward."""
+
+    @staticmethod
+    def forward(ctx, mlp, x, *params):
+        with torch.no_grad():
+            g = _input_grad(mlp, x.detach())
+        ctx.mlp = mlp
+        ctx.handle = mlp_handle(mlp)
+        ctx.save_for_backward(x)
+        return g
+
+    @staticmethod
+    def backward(ctx, dg):
+        import ctypes
+        (x,) = ctx.saved_tensors
+        mlp = ctx.mlp
+        lib = _lib.load(require_device=True)
+        M = x.shape[0]
+        dg = dg.float().contiguous()
+        lins = mlp._linears()
+        dws = [torch.empty_like(lin.weight) if lin.weight.requires_grad else None for lin in lins]
+        dbs = [torch.empty_like(lin.bias) if lin.bias.requires_grad else None for lin in lins]
+        wp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dws])
+        bp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dbs])
+        ws = torch.empty(max(lib.nrt_mlp_grad_backward_workspace_bytes(ctx.handle.value, M), 1),
+                         dtype=torch.uint8, device=x.device)
+        _lib.call("nrt_mlp_grad_backward", ctx.handle.value, _lib.ptr(x), None, M, _lib.ptr(dg),
+                  wp, bp, _lib.ptr(ws), _lib.stream())
+        grads = [g for pair in zip(dws, dbs) for g in pair]
+        return (None, None, *grads)

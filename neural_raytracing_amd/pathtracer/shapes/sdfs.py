@@ -11,6 +11,7 @@ import torch.nn.functional as F
 from ... import _lib
 from .._handles import _Handle, _cache, _host, mlp_handle
 from ..interaction import MixedInteraction
+from ..differentiable import coordinate_system, needs_grad, sdf_gradient, sdf_value
 from ..neural_blocks import SkipConnMLP
 
 
@@ -83,6 +84,10 @@ def _looks_like_sphere_sdf(m):
     return all(hasattr(m, a) for a in ("centers", "radii", "tfs", "shift"))
 
 
+def _is_sphere_sdf(m):
+    return isinstance(m, SphereSDF) or _looks_like_sphere_sdf(m)
+
+
 def sdf_eval(sdf, p):
     flat = p.reshape(-1, 3).float().contiguous()
     out = torch.empty(flat.shape[0], device=p.device)
@@ -98,6 +103,8 @@ class HipInteraction(MixedInteraction):
 
     @property
     def raw_normals(self):
+        if getattr(self, "_nrt_train", False):
+            return self._nrt_raw_train
         if not hasattr(self, "_nrt_raw"):
             return None
         hit = self._nrt_hit_mask.reshape(-1)
@@ -147,12 +154,20 @@ class SDF:
         if primary:
             dist = getattr(self, "dist", 2.2)
             scan_max_t = dist + random.random() * (2 / 128)
+        # training (sdfs.py:133-158 with autograd on): the march stays gradient-free; the scan
+        # reports its argmin so sdf(best_pos) and the normals are recomputed with gradients
+        train = needs_grad(self.sdf)
+        scan_idx = torch.empty(P, dtype=torch.int32, device=dev) if (train and primary) else None
         mp = _lib.MarchParams(int(self.max_steps), float(self.epsilon), float(max_t), int(bool(primary)),
-                              float(scan_max_t), _lib.precision_code())
+                              float(scan_max_t), _lib.precision_code(),
+                              None if scan_idx is None else scan_idx.data_ptr())
         _lib.call("nrt_sdf_intersect", h, _lib.ptr(flat), P, ctypes.byref(mp), _lib.ptr(t),
                   _lib.ptr(hit), _lib.ptr(p), _lib.ptr(n), _lib.ptr(raw), _lib.ptr(wi),
                   _lib.ptr(thr), _lib.ptr(hit_idx), _lib.ptr(hit_count), _lib.ptr(ws), _lib.stream())
         hit_b = hit.bool().reshape(lead)
+        if train:
+            return self._differentiable(flat, t, hit_b.reshape(-1), scan_idx, scan_max_t, lead,
+                                        (hit_idx, hit_count, flat)), hit_b
         throughput = thr.reshape(lead) if primary else 0
         si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead).squeeze(), obj=self,
                             throughput=throughput)
@@ -165,6 +180,37 @@ class SDF:
         si._nrt_raw = raw
         si._nrt_hit_mask = hit_b
         return si, hit_b
+
+    def _differentiable(self, flat, t, hit, scan_idx, scan_max_t, lead, hits):
+        """The parts of sdfs.py:133-158 that carry gradients, at the march's and the scan's
+        points: throughput = -1000 sdf(best_pos), raw normals (create_graph), p += 5 eps n,
+        frames and wi."""
+        o, d = flat[:, :3], flat[:, 3:]
+        p0 = o + t.unsqueeze(-1) * d
+        throughput = 0
+        if scan_idx is not None:
+            step = scan_max_t / 128
+            best = o + scan_idx.long().unsqueeze(-1) * step * d
+            throughput = (-1000 * sdf_value(self.sdf, best)).reshape(lead)
+        n = torch.zeros_like(p0)
+        p = p0
+        raw = None
+        if bool(hit.any()):
+            raw = sdf_gradient(self.sdf, p0[hit])
+            nh = F.normalize(raw, eps=1e-6, dim=-1)
+            n = n.index_put((hit,), nh)
+            p = p0.index_put((hit,), p0[hit] + nh * self.epsilon * 5)
+        frame = coordinate_system(n)
+        si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead).squeeze(), obj=self,
+                            throughput=throughput)
+        si.n = n.reshape(lead + (3,))
+        si.frame = frame.reshape(lead + (3, 3))
+        si.wi = si.to_local(-d.reshape(lead + (3,)))
+        si._nrt_hits = hits
+        si._nrt_train = True
+        si._nrt_raw_train = raw
+        si._nrt_hit_mask = hit.reshape(lead)
+        return si
 
     def intersect_test(self, rays, max_t=10, active=True):
         """sdfs.py:162-181 via nrt_sdf_occlusion."""
@@ -180,7 +226,11 @@ class SDF:
         return vis.bool().reshape(lead)
 
     def autograd_diff(self, p):
-        """Normal direction d sdf / dp (sdfs.py:184-197) from the f32 backward kernel."""
+        """Normal direction d sdf / dp (sdfs.py:184-197) from the f32 backward kernel; with
+        autograd on and trainable SDF parameters the result is differentiable
+        (create_graph=True, nrt_mlp_grad_backward)."""
+        if needs_grad(self.sdf):
+            return sdf_gradient(self.sdf, p)
         flat = p.reshape(-1, 3).float().contiguous()
         g = torch.empty_like(flat)
         _lib.call("nrt_sdf_grad", sdf_handle(self.sdf), _lib.ptr(flat), flat.shape[0], _lib.ptr(g),

@@ -45,7 +45,7 @@ def softplus(x):
     return F.softplus(x)
 
 
-ACTIVATIONS = {"leaky_relu": leaky_relu, "softplus": softplus}
+ACTIVATIONS = {"leaky_relu": leaky_relu, "softplus": softplus, "sigmoid": torch.sigmoid}
 
 
 class SkipMLP(nn.Module):
@@ -153,7 +153,11 @@ class SphereBlobSDF(nn.Module):
 class MarchedSDF:
     """Restatement of ``SDF`` (sdfs.py:89-277): sphere tracing, coarse scan, normals."""
 
-    def __init__(self, sdf=unit_sphere_sdf, epsilon=1e-3, max_steps=32, dist=2.2):
+    def __init__(self, sdf=unit_sphere_sdf, epsilon=1e-3, max_steps=32, dist=2.2,
+                 create_graph=False):
+        # create_graph=True keeps the normals differentiable, as the reference's autograd_diff
+        # does (sdfs.py:184-197) -- used by the training-gradient tests
+        self.create_graph = create_graph
         self.sdf = sdf
         self.epsilon = epsilon
         self.max_steps = max_steps
@@ -199,7 +203,8 @@ class MarchedSDF:
         with torch.enable_grad():
             p = p.detach().requires_grad_()
             out = self.sdf(p)
-            (g,) = torch.autograd.grad(out, p, torch.ones_like(out), create_graph=False)
+            (g,) = torch.autograd.grad(out, p, torch.ones_like(out),
+                                       create_graph=self.create_graph)
         return g
 
     def intersect(self, rays, max_t=10, active=True, primary=True, jitter=None):
@@ -314,8 +319,8 @@ def rusinkiewicz(wo, wi):
     """
     wo = F.normalize(wo, dim=-1)
     wi = F.normalize(wi, dim=-1)
-    ey = torch.tensor([0, 1, 0], dtype=torch.float).expand_as(wo)
-    ez = torch.tensor([0, 0, 1], dtype=torch.float).expand_as(wo)
+    ey = torch.tensor([0, 1, 0], dtype=wo.dtype).expand_as(wo)
+    ez = torch.tensor([0, 0, 1], dtype=wo.dtype).expand_as(wo)
     h = F.normalize(wo + wi, dim=-1)
     cos_th = h[..., 2]
     r = nonzero_eps(h[..., 1]).hypot(nonzero_eps(h[..., 0])).clamp(min=1e-6)

@@ -16,6 +16,11 @@ SHAPES = {
                                      activation="softplus"),
     "nerfle_second_70in": dict(num_layers=8, hidden_size=64, in_size=70, out=3, freqs=16),
     "latent_4x32": dict(num_layers=4, hidden_size=32, in_size=3, out=4, freqs=8, latent_size=8),
+    # the shading MLPs of the bench scene (bsdfs.py:487-496, 613-624; lights.py:160-163)
+    "neural_bsdf_6x96_F64": dict(num_layers=6, hidden_size=96, in_size=3, out=3, freqs=64),
+    "sp_var_16x256_F128": dict(num_layers=16, hidden_size=256, in_size=3, out=8, freqs=128,
+                               sigma=128, xavier_init=True),
+    "light_field_10x256": dict(num_layers=10, hidden_size=256, in_size=3, out=3, freqs=16),
 }
 
 

@@ -1,0 +1,259 @@
+"""Training through the fused render path: gradients of a loss on
+``pathtrace_sample`` -- throughput = -1000 sdf(best_pos), the create_graph SDF normals
+(``nrt_mlp_grad_backward``), the shading MLPs -- against torch autograd of the oracle.
+
+Tolerances are written per test: the double backward is compared with float64 autograd of the
+oracle's SkipMLP (as tests/test_gpu_train.py does for the first backward); whole-render
+gradients are FP32 on both sides with different batch-reduction orders, so they are compared at
+2e-3 of each tensor's largest entry (plus 1e-6 absolute)."""
+import copy
+import random
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import pathtracer_ref as R
+from tests.helpers import copy_mlp, seeded
+
+SHAPES = {
+    "sdf_8x256_softplus_F16": dict(num_layers=8, hidden_size=256, in_size=3, out=1, freqs=16,
+                                   activation="softplus"),
+    "shift_8x128_softplus_F32": dict(num_layers=8, hidden_size=128, in_size=3, out=1, freqs=32,
+                                     activation="softplus"),
+    "8x64_leaky_out3": dict(num_layers=8, hidden_size=64, in_size=3, out=3, freqs=16),
+    "sigmoid_4x32": dict(num_layers=4, hidden_size=32, in_size=3, out=1, freqs=8,
+                         activation="sigmoid"),
+}
+
+
+def _pair(kw, seed):
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    seeded(seed)
+    act = kw.get("activation", "leaky_relu")
+    ref = R.SkipMLP(**kw)
+    pkw = {k: v for k, v in kw.items() if k != "activation"}
+    if act != "leaky_relu":
+        pkw["activation"] = {"softplus": F.softplus, "sigmoid": torch.sigmoid}[act]
+    mine = SkipConnMLP(device="cpu", **pkw)
+    copy_mlp(mine, ref)
+    return ref, mine.cuda()
+
+
+def _double_backward(ref, x, v, dtype):
+    m = copy.deepcopy(ref).to(dtype)
+    m.basis_p = ref.basis_p.to(dtype)
+    xr = x.detach().clone().to(dtype).requires_grad_(True)
+    y = m(xr)
+    (g,) = torch.autograd.grad(y, xr, torch.ones_like(y), create_graph=True)
+    (g * v.to(dtype)).sum().backward()
+    out = {"g": g.detach()}
+    for i, lin in enumerate([m.init, *m.layers, m.out]):
+        out[f"dW[{i}]"] = lin.weight.grad if lin.weight.grad is not None else torch.zeros_like(lin.weight)
+        out[f"db[{i}]"] = lin.bias.grad if lin.bias.grad is not None else torch.zeros_like(lin.bias)
+    return out
+
+
+def _close(got, want, ref32, what, rel=1e-4):
+    scale = max(1.0, want.abs().max().item())
+    err = (got.detach().cpu().double() - want.double()).abs().max().item()
+    e32 = (ref32.detach().double() - want.double()).abs().max().item()
+    tol = max(rel * scale, 4 * e32)
+    assert err <= tol, f"{what}: max|diff| {err:.3g} > {tol:.3g} (scale {scale:.3g}, fp32 ref {e32:.3g})"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 45, 700])
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_mlp_grad_backward_matches_autograd(name, M):
+    """d/dtheta of sum(v . d(sum y)/dx): nrt_mlp_grad_backward vs float64 double backward."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import input_gradient
+    kw = SHAPES[name]
+    ref, mine = _pair(kw, 70 + M)
+    # the zero / default init leaves the deep layers' second-order terms tiny: widen the weights
+    with torch.no_grad():
+        for a in [ref.init, *ref.layers, ref.out]:
+            a.weight.mul_(1.5)
+    copy_mlp(mine, ref)
+    set_precision("fp32")
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, 3, generator=g) - 0.5)
+    v = torch.randn(M, 3, generator=g)
+    want = _double_backward(ref, x, v, torch.float64)
+    ref32 = _double_backward(ref, x, v, torch.float32)
+    gm = input_gradient(mine, x.cuda())
+    (gm * v.cuda()).sum().backward()
+    got = {"g": gm}
+    for i, a in enumerate(mine._linears()):
+        got[f"dW[{i}]"] = a.weight.grad
+        got[f"db[{i}]"] = a.bias.grad
+    for k in want:
+        _close(got[k], want[k], ref32[k], k)
+
+
+@pytest.mark.gpu
+def test_mlp_grad_backward_empty_and_refusals():
+    from neural_raytracing_amd import NrtError
+    from neural_raytracing_amd.pathtracer.neural_blocks import input_gradient
+    ref, mine = _pair(SHAPES["8x64_leaky_out3"], 1)
+    g = input_gradient(mine, torch.empty(0, 3, device="cuda"))
+    assert g.shape == (0, 3)
+    g.sum().backward()
+    assert all(float(p.grad.abs().max()) == 0 for p in mine.parameters())
+    with pytest.raises(NrtError):
+        input_gradient(mine, torch.rand(4, 3, device="cuda", requires_grad=True))
+
+
+def _perturbed_scene(smooth=False):
+    """The BASELINE.md §2 scene with a non-zero SphereSDF shift MLP (the recorded scene's shift is
+    zero-initialised, which would leave the double-backward terms zero).
+
+    ``smooth=True`` switches the leaky-ReLU shading MLPs (NeuralBSDFs, spatial weights,
+    LightField) to softplus on both sides: leaky_relu's kink makes per-element gradients
+    discontinuous -- this crop has a NeuralBSDF pre-activation at |z| = 3.4e-7, within FP32
+    rounding of 0, whose derivative flips between 1 and 0.01 between any two FP32
+    implementations (measured: the oracle's own FP32 run is 1.3 % off its float64 run there)."""
+    import tests.test_gpu_parity as P
+    ref, mine = P._scene_pair()
+    if smooth:
+        pairs = [(ref["bsdf"].sp_var_fn, mine["bsdf"].sp_var_fn),
+                 (ref["lights"].light_field_approx, mine["lights"].light_field_approx)]
+        pairs += [(a.mlp, b.mlp) for a, b in zip(ref["bsdf"].bsdfs, mine["bsdf"].bsdfs)]
+        for a, b in pairs:
+            a.act_name = "softplus"
+            b.activation = F.softplus
+    seeded(21)
+    with torch.no_grad():
+        sh = ref["shape"].sdf.shift
+        for a in [sh.init, *sh.layers]:
+            a.weight.normal_(0.0, 0.02)
+            a.bias.zero_()
+        sh.out.weight.normal_(0.0, 0.002)  # |shift| ~ 0.02: every ray of the crop still hits
+        sh.out.bias.zero_()
+    copy_mlp(mine["shape"].sdf.shift, sh)
+    ref["shape"].create_graph = True
+    return ref, mine
+
+
+def _named_params(scene, oracle):
+    out = {}
+    sdf = scene["shape"].sdf
+    out["centers"], out["radii"], out["tfs"] = sdf.centers, sdf.radii, sdf.tfs
+    sh = sdf.shift
+    lins = [sh.init, *sh.layers, sh.out]
+    for i, a in enumerate(lins):
+        out[f"shift.W{i}"], out[f"shift.b{i}"] = a.weight, a.bias
+    sp = scene["bsdf"].sp_var_fn
+    for i, a in enumerate([sp.init, *sp.layers, sp.out]):
+        out[f"sp.W{i}"], out[f"sp.b{i}"] = a.weight, a.bias
+    for j, b in enumerate(scene["bsdf"].bsdfs):
+        for i, a in enumerate([b.mlp.init, *b.mlp.layers, b.mlp.out]):
+            out[f"bsdf{j}.W{i}"], out[f"bsdf{j}.b{i}"] = a.weight, a.bias
+    lf = scene["lights"].light_field_approx
+    for i, a in enumerate([lf.init, *lf.layers, lf.out]):
+        out[f"light.W{i}"], out[f"light.b{i}"] = a.weight, a.bias
+    out["light.color"] = scene["lights"].color
+    return out
+
+
+def _oracle_render_grads(ref, dtype, w, crop):
+    """Oracle render of the crop + loss <img, w> + 0.1 eikonal(raw normals) in ``dtype``;
+    returns the image, the hit-point normals and every parameter's gradient."""
+    r = {k: copy.deepcopy(v) for k, v in ref.items()}
+    for m in (r["shape"].sdf, r["bsdf"], r["lights"]):
+        m.to(dtype)
+        for sub in m.modules():
+            if hasattr(sub, "basis_p"):
+                sub.basis_p = sub.basis_p.to(dtype)
+    r["camera"].cam_to_world = r["camera"].cam_to_world.to(dtype)
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        random.seed(11)
+        img = R.render(r["shape"], r["lights"], r["camera"], r["integrator"], r["bsdf"],
+                       size=256, chunk_size=256, background=0.0, with_noise=0.0,
+                       crop=(crop[0], crop[1], crop[2]))
+        # the interaction record is internal to DirectRef: recompute its normals the same way
+        rays = r["camera"].sample_positions(R._tile_positions(*crop), 256, 0.0)
+        o, d = rays.split(3, dim=-1)
+        t, hit = r["shape"].march(o, d)
+        raw = r["shape"].gradient((o + t * d)[hit])
+        loss = (img * w.to(dtype)).sum() + 0.1 * (raw.norm(dim=-1) - 1).square().mean()
+        loss.backward()
+    finally:
+        torch.set_default_dtype(old)
+    grads = {k: (a.grad if a.grad is not None else torch.zeros_like(a)).detach().double()
+             for k, a in _named_params(r, True).items()}
+    return img.detach(), raw.detach(), grads
+
+
+@pytest.mark.gpu
+def test_pathtrace_sample_gradients_match_oracle():
+    """loss = <img, w> + 0.1 eikonal(raw_normals) on a 32x32 crop: every parameter's gradient
+    (SphereSDF spheres and shift MLP through throughput and the create_graph normals, the
+    spatial-weights MLP, 8 NeuralBSDFs, the LightField).  Bar per tensor:
+    max|HIP - f64| <= max(2e-3 * max|f64|, 4 * max|oracle f32 - f64|) -- the deep shading MLPs'
+    FP32 gradients carry ~1 % rounding noise whichever implementation computes them."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    ref, mine = _perturbed_scene(smooth=True)
+    crop = (112, 112, 32)
+    w = torch.randn(32, 32, 4, generator=torch.Generator().manual_seed(5))
+    img64, raw64, want = _oracle_render_grads(ref, torch.float64, w, crop)
+    img32, _, ref32 = _oracle_render_grads(ref, torch.float32, w, crop)
+    random.seed(11)
+    captured = {}
+    img, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"],
+                                 mine["integrator"], bsdf=mine["bsdf"], size=256, chunk_size=256,
+                                 bundle_size=1, crop_size=32, uv=crop[:2], background=0,
+                                 with_noise=0.0, device="cuda",
+                                 addition=lambda it: captured.setdefault("raw", it.raw_normals))
+    assert img.requires_grad
+    diff = (img.detach().cpu() - img32).abs().max().item()
+    assert diff <= 1e-4, f"forward differs from the FP32 oracle by {diff}"
+    raw = captured["raw"]
+    assert raw is not None and raw.requires_grad and raw.shape == raw64.shape
+    loss = (img * w.cuda()).sum() + 0.1 * (raw.norm(dim=-1) - 1).square().mean()
+    loss.backward()
+    got = _named_params(mine, False)
+    bad = []
+    for k, g64 in want.items():
+        gb = got[k].grad
+        gb = torch.zeros_like(g64) if gb is None else gb.detach().cpu().double()
+        scale = g64.abs().max().item()
+        err = (gb - g64).abs().max().item()
+        e32 = (ref32[k] - g64).abs().max().item()
+        if err > max(2e-3 * scale, 4 * e32) + 1e-9:
+            bad.append(f"{k}: err {err:.3g} scale {scale:.3g} fp32-oracle err {e32:.3g}")
+    assert not bad, "\n".join(bad)
+    assert want["shift.W0"].abs().max() > 0  # the double-backward terms are exercised
+
+
+@pytest.mark.gpu
+def test_training_steps_reduce_render_loss():
+    """A few Adam steps of the full scene through pathtrace_sample lower an image loss."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    _, mine = _perturbed_scene()
+    target = torch.zeros(32, 32, 4, device="cuda")
+    target[..., :3] = 0.5
+    target[..., 3] = 1.0
+    params = [*mine["shape"].sdf.parameters(), *mine["bsdf"].parameters(),
+              *mine["lights"].parameters()]
+    opt = torch.optim.Adam(params, lr=1e-3)
+    losses = []
+    for step in range(8):
+        random.seed(step)
+        opt.zero_grad()
+        img, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"],
+                                     mine["integrator"], bsdf=mine["bsdf"], size=256,
+                                     chunk_size=256, bundle_size=1, crop_size=32, uv=(112, 112),
+                                     background=0, with_noise=0.0, device="cuda")
+        loss = F.mse_loss(img, target)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < losses[0], losses

@@ -1,0 +1,81 @@
+"""CPU checks of the element-wise glue the training path differentiates through
+(neural_raytracing_amd/pathtracer/differentiable.py) against the oracle's restatement:
+values and autograd gradients agree to float32 rounding (atol 1e-6 on unit-scale inputs)."""
+import torch
+
+from oracle import pathtracer_ref as R
+from tests.helpers import seeded
+
+
+def test_coordinate_system_matches_oracle_frames():
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    seeded(1)
+    n = torch.randn(500, 3)
+    n[0] = torch.tensor([0.0, 0.0, -1.0])  # the s_z clamp branch
+    n[1] = torch.tensor([0.0, 0.0, 1.0])
+    a = n.clone().requires_grad_(True)
+    b = n.clone().requires_grad_(True)
+    fa, fb = D.coordinate_system(a), R.shading_frame(b)
+    assert torch.allclose(fa, fb, atol=1e-6)
+    w = torch.randn_like(fa)
+    (fa * w).sum().backward()
+    (fb * w).sum().backward()
+    assert torch.allclose(a.grad, b.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_param_rusin2_matches_oracle():
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    seeded(2)
+    wo = torch.nn.functional.normalize(torch.randn(400, 3), dim=-1)
+    wi = torch.nn.functional.normalize(torch.randn(400, 3), dim=-1)
+    wi[0] = wo[0] = torch.tensor([0.0, 0.0, 1.0])  # SURVEY §8c KAT 6
+    a, b = wo.clone().requires_grad_(True), wo.clone().requires_grad_(True)
+    ra, rb = D.param_rusin2(a, wi), R.rusinkiewicz(b, wi)
+    assert torch.allclose(ra, rb, atol=1e-6)
+    ra.sum().backward()
+    rb.sum().backward()
+    assert torch.allclose(a.grad, b.grad, atol=1e-4, rtol=1e-4)
+
+
+def test_fresnel_and_reflect_match_oracle():
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    c = torch.linspace(-1, 1, 101)
+    assert torch.allclose(D.fresnel_conductor(c, 1.3, 0.0), R.fresnel_conductor(c, 1.3, 0.0),
+                          atol=1e-7)
+
+
+def test_sphere_part_and_gradient_match_oracle():
+    """SphereSDF's smooth-min part: values, d/dp with create_graph, and the parameter gradients
+    of an eikonal-style loss on that normal."""
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    from neural_raytracing_amd.pathtracer.shapes import SphereSDF
+    seeded(3)
+    ref = R.SphereBlobSDF(n=16)
+    seeded(3)
+    mine = SphereSDF(n=16, device="cpu")
+    assert torch.equal(mine.centers, ref.centers)
+    with torch.no_grad():
+        for t in (ref.tfs, mine.tfs):
+            t.copy_(0.05 * torch.sin(torch.arange(t.numel(), dtype=torch.float)).reshape(t.shape))
+    p = torch.randn(64, 3) * 0.3
+    assert torch.allclose(D.sphere_part(mine, p), ref.spheres(p), atol=1e-6)
+    for m, fn in ((mine, lambda q: D.sphere_part(mine, q)), (ref, ref.spheres)):
+        q = p.clone().requires_grad_(True)
+        out = fn(q)
+        (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+        (g.norm(dim=-1) - 1).square().mean().backward()
+    for a, b in ((mine.centers, ref.centers), (mine.radii, ref.radii), (mine.tfs, ref.tfs)):
+        assert torch.allclose(a.grad, b.grad, atol=1e-5, rtol=1e-4)
+
+
+def test_needs_grad_follows_autograd_mode():
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    from neural_raytracing_amd.pathtracer.shapes import SPHERE_SDF, SDF, SphereSDF
+    s = SphereSDF(n=4, device="cpu")
+    assert D.needs_grad(s)
+    assert not D.needs_grad(SDF(sdf=SPHERE_SDF, device="cpu"))  # no parameters
+    with torch.no_grad():
+        assert not D.needs_grad(s)
+    for q in s.parameters():
+        q.requires_grad_(False)
+    assert not D.needs_grad(s)
