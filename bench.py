@@ -50,10 +50,18 @@ def parse():
     ap.add_argument("--cpu-crop", type=int, default=128, help="side of the CPU-baseline crop")
     ap.add_argument("--no-fp32-check", action="store_true")
     ap.add_argument("--scene", default="nerf_synthetic",
-                    choices=["nerf_synthetic", "colocate", "dtu", "nerfle"],
+                    choices=["nerf_synthetic", "colocate", "dtu", "nerfle", "train"],
                     help="nerf_synthetic = the BASELINE metric (default); the others are "
                          "BASELINE.json configs[2..4] as one-GPU workloads")
+    ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
+    ap.add_argument("--crop", type=int, default=80, help="--scene train: crop side")
     args = ap.parse_args()
+    if args.scene == "train":
+        if args.size is None:
+            args.size = 256
+        if args.samples is None:
+            args.samples = 64
+        return args
     big = args.scene == "nerfle"
     if args.size is None:
         args.size = 1600 if big else 800
@@ -139,6 +147,8 @@ def _copy_to_oracle(dst, src):
 
 def main():
     args = parse()
+    if args.scene == "train":
+        return bench_train(args)
     if args.scene != "nerf_synthetic":
         return bench_other(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -418,6 +428,99 @@ def bench_other(args):
                      "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "flop_per_step": flop / args.steps,
                      "kernel_ms_per_step": k_ms / args.steps, "launches": k_n},
+    }
+    print(json.dumps(line), flush=True)
+
+
+def bench_train(args):
+    """One-GPU training-step line: the nerf_synthetic training iteration of
+    training_utils.py:246-285 / scripts/nerf_synthetic.py:61-116 -- N=6 views, an 80x80 crop of
+    a 256^2 frame, SDF(SphereSDF(n=128), max_steps=64), 8 NeuralBSDF(Softplus) +
+    ComposeSpatialVarying, LightField, NeRFIntegrator(Direct); loss = MSE + eikonal(raw_normals);
+    backward through the fused path; AdamW with the script's three learning rates.  FP32."""
+    from neural_raytracing_amd import _lib
+    import neural_raytracing_amd as nra
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, NeuralBSDF
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.lights import LightField
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--scene train runs on one GPU")
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    _lib.load(require_device=True)
+    nra.set_precision("fp32")
+    torch.manual_seed(0)
+    random.seed(0)
+    sdf = SphereSDF(n=128, device="cpu")
+    with torch.no_grad():  # a non-trivial residual (the scripts load a trained one)
+        for a in [sdf.shift.init, *sdf.shift.layers]:
+            a.weight.normal_(0.0, 0.02)
+        sdf.shift.out.weight.normal_(0.0, 0.002)
+    shape = SDF(sdf=sdf.to(device), device=device, max_steps=args.samples)
+    bsdf = ComposeSpatialVarying([NeuralBSDF(activation=torch.nn.Softplus(), device="cpu")
+                                  for _ in range(8)], device="cpu")
+    for b in bsdf.bsdfs:
+        b.mlp.to(device)
+    bsdf.sp_var_fn.to(device)
+    lights = LightField(device="cpu").to(device)
+    integrator = NeRFIntegrator(Direct())
+    opt = torch.optim.AdamW([
+        {"params": list(shape.parameters()), "lr": 8e-5},
+        {"params": list(bsdf.parameters()), "lr": 8e-4},
+        {"params": list(lights.parameters()), "lr": 8e-5},
+    ], lr=8e-5, weight_decay=0)
+    size, crop, N = args.size, args.crop, args.views
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    c2w = torch.stack([view_c2w(i, N) for i in range(N)]).to(device)
+    cameras = pt.cameras.NeRFCamera(cam_to_world=c2w, focal=focal, device=device)
+    g = torch.Generator().manual_seed(1)
+    target = torch.rand(N, crop, crop, 3, generator=g).to(device)
+
+    def step(i):
+        random.seed(i)
+        opt.zero_grad()
+        uv = ((37 * i) % (size - crop), (53 * i) % (size - crop))
+        got, mi = pt.pathtrace_sample(shape, lights, cameras, integrator, bsdf=bsdf, size=size,
+                                      chunk_size=size, bundle_size=1, crop_size=crop, uv=uv,
+                                      background=0, addition=lambda m: m, squeeze_first=False,
+                                      device=device)
+        loss = F.mse_loss(got[..., :3], target)
+        raw = getattr(mi, "raw_normals", None)
+        if raw is not None:
+            loss = loss + (raw.norm(dim=-1) - 1).square().mean()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(args.warmup + i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    kms = {k: _lib.profile_read(k)[0] / args.steps
+           for k in ("k_intersect", "k_mlp_backward32", "k_mlp_grad_backward32")}
+    rays = N * crop * crop
+    line = {
+        "metric": f"training ray-samples/sec/GPU (nerf_synthetic step, {N}x{crop}x{crop} crop "
+                  f"of {size}^2, {args.samples} march steps)",
+        "value": rays * args.samples * args.steps / elapsed, "unit": "ray-samples/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded random-init weights, random target crops)",
+        "config": {"workload": "forward (fused march + scan) + backward (MLP backward, SDF-normal "
+                               "double backward, shading autograd) + AdamW",
+                   "views": N, "crop": crop, "image": [size, size],
+                   "samples_per_ray": args.samples},
+        "kernel_ms_per_step": kms, "final_loss": float(loss),
     }
     print(json.dumps(line), flush=True)
 

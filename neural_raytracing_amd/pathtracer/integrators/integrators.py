@@ -197,6 +197,9 @@ class Path(Integrator):
         lights = kwargs.get("lights", self.lights)
         shadow, occ = _emitter_mode(kwargs.get("w_isect", False))
         uniforms = kwargs.get("uniforms")
+        if needs_grad(shapes, bsdf, lights):
+            raise _lib.NrtError("Path is not on the HIP training path: render it under "
+                                "torch.no_grad()")
         dev = rays.device
         lead = rays.shape[:-1]
         it, active = shapes.intersect(rays, primary=self.training)

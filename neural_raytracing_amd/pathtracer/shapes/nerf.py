@@ -4,9 +4,11 @@ reference's compositing on the GPU.  Constructor and RNG consumption follow nerf
 import random
 
 import torch
+import torch.nn.functional as F
 import torch.nn as nn
 
 from ... import _lib
+from ..differentiable import needs_grad
 from ..neural_blocks import SkipConnMLP
 
 
@@ -42,6 +44,11 @@ class NeRFLE(nn.Module):
         dev = flat.device
         # torch.linspace on the host: the same float32 sequence the CPU reference computes
         ts = torch.linspace(0, 2 + random.random() * 0.1, self.steps).to(dev)
+        if needs_grad(self):
+            if getattr(self, "envmap", False):
+                raise _lib.NrtError("NeRFLE(envmap=True) is not on the HIP training path")
+            light = lights.location.reshape(-1, 3)[0].detach().float().to(dev)
+            return self._forward_train(flat, ts, light).reshape(lead + (3,))
         lib = _lib.load(require_device=True)
         if getattr(self, "envmap", False):
             handle = getattr(lights, "nrt", None)
@@ -64,3 +71,23 @@ class NeRFLE(nn.Module):
                       _lib.ptr(rgb[r0:r0 + n]),
                       _lib.ptr(ws), _lib.precision_code(), _lib.stream())
         return rgb.reshape(lead + (3,))
+
+    def _forward_train(self, flat, ts, light):
+        """nerf.py:175-214 with autograd: both MLPs on the HIP MLP kernels
+        with nrt_mlp_backward behind them; the sample points and the rolled-cumprod compositing
+        are tensor ops in the reference's order.  FP32 intermediates [S, P, 65 / 70]."""
+        o, d = flat[:, :3], flat[:, 3:]
+        pts = o.unsqueeze(0) + torch.tensordot(ts, d, dims=0)
+        first = self.first(pts)
+        latent = first[..., 1:]
+        alpha = first[..., 0, None]
+        light_enc = light.reshape(1, 1, 3).expand(latent.shape[:-1] + (3,))
+        rgb = self.second(torch.cat([latent, d[None].expand(latent.shape[:-1] + (3,)), light_enc],
+                                    dim=-1)).sigmoid()
+        sigma = F.relu(alpha).squeeze(-1)
+        alpha = 1 - torch.exp(-sigma * ts[:, None].expand_as(sigma))
+        cp = torch.cumprod((1 - alpha).clamp(min=1e-10), dim=0)
+        cp = torch.roll(cp, 1, 0)
+        cp[-1, ...] = 1
+        w = alpha * cp
+        return (w[..., None] * rgb).sum(dim=0)

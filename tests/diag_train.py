@@ -1,4 +1,4 @@
-"""Diagnostic (test infrastructure): per-stage differences between the HIP training path and the
+"""Diagnostic script, not collected by pytest (test infrastructure): per-stage differences between the HIP training path and the
 oracle on the perturbed BASELINE scene crop.  Writes gpurun_out/diag_train.txt."""
 import random
 import sys

@@ -257,3 +257,81 @@ def test_training_steps_reduce_render_loss():
         opt.step()
         losses.append(loss.item())
     assert losses[-1] < losses[0], losses
+
+
+def _nerfle_grads(ref, rays, loc, w, dtype, jitter):
+    r = copy.deepcopy(ref).to(dtype)
+    for sub in r.modules():
+        if hasattr(sub, "basis_p"):
+            sub.basis_p = sub.basis_p.to(dtype)
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        out = r(rays.to(dtype), loc.to(dtype), jitter=jitter)
+        (out * w.to(dtype)).sum().backward()
+    finally:
+        torch.set_default_dtype(old)
+    lins = {"first": r.first, "second": r.second}
+    return out.detach(), {f"{n}.{k}{i}": getattr(a, "weight" if k == "W" else "bias").grad.double()
+                          for n, m in lins.items()
+                          for i, a in enumerate([m.init, *m.layers, m.out]) for k in ("W", "b")}
+
+
+@pytest.mark.gpu
+def test_nerfle_training_gradients_match_oracle():
+    """NeRFLE (nerf.py:175-214) with autograd: both MLPs' gradients of <rgb, w> against float64
+    autograd of the oracle (softplus MLPs, so the gradients are smooth in the weights; same
+    bar as the render test)."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from tests.test_gpu_parity import _nerfle_pair
+    ref, mine = _nerfle_pair()
+    for m in (ref.first, ref.second):
+        m.act_name = "softplus"
+    for m in (mine.first, mine.second):
+        m.activation = F.softplus
+    g = torch.Generator().manual_seed(8)
+    o = torch.tensor([0.0, 0.2, 1.2]) + 0.1 * torch.randn(1, 9, 7, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, 9, 7, 1, 2, generator=g) - 0.5,
+                               -torch.ones(1, 9, 7, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    loc = torch.tensor([[0.3, 1.0, 0.2]])
+    w = torch.randn(1, 9, 7, 1, 3, generator=g)
+    random.seed(6)
+    jitter = random.random()
+    want_img, want = _nerfle_grads(ref, rays, loc, w, torch.float64, jitter)
+    _, ref32 = _nerfle_grads(ref, rays, loc, w, torch.float32, jitter)
+    set_precision("fp32")
+    lights = PointLights(location=loc.cuda(), device="cuda")
+    random.seed(6)
+    got_img = mine(rays.cuda(), lights)
+    assert got_img.requires_grad
+    assert (got_img.detach().cpu().double() - want_img).abs().max().item() <= 1e-4
+    (got_img * w.cuda()).sum().backward()
+    got = {f"{n}.{k}{i}": getattr(a, "weight" if k == "W" else "bias").grad
+           for n, m in {"first": mine.first, "second": mine.second}.items()
+           for i, a in enumerate(m._linears()) for k in ("W", "b")}
+    bad = []
+    for k, g64 in want.items():
+        err = (got[k].detach().cpu().double() - g64).abs().max().item()
+        e32 = (ref32[k] - g64).abs().max().item()
+        if err > max(2e-3 * g64.abs().max().item(), 4 * e32) + 1e-9:
+            bad.append(f"{k}: err {err:.3g} scale {g64.abs().max().item():.3g} fp32 {e32:.3g}")
+    assert not bad, "\n".join(bad)
+
+
+@pytest.mark.gpu
+def test_path_and_envmap_refuse_autograd():
+    """Integrators without a HIP training path fail loudly instead of dropping gradients."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import NrtError
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.shapes import NeRFLE
+    _, mine = _perturbed_scene()
+    rays = mine["camera"].rays_tile(120, 120, 4, 4, 256)
+    with pytest.raises(NrtError):
+        Path().sample(mine["shape"], rays, mine["bsdf"], lights=mine["lights"])
+    nerf = NeRFLE(envmap=True, device="cuda")
+    with pytest.raises(NrtError):
+        nerf(rays, PointLights(device="cuda"))
