@@ -352,8 +352,11 @@ __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
 namespace {
 size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+constexpr int kBiasChunks = 256;  // bias-gradient partial sums (k_colsum_*)
+constexpr int kBiasMaxR = 256;
+
 struct TrainWs {
-  float *Z, *A, *dZ, *Eraw, *Eact, *part;
+  float *Z, *A, *dZ, *Eraw, *Eact, *part, *kpart;
 };
 
 TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
@@ -367,7 +370,8 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   w.dZ = (float*)p; p += a256(lay);
   w.Eraw = (float*)p; p += a256(enc);
   w.Eact = (float*)p; p += a256(enc);
-  w.part = (float*)p;
+  w.part = (float*)p; p += a256((size_t)kBiasChunks * kBiasMaxR * 4);
+  w.kpart = (float*)p;
   return w;
 }
 
@@ -384,21 +388,72 @@ int blas_fail(rocblas_status s, const char* what) {
   return NRT_EHIP;
 }
 
+// Split-K weight gradients.  dW = dZ^T In has a tiny output (R x C <= 256 x 550) and a huge
+// K (the batch, ~10^4-10^5): one sgemm covers a handful of output tiles, i.e. a handful of CUs.
+// The batch is cut into S equal chunks (one strided-batched sgemm, S x the tiles) plus a
+// remainder, and the partial products are summed in chunk order (deterministic).
+constexpr int kSplitMax = 64;
+constexpr int64_t kSplitRows = 1024;  // rows per chunk at least
+
+size_t split_part_floats(const MlpDev& d) {
+  const size_t rc = (size_t)std::max(d.hidden, d.out) * (size_t)(d.hidden + d.dp);
+  return (size_t)(kSplitMax + 1) * rc;
+}
+
+struct GemmCtx {
+  rocblas_handle hb;
+  float* part;  // split_part_floats(d) floats
+  hipStream_t st;
+};
+
+// dW[r][c0 + c] = sum_{s < slots} part[s][r][c]
+template <int = 0>
+__global__ void k_split_reduce(const float* __restrict__ part, int slots, int R, int C,
+                               float* __restrict__ dW, int ldw, int c0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t n = (int64_t)R * C;
+  if (i >= n) return;
+  float acc = 0.f;
+  for (int k = 0; k < slots; ++k) acc += part[(int64_t)k * n + i];
+  const int r = (int)(i / C), c = (int)(i % C);
+  dW[(int64_t)r * ldw + c0 + c] = acc;
+}
+
 // row-major dW[R][ldw] (columns c0 .. c0+C) = dZ[M][R]^T @ In[M][C]
-int grad_gemm(rocblas_handle hb, const float* dZ, int R, const float* In, int C, int64_t M,
+int grad_gemm(const GemmCtx& g, const float* dZ, int R, const float* In, int C, int64_t M,
               float* dW, int ldw, int c0) {
   const float one = 1.f, zero = 0.f;
-  // column-major view: dW^T (C x R, ld ldw) = In^T (C x M, ld C) * dZ (M x R = (R x M, ld R)^T)
-  rocblas_status s = rocblas_sgemm(hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
-                                   (rocblas_int)M, &one, In, C, dZ, R, &zero, dW + c0, ldw);
-  return s == rocblas_status_success ? NRT_OK : blas_fail(s, "rocblas_sgemm");
+  const int S = (int)std::min<int64_t>(kSplitMax, M / kSplitRows);
+  rocblas_status s;
+  if (S <= 1) {
+    // column-major view: dW^T (C x R, ld ldw) = In^T (C x M, ld C) * dZ (M x R = (R x M, ld R)^T)
+    s = rocblas_sgemm(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
+                      (rocblas_int)M, &one, In, C, dZ, R, &zero, dW + c0, ldw);
+    return s == rocblas_status_success ? NRT_OK : blas_fail(s, "rocblas_sgemm");
+  }
+  const int64_t Mc = M / S, rem = M - (int64_t)S * Mc;
+  const rocblas_stride pc = (rocblas_stride)R * C;
+  s = rocblas_sgemm_strided_batched(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
+                                    (rocblas_int)Mc, &one, In, C, (rocblas_stride)(Mc * C), dZ, R,
+                                    (rocblas_stride)(Mc * R), &zero, g.part, C, pc, S);
+  if (s != rocblas_status_success) return blas_fail(s, "rocblas_sgemm_strided_batched");
+  int slots = S;
+  if (rem > 0) {
+    s = rocblas_sgemm(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
+                      (rocblas_int)rem, &one, In + S * Mc * C, C, dZ + S * Mc * R, R, &zero,
+                      g.part + (size_t)S * pc, C);
+    if (s != rocblas_status_success) return blas_fail(s, "rocblas_sgemm");
+    ++slots;
+  }
+  const int64_t n = (int64_t)R * C;
+  k_split_reduce<><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g.st>>>(g.part, slots, R, C,
+                                                                            dW, ldw, c0);
+  return check_launch("k_split_reduce");
 }
 
 // db[r] = sum_m dZ[m][r] (row-major dZ [M][R]) in a fixed order: per chunk of rows a partial
 // column sum (4 row groups x 64 consecutive columns per block, coalesced), then the partials in
 // chunk order.  Replaces a rocBLAS gemv that took ~0.3 ms per bias at M = 38k.
-constexpr int kBiasChunks = 256;
-constexpr int kBiasMaxR = 256;
 
 template <int = 0>
 __global__ void __launch_bounds__(256) k_colsum_partial(const float* __restrict__ dZ, int R,
@@ -449,7 +504,8 @@ size_t nrt_mlp_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
   const MlpDev& d = m->host_dev;
   const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
   const size_t enc = (size_t)M * d.dp * 4;
-  return 3 * a256(lay) + 2 * a256(enc) + a256((size_t)kBiasChunks * kBiasMaxR * 4);
+  return 3 * a256(lay) + 2 * a256(enc) + a256((size_t)kBiasChunks * kBiasMaxR * 4) +
+         a256(split_part_floats(d) * 4);
 }
 
 int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int64_t M,
@@ -494,6 +550,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   if (!hb) { set_error("nrt_mlp_backward: rocblas_create_handle failed"); return NRT_EHIP; }
   rocblas_status s = rocblas_set_stream(hb, st);
   if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
+  const GemmCtx gc{hb, w.kpart, st};
   const size_t lay = (size_t)M * H;
   for (int l = 0; l <= L + 1; ++l) {
     const bool outl = l == L + 1;
@@ -501,13 +558,13 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     const float* dZ = outl ? dy : w.dZ + (size_t)l * lay;
     if (dweights && dweights[l]) {
       if (l == 0) {
-        rc = grad_gemm(hb, dZ, R, w.Eraw, d.dp, M, dweights[0], d.dp, 0);
+        rc = grad_gemm(gc, dZ, R, w.Eraw, d.dp, M, dweights[0], d.dp, 0);
       } else {
         const int i = l - 1;
         const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
         const int C = H + (skip ? d.dp : 0);
-        rc = grad_gemm(hb, dZ, R, w.A + (size_t)(l - 1) * lay, H, M, dweights[l], C, 0);
-        if (!rc && skip) rc = grad_gemm(hb, dZ, R, w.Eact, d.dp, M, dweights[l], C, H);
+        rc = grad_gemm(gc, dZ, R, w.A + (size_t)(l - 1) * lay, H, M, dweights[l], C, 0);
+        if (!rc && skip) rc = grad_gemm(gc, dZ, R, w.Eact, d.dp, M, dweights[l], C, H);
       }
       if (rc) return rc;
     }
@@ -516,7 +573,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   return NRT_OK;
 }
 
-static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[8]) {
+static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {
   const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
   sz[0] = lay;          // Z
   sz[1] = lay;          // Z tangent
@@ -526,14 +583,15 @@ static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[8]) {
   sz[5] = sz[4];                      // E1
   sz[6] = (size_t)2 * M * d.out * 4;  // output seed
   sz[7] = (size_t)kBiasChunks * kBiasMaxR * 4;  // bias partial sums
+  sz[8] = split_part_floats(d) * 4;             // split-K partial products
   size_t tot = 0;
-  for (int i = 0; i < 8; ++i) tot += a256(sz[i]);
+  for (int i = 0; i < 9; ++i) tot += a256(sz[i]);
   return tot;
 }
 
 size_t nrt_mlp_grad_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
   if (!m) return 0;
-  size_t sz[8];
+  size_t sz[9];
   return gb_sizes(m->host_dev, std::max<int64_t>(M, 1), sz);
 }
 
@@ -560,11 +618,11 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   };
   if (M == 0) return zero_all();
   if (!dweights && !dbiases) return NRT_OK;
-  size_t sz[8];
+  size_t sz[9];
   gb_sizes(d, M, sz);
-  float* buf[8];
+  float* buf[9];
   char* p = (char*)workspace;
-  for (int i = 0; i < 8; ++i) { buf[i] = (float*)p; p += a256(sz[i]); }
+  for (int i = 0; i < 9; ++i) { buf[i] = (float*)p; p += a256(sz[i]); }
   // slab row: primal activations | encoding | encoding tangent | tangent activations
   const int RS = (2 * std::max(H, 32) + 2 * std::max(d.ke, 16)) | 1;
   const int per_wave = 32 * RS;
@@ -596,6 +654,7 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   if (!hb) { set_error("nrt_mlp_grad_backward: rocblas_create_handle failed"); return NRT_EHIP; }
   rocblas_status s = rocblas_set_stream(hb, st);
   if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
+  const GemmCtx gc{hb, buf[8], st};
   const size_t lay2 = (size_t)M2 * H;
   for (int l = 0; l <= L + 1; ++l) {
     const bool outl = l == L + 1;
@@ -603,13 +662,13 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
     const float* dZ = outl ? seed : buf[3] + (size_t)l * lay2;
     if (dweights && dweights[l]) {
       if (l == 0) {
-        rc = grad_gemm(hb, dZ, R, buf[4], d.dp, M2, dweights[0], d.dp, 0);
+        rc = grad_gemm(gc, dZ, R, buf[4], d.dp, M2, dweights[0], d.dp, 0);
       } else {
         const int i = l - 1;
         const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
         const int C = H + (skip ? d.dp : 0);
-        rc = grad_gemm(hb, dZ, R, buf[2] + (size_t)(l - 1) * lay2, H, M2, dweights[l], C, 0);
-        if (!rc && skip) rc = grad_gemm(hb, dZ, R, buf[5], d.dp, M2, dweights[l], C, H);
+        rc = grad_gemm(gc, dZ, R, buf[2] + (size_t)(l - 1) * lay2, H, M2, dweights[l], C, 0);
+        if (!rc && skip) rc = grad_gemm(gc, dZ, R, buf[5], d.dp, M2, dweights[l], C, H);
       }
       if (rc) return rc;
     }
