@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
     ap.add_argument("--crop", type=int, default=80, help="--scene train: crop side")
     args = ap.parse_args()
+    import sys
+    args.precision_set = any(a.startswith("--precision") for a in sys.argv[1:])
     if args.scene == "train":
         if args.size is None:
             args.size = 256
@@ -450,7 +452,10 @@ def bench_train(args):
     device = torch.device("cuda", 0)
     torch.cuda.set_device(device)
     _lib.load(require_device=True)
-    nra.set_precision("fp32")
+    # --precision fp16: mixed precision -- the gradient-free march / scan and the MLP forwards on
+    # the FP16 kernels, every backward in FP32 (default fp32: the reference's arithmetic)
+    prec = args.precision if args.precision_set else "fp32"
+    nra.set_precision(prec)
     torch.manual_seed(0)
     random.seed(0)
     sdf = SphereSDF(n=128, device="cpu")
@@ -514,7 +519,8 @@ def bench_train(args):
         "value": rays * args.samples * args.steps / elapsed, "unit": "ray-samples/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if prec == "fp32" else "fp16 forward / fp32 backward",
         "data": "synthetic (seeded random-init weights, random target crops)",
         "config": {"workload": "forward (fused march + scan) + backward (MLP backward, SDF-normal "
                                "double backward, shading autograd) + AdamW",

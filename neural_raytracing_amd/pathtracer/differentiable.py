@@ -157,7 +157,8 @@ def sdf_gradient(sdf, p):
 # ---- shading (integrators.py:139-206 with emitter_samples=1, bsdf_samples=0) -----------------
 
 def light_sample(lights, it, active):
-    """sample_emitter_dir_wo_isect (scene.py:321-324) -> (d, Le, pdf)."""
+    """lights.sample_direction + sample_emitter_dir_wo_isect (scene.py:321-324)
+    -> (d, Le, pdf, dist); dist is None for a LightField (lights.py:181-183)."""
     from .lights.lights import LightField, PointLights
     p = it.p
     if isinstance(lights, LightField):
@@ -168,6 +169,7 @@ def light_sample(lights, it, active):
         le = torch.zeros_like(p)
         le[active] = torch.linalg.norm(v, ord=2, dim=-1, keepdim=True) * lights.color.sigmoid()
         pdf = torch.ones(p.shape[:-1], device=p.device)
+        dist = None
     elif isinstance(lights, PointLights):
         # lights.py:89-110
         loc = lights.location.reshape(-1, 3)[0]
@@ -183,6 +185,28 @@ def light_sample(lights, it, active):
     else:
         raise _lib.NrtError(f"light {type(lights).__name__} has no HIP training path")
     le = torch.where(active.unsqueeze(-1), le, torch.zeros_like(le))
+    return d, le, pdf, dist
+
+
+def shadowed_light(shapes, lights, it, active, w_isect):
+    """sample_emitter_dir_w_isect / _w_learned_occ (scene.py:290-319) with autograd: the shadow
+    march is gradient-free in the reference too (intersect_test runs under no_grad, sdfs.py:
+    170-179) and runs on the fused kernel; Le is masked (w_isect=True) or scaled by
+    sigmoid(occ([p, dir_to_elev_azim(d)])) where occluded (w_isect=<occlusion MLP>)."""
+    from .utils import dir_to_elev_azim
+    d, le, pdf, dist = light_sample(lights, it, active)
+    if dist is None:
+        raise _lib.NrtError("shadow rays need a PointLights (ds.dist, scene.py:296)")
+    rays = torch.cat([it.p, d], dim=-1).detach()
+    with torch.no_grad():
+        visible = shapes.intersect_test(rays, max_t=dist.detach().reshape_as(active)[..., None],
+                                        active=active)
+    if w_isect is True:
+        le = torch.where((~visible | ~active).unsqueeze(-1), torch.zeros_like(le), le)
+    else:
+        occ_rays = torch.cat([it.p, dir_to_elev_azim(d)], dim=-1)
+        le = torch.where((~visible)[..., None], w_isect(occ_rays).sigmoid() * le, le)
+        le = active[..., None] * le
     return d, le, pdf
 
 
@@ -224,12 +248,17 @@ def bsdf_eval(bsdf, it, wo, active):
     raise _lib.NrtError(f"BSDF {type(bsdf).__name__} has no HIP training path")
 
 
-def direct_sample(it, active, bsdf, lights, lead, device):
-    """Direct.sample's shading with autograd (integrators.py:167-189)."""
+def direct_sample(it, active, bsdf, lights, lead, device, shapes=None, w_isect=False):
+    """Direct.sample's shading with autograd (integrators.py:167-189); w_isect as in
+    integrators.py:161-166 (True: shadow rays, an MLP: learned occlusion)."""
+    from .neural_blocks import SkipConnMLP
     result = torch.zeros(*lead, 3, device=device)
     if not bool(active.any()):
         return result
-    d, le, pdf = light_sample(lights, it, active)
+    if w_isect is True or type(w_isect) is SkipConnMLP:
+        d, le, pdf = shadowed_light(shapes, lights, it, active, w_isect)
+    else:
+        d, le, pdf, _ = light_sample(lights, it, active)
     ae = active & (pdf > 0)
     wo = it.to_local(d)
     f, _ = bsdf_eval(bsdf, it, wo, ae)

@@ -134,11 +134,10 @@ class Direct(Integrator):
         if self.emitter_samples != 1 or self.bsdf_samples != 0:
             raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
         it, active = shapes.intersect(rays, primary=self.training)
-        if getattr(it, "_nrt_train", False) or needs_grad(bsdf, lights):
+        if getattr(it, "_nrt_train", False) or needs_grad(bsdf, lights, kwargs.get("w_isect")):
             # training: shading with autograd through the HIP MLPs
-            if shadow:
-                raise _lib.NrtError("Direct with w_isect is not on the HIP training path")
-            return direct_sample(it, active, bsdf, lights, rays.shape[:-1], rays.device), active, it
+            return direct_sample(it, active, bsdf, lights, rays.shape[:-1], rays.device, shapes,
+                                 kwargs.get("w_isect", False)), active, it
         result = torch.zeros(*rays.shape[:-1], 3, device=rays.device)
         hit_idx, hit_count, flat = it._nrt_hits
         P = flat.shape[0]

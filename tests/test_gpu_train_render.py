@@ -335,3 +335,126 @@ def test_path_and_envmap_refuse_autograd():
     nerf = NeRFLE(envmap=True, device="cuda")
     with pytest.raises(NrtError):
         nerf(rays, PointLights(device="cuda"))
+
+
+@pytest.mark.gpu
+def test_mixed_precision_training_steps():
+    """set_precision("fp16") with autograd: FP16 march / scan (ring kernels, scan argmin from the
+    64-bit keys) and MLP forwards, FP32 backward; the loop still lowers the loss and the
+    gradients stay finite."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    _, mine = _perturbed_scene()
+    set_precision("fp16")
+    try:
+        target = torch.full((32, 32, 4), 0.5, device="cuda")
+        params = [*mine["shape"].sdf.parameters(), *mine["bsdf"].parameters(),
+                  *mine["lights"].parameters()]
+        opt = torch.optim.Adam(params, lr=1e-3)
+        losses = []
+        for step in range(6):
+            random.seed(step)
+            opt.zero_grad()
+            img, mi = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"],
+                                          mine["integrator"], bsdf=mine["bsdf"], size=256,
+                                          chunk_size=256, bundle_size=1, crop_size=32,
+                                          uv=(112, 112), background=0, with_noise=0.0,
+                                          device="cuda", addition=lambda m: m)
+            loss = F.mse_loss(img, target) + 0.1 * (mi.raw_normals.norm(dim=-1) - 1).square().mean()
+            loss.backward()
+            assert all(p.grad is None or bool(torch.isfinite(p.grad).all()) for p in params)
+            opt.step()
+            losses.append(loss.item())
+        assert losses[-1] < losses[0], losses
+    finally:
+        set_precision("fp32")
+
+
+def _shadow_oracle(ref, occ_ref, dtype, w, kind):
+    """Oracle Direct render of the shadow scene with w_isect = True | occ MLP, in ``dtype``;
+    returns the image and the gradients of <img, w> for the SDF, Diffuse and occlusion MLP."""
+    r = {k: copy.deepcopy(v) for k, v in ref.items()}
+    r["shape"].create_graph = True  # differentiable normals, as the reference's autograd_diff
+    occ = copy.deepcopy(occ_ref)
+    mods = [r["shape"].sdf, occ]
+    for m in mods:
+        m.to(dtype)
+        for sub in m.modules():
+            if hasattr(sub, "basis_p"):
+                sub.basis_p = sub.basis_p.to(dtype)
+    r["bsdf"].reflectance = r["bsdf"].reflectance.to(dtype).requires_grad_(True)
+    li = r["lights"]
+    for a in ("scale", "intensity", "location", "const", "linear", "square"):
+        setattr(li, a, getattr(li, a).to(dtype))
+    r["camera"].cam_to_world = r["camera"].cam_to_world.to(dtype)
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        random.seed(8)
+        img = R.render(r["shape"], r["lights"], r["camera"], R.DirectRef(), r["bsdf"], size=64,
+                       chunk_size=64, background=0.0, with_noise=0.0,
+                       w_isect=True if kind == "hard" else occ)
+        if w is not None:
+            (img * w.to(dtype)).sum().backward()
+    finally:
+        torch.set_default_dtype(old)
+    grads = {}
+    if w is not None:
+        sdf = r["shape"].sdf
+        grads = {"centers": sdf.centers.grad, "radii": sdf.radii.grad,
+                 "reflectance": r["bsdf"].reflectance.grad}
+        for i, a in enumerate([occ.init, *occ.layers, occ.out]):
+            grads[f"occ.W{i}"], grads[f"occ.b{i}"] = a.weight.grad, a.bias.grad
+        grads = {k: (torch.zeros(1) if g is None else g.detach().double()) for k, g in grads.items()}
+    return img.detach(), grads
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["hard", "learned_occ"])
+def test_shadowed_direct_gradients_match_oracle(kind):
+    """Direct with w_isect=True / an occlusion MLP under autograd (colocate.py trains with the
+    latter, :137): gradients of <img, w> for the SDF spheres, the Diffuse reflectance and the
+    occlusion MLP vs float64 oracle autograd.  Pixels whose shadow test flips between
+    implementations (ulp-level march differences at the shadow boundary) get w = 0 on both
+    sides, so every compared gradient comes from rays all three runs agree on."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    import tests.test_gpu_parity as P
+    ref, mine = P._shadow_scene()
+    occ_ref, occ_mine = P._occ_pair(1)
+    occ_ref.act_name = "softplus"
+    occ_mine.activation = F.softplus
+    img64, _ = _shadow_oracle(ref, occ_ref, torch.float64, None, kind)
+    img32, _ = _shadow_oracle(ref, occ_ref, torch.float32, None, kind)
+    set_precision("fp32")
+    random.seed(8)
+    got, _ = pt.pathtrace_sample(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                                 bsdf=mine["bsdf"], size=64, chunk_size=64, bundle_size=1,
+                                 crop_size=64, uv=(0, 0), background=0, with_noise=0.0,
+                                 w_isect=True if kind == "hard" else occ_mine)
+    assert got.requires_grad
+    agree = ((got.detach().cpu().double() - img64).abs().amax(-1) <= 1e-4) & \
+        ((img32.double() - img64).abs().amax(-1) <= 1e-4)
+    assert agree.float().mean() >= 0.99
+    w = torch.randn(64, 64, 3, generator=torch.Generator().manual_seed(2)) * agree[..., None]
+    _, want = _shadow_oracle(ref, occ_ref, torch.float64, w, kind)
+    _, ref32 = _shadow_oracle(ref, occ_ref, torch.float32, w, kind)
+    (got * w.cuda()).sum().backward()
+    sdf = mine["shape"].sdf
+    have = {"centers": sdf.centers.grad, "radii": sdf.radii.grad,
+            "reflectance": mine["bsdf"].reflectance.grad}
+    for i, a in enumerate(occ_mine._linears()):
+        have[f"occ.W{i}"], have[f"occ.b{i}"] = a.weight.grad, a.bias.grad
+    bad = []
+    for k, g64 in want.items():
+        gb = have[k]
+        gb = torch.zeros_like(g64) if gb is None else gb.detach().cpu().double().reshape(g64.shape)
+        err = (gb - g64).abs().max().item()
+        e32 = (ref32[k].reshape(g64.shape) - g64).abs().max().item()
+        if err > max(2e-3 * g64.abs().max().item(), 4 * e32) + 1e-9:
+            bad.append(f"{k}: err {err:.3g} scale {g64.abs().max().item():.3g} fp32 {e32:.3g}")
+    assert not bad, "\n".join(bad)
+    assert want["reflectance"].abs().max() > 0
+    if kind == "learned_occ":
+        assert want["occ.W0"].abs().max() > 0  # the occlusion MLP is on the gradient path
