@@ -528,7 +528,51 @@ def bench_train(args):
                    "samples_per_ray": args.samples},
         "kernel_ms_per_step": kms, "final_loss": float(loss),
     }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_train_baseline(sdf, bsdf, lights, size, focal, args)
     print(json.dumps(line), flush=True)
+
+
+def cpu_train_baseline(sdf, bsdf, lights, size, focal, args, crop=48):
+    """The oracle (torch-CPU restatement, 'port') running the same training step -- forward,
+    create_graph normals, loss = MSE + eikonal, backward -- on one view's crop x crop window, on
+    this host's threads; rate in training ray-samples/s like the GPU line."""
+    from oracle import pathtracer_ref as R
+    blob = R.SphereBlobSDF(n=sdf.centers.shape[0])
+    with torch.no_grad():
+        blob.centers.copy_(sdf.centers.cpu())
+        blob.radii.copy_(sdf.radii.cpu())
+        blob.tfs.copy_(sdf.tfs.cpu())
+    _copy_to_oracle(blob.shift, sdf.shift)
+    shape = R.MarchedSDF(sdf=blob, max_steps=args.samples, create_graph=True)
+    parts = [R.NeuralBSDFRef(activation="softplus") for _ in bsdf.bsdfs]
+    for a, b in zip(parts, bsdf.bsdfs):
+        _copy_to_oracle(a.mlp, b.mlp)
+    obsdf = R.SpatialMixBSDF(parts)
+    _copy_to_oracle(obsdf.sp_var_fn, bsdf.sp_var_fn)
+    olights = R.LightFieldRef()
+    _copy_to_oracle(olights.light_field_approx, lights.light_field_approx)
+    with torch.no_grad():
+        olights.color.copy_(lights.color.cpu())
+    cam = R.NeRFCameraRef(view_c2w(0, 1).unsqueeze(0), focal)
+    integ = R.NeRFIntegratorRef(R.DirectRef())
+    c0 = (size - crop) // 2
+    target = torch.rand(crop, crop, 3, generator=torch.Generator().manual_seed(2))
+    random.seed(9)
+    t0 = time.perf_counter()
+    img = R.render(shape, olights, cam, integ, obsdf, size=size, chunk_size=size, background=0.0,
+                   with_noise=0.0, crop=(c0, c0, crop))
+    rays = cam.sample_positions(R._tile_positions(c0, c0, crop), size, 0.0)
+    o, d = rays.split(3, dim=-1)
+    t, hit = shape.march(o, d)
+    raw = shape.gradient((o + t * d)[hit])
+    loss = F.mse_loss(img[..., :3], target) + (raw.norm(dim=-1) - 1).square().mean()
+    loss.backward()
+    cpu_s = time.perf_counter() - t0
+    return {"value": crop * crop * args.samples / cpu_s, "unit": "ray-samples/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"one view, {crop}x{crop} crop, {args.samples} march steps + scan, forward + "
+                      f"backward (oracle/pathtracer_ref.py autograd), {cpu_s:.1f} s"}
 
 
 def rr_hit_fraction(rr):
