@@ -11,6 +11,10 @@
 * ``KRt_from_P`` / ``load_dtu_cameras`` / ``load_dtu`` -- scripts/dtu.py:50-89: ``cameras.npz``
   world_mat_i @ scale_mat_i, intrinsics K / K[2,2] as a 4x4, pose [R^T | centre], translations
   divided by the largest camera distance; sorted ``mask/`` and ``image/`` directories.
+* ``train_nerf`` / ``train_dtu`` -- the per-scene optimisation loops (training_utils.py:211-300,
+  347-434): N views per step chosen by a ``LossSampler``, ``pathtrace_sample`` of a crop with
+  autograd through the HIP path, ``masked_loss`` + ``extra_loss``, one
+  optimiser step, periodic validation renders under ``torch.no_grad``.
 """
 import json
 import os
@@ -117,3 +121,106 @@ def load_dtu(directory, size=512, device="cuda"):
     intrinsics, poses = load_dtu_cameras(os.path.join(directory, "cameras.npz"), len(exp_imgs),
                                          device)
     return exp_imgs, exp_masks, intrinsics, poses
+
+
+def _train_loop(make_cameras, valid_cameras, shape, bsdf, integrator, lights, exp_imgs, exp_masks,
+                opt, size, crop_size, N, iters, num_ckpts, save_freq, valid_freq, max_valid_size,
+                extra_loss, save_fn, name_fn, valid_name_fn, uv_select, silent, mask_weight):
+    from .. import pathtracer as pt
+    from .integrators import NeRFIntegrator
+    from .utils import LossSampler, masked_loss, save_image
+    train_integrator = NeRFIntegrator(integrator)
+    device = exp_imgs[0].device
+    ckpt_freq = (iters // num_ckpts) - 1
+    losses = []
+    selector = LossSampler(len(exp_imgs))
+    for i in range(iters):
+        idxs = selector.sample(n=N)
+        cameras = make_cameras(idxs)
+        exp = torch.stack([exp_imgs[j] for j in idxs])
+        mask = torch.stack([exp_masks[j] for j in idxs])
+        opt.zero_grad()
+        (u, v) = uv_select(mask[0], crop_size)
+        u, v = int(u), int(v)
+        got, mi = pt.pathtrace_sample(shape, size=size, chunk_size=size, bundle_size=1,
+                                      crop_size=crop_size, bsdf=bsdf, integrator=train_integrator,
+                                      cameras=cameras, lights=lights, device=device, uv=(u, v),
+                                      background=0, addition=lambda m: m, squeeze_first=False,
+                                      silent=True)
+        if save_freq and (i % save_freq) == 0 and name_fn is not None:
+            save_image(name_fn(i), got[0])
+        exp = exp[:, u:u + crop_size, v:v + crop_size]
+        mask = mask[:, u:u + crop_size, v:v + crop_size]
+        loss = masked_loss(got[..., :3], exp, mi.throughput.squeeze(-1), mask,
+                           mask_weight=mask_weight, with_logits=mi.with_logits) + \
+            extra_loss(mi, got, exp, mask)
+        if loss.isnan():
+            loss.backward()
+            opt.step()
+            raise Exception("Unexpected NaN")
+        loss.backward()
+        opt.step()
+        loss = loss.detach().item()
+        losses.append(loss)
+        selector.update_idxs(idxs, loss)
+        if silent:
+            print(f"{i:06}: {loss:.05}")
+        if ((i % ckpt_freq) == 0) and (i != 0):
+            save_fn(i)
+        if valid_freq and (i % valid_freq) == 0 and valid_name_fn is not None:
+            with torch.no_grad():
+                validate, _ = pt.pathtrace(shape, size=size, chunk_size=min(size, max_valid_size),
+                                           bundle_size=1, bsdf=bsdf, integrator=train_integrator,
+                                           cameras=valid_cameras(idxs), lights=lights,
+                                           device=device, silent=True)
+                save_image(valid_name_fn(i), validate)
+    return losses
+
+
+def train_nerf(shape, bsdf, integrator, lights, cam_to_worlds, focal, exp_imgs, exp_masks, opt,
+               size, crop_size, N=3, iters=50_000, num_ckpts=5, save_freq=50, valid_freq=250,
+               max_valid_size=128, extra_loss=lambda mi, got, exp, mask: 0,
+               save_fn=lambda i: None, name_fn=lambda i: f"outputs/train_{i:05}.png",
+               valid_name_fn=lambda i: f"outputs/valid_{i:05}.png", uv_select=None,
+               silent=False):
+    """training_utils.py:211-300 (NeRF-synthetic scenes, NeRFCamera, mask_weight 15)."""
+    from .cameras import NeRFCamera
+    from .utils import rand_uv_mask
+    device = exp_imgs[0].device
+
+    def cams(idxs):
+        c2w = torch.stack([cam_to_worlds[j] for j in idxs], dim=0)
+        return NeRFCamera(cam_to_world=c2w, focal=focal, device=device)
+
+    def valid(idxs):
+        return NeRFCamera(cam_to_world=cam_to_worlds[idxs[0]].unsqueeze(0), focal=focal,
+                          device=device)
+    return _train_loop(cams, valid, shape, bsdf, integrator, lights, exp_imgs, exp_masks, opt,
+                       size, crop_size, N, iters, num_ckpts, save_freq, valid_freq,
+                       max_valid_size, extra_loss, save_fn, name_fn, valid_name_fn,
+                       uv_select or rand_uv_mask, silent, 15)
+
+
+def train_dtu(shape, bsdf, integrator, lights, poses, intrinsics, exp_imgs, exp_masks, opt, size,
+              crop_size, N=3, iters=50_000, num_ckpts=5, save_freq=50, valid_freq=250,
+              max_valid_size=128, extra_loss=lambda mi, got, exp, mask: 0,
+              save_fn=lambda i: None, name_fn=lambda i: f"outputs/train_{i:05}.png",
+              valid_name_fn=lambda i: f"outputs/valid_{i:05}.png", uv_select=None,
+              silent=False):
+    """training_utils.py:347-434 (DTU scans, DTUCamera, mask_weight 10)."""
+    from .cameras import DTUCamera
+    from .utils import rand_uv_mask
+    device = exp_imgs[0].device
+
+    def cams(idxs):
+        pose = torch.stack([poses[j] for j in idxs], dim=0)
+        intr = torch.stack([intrinsics[j] for j in idxs], dim=0)
+        return DTUCamera(pose=pose, intrinsic=intr, device=device)
+
+    def valid(idxs):
+        # training_utils.py:421-423: the first drawn pose with intrinsics[0]
+        return DTUCamera(pose=poses[idxs[0]][None], intrinsic=intrinsics[0][None], device=device)
+    return _train_loop(cams, valid, shape, bsdf, integrator, lights, exp_imgs, exp_masks, opt,
+                       size, crop_size, N, iters, num_ckpts, save_freq, valid_freq,
+                       max_valid_size, extra_loss, save_fn, name_fn, valid_name_fn,
+                       uv_select or rand_uv_mask, silent, 10)

@@ -51,3 +51,68 @@ def dir_to_elev_azim(direc):
     elev = z.asin()
     azim = torch.atan2(x, (1 - x.square() - z.square()).clamp(min=1e-10).sqrt())
     return torch.cat([elev, azim], dim=-1)
+
+
+class LossSampler:
+    """View selection weighted by the squared last loss (utils.py:134-147); views not drawn for a
+    while gain likelihood by ``likelihood_inc`` per update."""
+
+    def __init__(self, N, default=1e5, likelihood_inc=1.00001):
+        self.losses = np.array([default] * N)
+        self.l_inc = likelihood_inc
+
+    def update(self, idx, loss):
+        self.losses *= self.l_inc
+        self.losses[idx] = loss + 1
+
+    def sample(self, n=1, replace=False):
+        sq = self.losses * self.losses
+        return np.random.choice(len(self.losses), replace=replace, size=n, p=sq / sq.sum())
+
+    def update_idxs(self, idxs, loss):
+        for idx in idxs:
+            self.update(idx, loss)
+
+
+def rand_uv_mask(mask, size: int):
+    """A crop corner inside the mask's valid region (utils.py:378-383)."""
+    half = int(math.ceil(size / 2))
+    valid = mask[half:-half - size, half:-half - size, ...]
+    p, q = valid.nonzero(as_tuple=True)
+    idx = random.randint(0, len(p) - 1)
+    return p[idx], q[idx]
+
+
+def masked_loss(got, exp, throughput, exp_mask, eps: float = 1e-10, trim: int = 0,
+                mask_weight: float = 1, with_logits: bool = True, tone_mapping: bool = False):
+    """utils.py:307-359: on rays that hit inside the mask, 10 x (L2 + RMSE + L1 - log SSIM) of the
+    masked colours (tone-mapped x/(1+x) if asked); on the others, BCE of the throughput logits
+    against the mask, weighted by ``mask_weight``."""
+    from .metrics import ssim
+    active = ((throughput > 0) & (exp_mask == 1)).squeeze(-1)
+    misses = ~active
+    color_loss = 0
+    if active.any():
+        got_active = got * active[..., None]
+        exp_active = exp * active[..., None]
+        if tone_mapping:
+            got_active = got_active / (1 + got_active)
+            exp_active = exp_active / (1 + exp_active)
+        l1_loss = F.l1_loss(got_active, exp_active)
+        l2_loss = F.mse_loss(got_active, exp_active)
+        rmse_loss = l2_loss.clamp(min=1e-10).sqrt()
+        ssim_loss = -ssim(got_active.permute(0, 3, 1, 2), exp_active.permute(0, 3, 1, 2),
+                          data_range=1, size_average=True).log()
+        color_loss = l2_loss + rmse_loss + l1_loss + ssim_loss
+    mask_loss = 0
+    if misses.any():
+        loss_fn = F.binary_cross_entropy_with_logits if with_logits else F.binary_cross_entropy
+        mask_loss = loss_fn(throughput[misses].reshape(-1, 1), exp_mask[misses].reshape(-1, 1))
+    return mask_weight * mask_loss + 10 * color_loss
+
+
+def save_image(name, img):
+    """training_utils.py:21 (PNG through PIL; matplotlib is not needed)."""
+    from PIL import Image
+    arr = (img.detach().cpu().clamp(0, 1).numpy() * 255 + 0.5).astype(np.uint8)
+    Image.fromarray(arr).save(name)

@@ -7,6 +7,7 @@ oracle's SkipMLP (as tests/test_gpu_train.py does for the first backward); whole
 gradients are FP32 on both sides with different batch-reduction orders, so they are compared at
 2e-3 of each tensor's largest entry (plus 1e-6 absolute)."""
 import copy
+import math
 import random
 
 import pytest
@@ -458,3 +459,47 @@ def test_shadowed_direct_gradients_match_oracle(kind):
     assert want["reflectance"].abs().max() > 0
     if kind == "learned_occ":
         assert want["occ.W0"].abs().max() > 0  # the occlusion MLP is on the gradient path
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loop", ["nerf", "dtu"])
+def test_training_loops_run_on_the_hip_path(loop, tmp_path):
+    """training_utils.train_nerf / train_dtu (training_utils.py:211-300, 347-434): a few
+    iterations over synthetic views with the scripts' extra eikonal loss; finite losses, images
+    written, parameters moved."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer import training_utils as TU
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    from neural_raytracing_amd.pathtracer.utils import eikonal_loss
+    set_precision("fp32")
+    _, mine = _perturbed_scene()
+    size, n_views = 64, 4
+    g = torch.Generator().manual_seed(3)
+    imgs = [torch.rand(size, size, 3, generator=g).cuda() for _ in range(n_views)]
+    masks = [torch.ones(size, size, device="cuda") for _ in range(n_views)]
+    before = mine["shape"].sdf.centers.detach().clone()
+    opt = torch.optim.AdamW([*mine["shape"].parameters(), *mine["bsdf"].parameters(),
+                             *mine["lights"].parameters()], lr=1e-3, weight_decay=0)
+    extra = lambda mi, got, exp, mask: eikonal_loss(mi.raw_normals) if mi.raw_normals is not None else 0
+    common = dict(opt=opt, size=size, crop_size=16, N=2, iters=3, num_ckpts=1, save_freq=2,
+                  valid_freq=0, extra_loss=extra, silent=False,
+                  name_fn=lambda i: str(tmp_path / f"train_{i}.png"),
+                  uv_select=lambda mask, crop: (20, 24))
+    random.seed(0)
+    if loop == "nerf":
+        c2w = mine["camera"].cam_to_world.reshape(-1, 3, 4)[0]
+        losses = TU.train_nerf(mine["shape"], mine["bsdf"], Direct(), mine["lights"],
+                               [c2w] * n_views, mine["camera"].focal, imgs, masks, **common)
+    else:
+        pose = torch.eye(4)
+        pose[:3, :4] = mine["camera"].cam_to_world.reshape(-1, 3, 4)[0].cpu()
+        pose[:3, 1:3] *= -1  # DTU looks down +z
+        K = torch.eye(4)
+        K[0, 0] = K[1, 1] = 2890.0
+        K[0, 2], K[1, 2] = 800.0, 600.0
+        losses = TU.train_dtu(mine["shape"], mine["bsdf"], Direct(), mine["lights"],
+                              [pose.cuda()] * n_views, [K.cuda()] * n_views, imgs, masks,
+                              **common)
+    assert len(losses) == 3 and all(math.isfinite(x) for x in losses), losses
+    assert (tmp_path / "train_0.png").exists()
+    assert not torch.equal(before, mine["shape"].sdf.centers.detach())
