@@ -75,6 +75,13 @@ int nrt_mlp_create(const nrt_mlp_desc* desc, const float* host_basis,
                    const float* const* host_weights, const float* const* host_biases,
                    nrt_mlp** out);
 int nrt_mlp_destroy(nrt_mlp* mlp);
+/* Re-pack an MLP handle from the caller's DEVICE weights after an optimiser step (training,
+ * SURVEY §8f rank 1; the same nn.Linear layouts as nrt_mlp_create, stream-ordered, no host copy):
+ * refreshes the fragments nrt_mlp_forward / nrt_mlp_backward / nrt_mlp_grad_backward read.  A
+ * refreshed handle no longer serves the FP16 ring march or shading programs (NRT_EINVAL there);
+ * render with a handle from nrt_mlp_create. */
+int nrt_mlp_refresh(nrt_mlp* mlp, const float* const* device_weights,
+                    const float* const* device_biases, void* stream);
 
 /* y[M, out] = SkipConnMLP(x[M, in], latent[M, latent]) -- neural_blocks.py:75-86 */
 int nrt_mlp_forward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,

@@ -60,6 +60,7 @@ _SIGNATURES = {
     "nrt_device_ok": (_I32, []),
     "nrt_mlp_create": (_I32, [ctypes.POINTER(MlpDesc), _P, _P, _P, ctypes.POINTER(_P)]),
     "nrt_mlp_destroy": (_I32, [_P]),
+    "nrt_mlp_refresh": (_I32, [_P, _P, _P, _P]),
     "nrt_mlp_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P]),
     "nrt_sdf_create_unit_sphere": (_I32, [ctypes.POINTER(_P)]),
     "nrt_sdf_create_mlp": (_I32, [_P, ctypes.POINTER(_P)]),

@@ -359,6 +359,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
 static bool nerf_fusable(const nrt_mlp* f, const nrt_mlp* s) {
   const MlpDev& a = f->host_dev;
   const MlpDev& b = s->host_dev;
+  if (f->refreshed || s->refreshed) return false;  // stale program streams: unfused path
   return a.in_size == 3 && a.nb == 4 && a.freqs == 16 && a.out == 65 && a.latent == 0 &&
          a.act == ACT_LEAKY && b.in_size == 70 && b.nb == 2 && b.freqs == 16 && b.out == 3 &&
          b.latent == 0 && b.act == ACT_LEAKY && a.n_hidden == kNerfL1 && b.n_hidden == kNerfL2 &&

@@ -27,6 +27,16 @@ struct nrt_mlp {
   mutable std::unique_ptr<nrt_prog> nerf_prog;
   mutable uint64_t nerf_first_serial = 0;
   uint64_t serial = 0;  // unique per created MLP (cache key; addresses can be reused)
+  // nrt_mlp_refresh (nrt_refresh.hip): gather maps of the per-kernel fragment arrays, built on
+  // the first refresh; after a refresh the FP16 ring / program streams and the host copies
+  // above are stale and the handle only serves nrt_mlp_forward / _backward / _grad_backward
+  int* gather_map = nullptr;     // [n_gather] source index into [W_0..W_L+1 | b_0..b_L+1] or -1
+  float* gather_src = nullptr;   // staging copy of the caller's weights and biases
+  int64_t n_src = 0;
+  std::vector<void*> gather_dst;   // per section: destination array, element count, FP16?
+  std::vector<int64_t> gather_n;
+  std::vector<char> gather_f16;
+  bool refreshed = false;
   ~nrt_mlp();
 };
 

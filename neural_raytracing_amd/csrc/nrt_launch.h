@@ -81,7 +81,7 @@ static inline int sdf_dims(const nrt_sdf* s, int& hidden, int& ke) {
 // Configurations with a compiled ring kernel: 8 hidden layers of 128/256, skip 3, F = 16/32
 // (3 or 5 encoding k-steps), 3 inputs, no latent, <= 32 outputs.
 inline bool ring_supported(const nrt_sdf* s) {
-  if (!s->mlp) return false;
+  if (!s->mlp || s->mlp->refreshed) return false;  // a refreshed handle's FP16 stream is stale
   const MlpDev& m = s->mlp->host_dev;
   const int ne = m.ke / 16;
   return (m.nb == 8 || m.nb == 4) && (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&

@@ -293,6 +293,8 @@ extern "C" int nrt_mlp_destroy(nrt_mlp* m) {
   if (!m) return NRT_OK;
   if (m->blob) (void)hipFree(m->blob);
   if (m->dev) (void)hipFree(m->dev);
+  if (m->gather_map) (void)hipFree(m->gather_map);
+  if (m->gather_src) (void)hipFree(m->gather_src);
   delete m;
   return NRT_OK;
 }

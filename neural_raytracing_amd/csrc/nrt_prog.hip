@@ -26,6 +26,11 @@ size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 int build_program(const std::vector<const nrt_mlp*>& mlps, nrt_prog& out) {
   out.ok = false;
   if (mlps.empty() || (int)mlps.size() > kMaxProgMlp) return NRT_OK;
+  for (const nrt_mlp* m : mlps)
+    if (m->refreshed) {  // nrt_mlp_refresh does not re-pack the program streams
+      set_error("shading program: an MLP handle refreshed by nrt_mlp_refresh cannot build one");
+      return NRT_EINVAL;
+    }
   ProgDev& d = out.d;
   std::memset(&d, 0, sizeof(d));
   std::vector<int> coff;

@@ -6,7 +6,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _lib
-from ._handles import mlp_handle
+from ._handles import mlp_handle, train_handle
 from .utils import create_fourier_basis2
 
 
@@ -110,9 +110,10 @@ class SkipConnMLP(nn.Module):
         return y.reshape(batches + (self.out.out_features,))
 
 
-def _mlp_forward(mlp, x, lat):
+def _mlp_forward(mlp, x, lat, handle=None):
     y = torch.empty(x.shape[0], mlp.out.out_features, device=x.device)
-    _lib.call("nrt_mlp_forward", mlp.nrt(), _lib.ptr(x), _lib.ptr(lat), x.shape[0],
+    h = mlp.nrt() if handle is None else handle.value
+    _lib.call("nrt_mlp_forward", h, _lib.ptr(x), _lib.ptr(lat), x.shape[0],
               _lib.ptr(y), _lib.precision_code(), _lib.stream())
     return y
 
@@ -124,10 +125,11 @@ class _MlpFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mlp, x, lat, *params):
+        handle = train_handle(mlp)  # device re-pack after an optimiser step
         with torch.no_grad():
-            y = _mlp_forward(mlp, x.detach(), None if lat is None else lat.detach())
+            y = _mlp_forward(mlp, x.detach(), None if lat is None else lat.detach(), handle)
         ctx.mlp = mlp
-        ctx.handle = mlp_handle(mlp)  # the packed weights this forward used
+        ctx.handle = handle  # the packed weights this forward used
         ctx.has_lat = lat is not None
         ctx.save_for_backward(x, lat if lat is not None else x.new_empty(0))
         return y
@@ -183,16 +185,17 @@ def input_gradient(mlp, x):
     return g.reshape(lead + (mlp.in_size,))
 
 
-def _input_grad(mlp, x):
+def _input_grad(mlp, x, handle=None):
     lib = _lib.load(require_device=True)
     M = x.shape[0]
     g = torch.empty_like(x)
     if M == 0:
         return g
+    h = mlp.nrt() if handle is None else handle.value
     dy = torch.ones(M, mlp.out.out_features, device=x.device)
-    ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(mlp.nrt(), M), dtype=torch.uint8,
+    ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(h, M), dtype=torch.uint8,
                      device=x.device)
-    _lib.call("nrt_mlp_backward", mlp.nrt(), _lib.ptr(x), None, M, _lib.ptr(dy), _lib.ptr(g),
+    _lib.call("nrt_mlp_backward", h, _lib.ptr(x), None, M, _lib.ptr(dy), _lib.ptr(g),
               None, None, None, _lib.ptr(ws), _lib.stream())
     return g
 
@@ -202,10 +205,11 @@ class _InputGradFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mlp, x, *params):
+        handle = train_handle(mlp)
         with torch.no_grad():
-            g = _input_grad(mlp, x.detach())
+            g = _input_grad(mlp, x.detach(), handle)
         ctx.mlp = mlp
-        ctx.handle = mlp_handle(mlp)
+        ctx.handle = handle
         ctx.save_for_backward(x)
         return g
 

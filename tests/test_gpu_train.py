@@ -122,3 +122,48 @@ def test_mlp_parameters_on_another_device_are_refused():
     mlp = SkipConnMLP(num_layers=2, hidden_size=32, in_size=3, out=1, freqs=4, device="cuda")
     with pytest.raises(NrtError):
         mlp(torch.rand(8, 3, device="cuda"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_refreshed_handle_matches_a_fresh_pack(prec):
+    """nrt_mlp_refresh (device re-pack after an optimiser step) gives the same forward outputs
+    and gradients as a handle packed from scratch on the host: after in-place weight updates the
+    autograd path (refreshed training handle) and the no-grad path (fresh host pack) agree
+    bit for bit; the refreshed handle refuses the FP16 program engine."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    seeded(12)
+    mlp = SkipConnMLP(num_layers=8, hidden_size=64, in_size=3, out=3, freqs=16,
+                      device="cpu").cuda()
+    x = torch.rand(777, 3, device="cuda") - 0.5
+    set_precision(prec)
+    try:
+        opt = torch.optim.SGD(mlp.parameters(), lr=0.05)
+        for _ in range(3):
+            opt.zero_grad()
+            y = mlp(x)  # training handle: created, then refreshed on the device
+            y.square().mean().backward()
+            opt.step()
+        y_train = mlp(x).detach()  # refreshed after the last step
+        with torch.no_grad():
+            y_fresh = mlp(x)  # mlp_handle: re-packed on the host from the same weights
+        assert torch.equal(y_train, y_fresh)
+        h = mlp._nrt_train[2]
+        assert h.value != mlp.nrt()
+    finally:
+        set_precision("fp32")
+    # gradients through the refreshed handle vs float64 autograd of the same weights
+    ref = R.SkipMLP(num_layers=8, hidden_size=64, in_size=3, out=3, freqs=16)
+    with torch.no_grad():
+        ref.basis_p = mlp.basis_p.detach().cpu().clone()
+        for a, b in zip([ref.init, *ref.layers, ref.out], mlp._linears()):
+            a.weight.copy_(b.weight.cpu())
+            a.bias.copy_(b.bias.cpu())
+    dy = torch.randn(777, 3, generator=torch.Generator().manual_seed(1))
+    want = _grads(ref, x.cpu(), None, dy, torch.float64)
+    ref32 = _grads(ref, x.cpu(), None, dy, torch.float32)
+    mlp.zero_grad()
+    (mlp(x) * dy.cuda()).sum().backward()
+    for i, a in enumerate(mlp._linears()):
+        _close(a.weight.grad, want[f"dW[{i}]"], ref32[f"dW[{i}]"], f"dW[{i}]")
