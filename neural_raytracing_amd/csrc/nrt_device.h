@@ -356,21 +356,46 @@ __device__ __forceinline__ void write_enc_slab(const MlpDev& m, const EncIn& e, 
 
 // One FP32 GEMM over `nks` k-steps of the slab starting at column kcol; accumulates into acc.
 // act_in >= 0 applies the activation to B on the fly (skip-concat of the encoding).
+// The A fragments are read through a global-address-space pointer (generic "flat" loads also
+// count in lgkmcnt, so the slab's ds_read waits drained them) and prefetched one k-step ahead:
+// the wait before a k-step's MFMAs covers only the previous step's loads.
 template <int NB>
 __device__ __forceinline__ void gemm32(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
                                        int rb0, int nks, const float* X, int RS, int kcol,
                                        int act_in) {
+  using gptr = const __attribute__((address_space(1))) float*;
+  if (nks <= 0) return;
   const int lane = lane_id();
   const int r = lane & 31, h = lane >> 5;
   const float* xr = X + r * RS + kcol + h;
-  for (int s = 0; s < nks; ++s) {
+  const gptr Ag = (gptr)(A + (size_t)rb0 * 64 + lane);
+  const int stride = nrb * 64;
+  // loads are unconditional (clamped row block / k-step) so the compiler counts them exactly
+  int off[NB];
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) off[ib] = (rb0 + ib < nrb ? ib : nrb - 1 - rb0) * 64;
+  // ping-pong fragment buffers (no register copies, which would wait for the prefetch)
+  float a0[NB], a1[NB];
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[off[ib]];
+  auto step = [&](const float (&a)[NB], int s) {
     float b = xr[2 * s];
     if (act_in >= 0) b = act_fwd<false>(b, act_in);
-    const float* As = A + (s * nrb + rb0) * 64 + lane;
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib)
-      if (rb0 + ib < nrb) acc[ib] = mfma32(As[ib * 64], b, acc[ib]);
+      if (rb0 + ib < nrb) acc[ib] = mfma32(a[ib], b, acc[ib]);
+  };
+  int s = 0;
+  for (; s + 1 < nks; s += 2) {
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a1[ib] = Ag[(size_t)(s + 1) * stride + off[ib]];
+    step(a0, s);
+    const int s2 = s + 2 < nks ? s + 2 : nks - 1;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[(size_t)s2 * stride + off[ib]];
+    step(a1, s + 1);
   }
+  if (s < nks) step(a0, s);
 }
 
 template <int NB>
