@@ -443,9 +443,8 @@ __device__ __forceinline__ void mlp32_forward(const MlpDev& m, const EncIn& e, f
   for (int ob = 0; ob < m.ob; ++ob) {
     f16v o[1];
     o[0] = bias_tile(m.bias[m.n_hidden + 1], ob, h);
-    // k-steps over hidden; A is [s][ob][64]
-    const float* xr = X + r * RS + h;
-    for (int s = 0; s < (H >> 1); ++s) o[0] = mfma32(Ao[(s * m.ob + ob) * 64 + lane], xr[2 * s], o[0]);
+    // k-steps over hidden; A is [s][ob][64] (row block ob of m.ob), prefetched like the hidden layers
+    gemm32<1>(o, Ao, m.ob, ob, H >> 1, X, RS, 0, -1);
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
       int row = 32 * ob + (reg & 3) + 8 * (reg >> 2) + 4 * h;

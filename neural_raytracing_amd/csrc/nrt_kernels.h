@@ -68,11 +68,15 @@ __host__ __device__ inline int wave_lds_floats(int RS, int ys, bool f16) {
 // ------------------------------------------------------------------------------------------
 // SDF
 // ------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(4))) float ConstF;
+
 template <bool FAST>
 __device__ __forceinline__ float spheres_value(const SdfDev& s, float x, float y, float z) {
   // smooth_min(|(I+T_i) p - c_i| - r_i, k)   (sdfs.py:37-43, utils.py:386-387)
   float acc = 0.f;
-  const float* sp = s.spheres;
+  // the sphere table is uniform across the wave and read-only: constant address space, so the
+  // compiler reads it with scalar loads instead of 64-lane flat loads that drain lgkmcnt
+  const ConstF* sp = (const ConstF*)s.spheres;
   for (int i = 0; i < s.n_spheres; ++i, sp += 16) {
     float qx = fmaf(sp[2], z, fmaf(sp[1], y, sp[0] * x)) - sp[9];
     float qy = fmaf(sp[5], z, fmaf(sp[4], y, sp[3] * x)) - sp[10];
@@ -85,7 +89,7 @@ __device__ __forceinline__ float spheres_value(const SdfDev& s, float x, float y
 
 __device__ __forceinline__ void spheres_grad(const SdfDev& s, float x, float y, float z, float g[3]) {
   float acc = 0.f, gx = 0.f, gy = 0.f, gz = 0.f;
-  const float* sp = s.spheres;
+  const ConstF* sp = (const ConstF*)s.spheres;
   for (int i = 0; i < s.n_spheres; ++i, sp += 16) {
     float qx = fmaf(sp[2], z, fmaf(sp[1], y, sp[0] * x)) - sp[9];
     float qy = fmaf(sp[5], z, fmaf(sp[4], y, sp[3] * x)) - sp[10];
