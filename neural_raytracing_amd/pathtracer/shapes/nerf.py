@@ -44,10 +44,20 @@ class NeRFLE(nn.Module):
         dev = flat.device
         # torch.linspace on the host: the same float32 sequence the CPU reference computes
         ts = torch.linspace(0, 2 + random.random() * 0.1, self.steps).to(dev)
-        if needs_grad(self):
+        if needs_grad(self, lights):
             if getattr(self, "envmap", False):
-                raise _lib.NrtError("NeRFLE(envmap=True) is not on the HIP training path")
-            light = lights.location.reshape(-1, 3)[0].detach().float().to(dev)
+                # nerf.py:183-191: the light's envmap at bins^2 directions (degree values passed
+                # as radians, as in the reference), differentiable in the light's parameters
+                if not hasattr(lights, "envmap"):
+                    raise _lib.NrtError("NeRFLE(envmap=True) needs PointLights (lights.envmap)")
+                from ..utils import elev_azim_to_dir
+                points = torch.stack(torch.meshgrid(
+                    torch.linspace(0, 180, self.bins, device=dev),
+                    torch.linspace(0, 45, self.bins, device=dev), indexing="ij"),
+                    dim=-1).reshape(-1, 2)
+                light = lights.envmap(elev_azim_to_dir(points)).reshape(-1).float()
+            else:
+                light = lights.location.reshape(-1, 3)[0].detach().float().to(dev)
             return self._forward_train(flat, ts, light).reshape(lead + (3,))
         lib = _lib.load(require_device=True)
         if getattr(self, "envmap", False):
@@ -73,7 +83,8 @@ class NeRFLE(nn.Module):
         return rgb.reshape(lead + (3,))
 
     def _forward_train(self, flat, ts, light):
-        """nerf.py:175-214 with autograd: both MLPs on the HIP MLP kernels
+        """nerf.py:175-214 with autograd (point light or envmap encoding
+        ``light``): both MLPs on the HIP MLP kernels
         with nrt_mlp_backward behind them; the sample points and the rolled-cumprod compositing
         are tensor ops in the reference's order.  FP32 intermediates [S, P, 65 / 70]."""
         o, d = flat[:, :3], flat[:, 3:]
@@ -81,7 +92,7 @@ class NeRFLE(nn.Module):
         first = self.first(pts)
         latent = first[..., 1:]
         alpha = first[..., 0, None]
-        light_enc = light.reshape(1, 1, 3).expand(latent.shape[:-1] + (3,))
+        light_enc = light.reshape(1, 1, -1).expand(latent.shape[:-1] + (light.numel(),))
         rgb = self.second(torch.cat([latent, d[None].expand(latent.shape[:-1] + (3,)), light_enc],
                                     dim=-1)).sigmoid()
         sigma = F.relu(alpha).squeeze(-1)

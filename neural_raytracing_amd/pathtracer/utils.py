@@ -45,6 +45,13 @@ def crop(img, u, v, size):
     return img[u:u + size, v:v + size, ...]
 
 
+def elev_azim_to_dir(elev_azim):
+    """utils.py:478-486."""
+    limit = math.pi - 1e-7
+    elev, azim = elev_azim.clamp(min=-limit, max=limit).split(1, dim=-1)
+    return torch.cat([azim.sin() * elev.cos(), azim.cos() * elev.cos(), elev.sin()], dim=-1)
+
+
 def dir_to_elev_azim(direc):
     """utils.py:490-494."""
     x, y, z = F.normalize(direc, dim=-1).clamp(min=-1 + 1e-7, max=1 - 1e-7).split(1, dim=-1)

@@ -335,7 +335,68 @@ def test_path_and_envmap_refuse_autograd():
         Path().sample(mine["shape"], rays, mine["bsdf"], lights=mine["lights"])
     nerf = NeRFLE(envmap=True, device="cuda")
     with pytest.raises(NrtError):
-        nerf(rays, PointLights(device="cuda"))
+        nerf(rays, mine["lights"])  # envmap needs a PointLights
+
+
+@pytest.mark.gpu
+def test_nerfle_envmap_training_gradients_match_oracle():
+    """NeRF+LE (envmap=True) with autograd: the colour MLP sees the point light's envmap at
+    bins^2 directions (nerf.py:183-191); both MLPs' gradients vs float64 oracle autograd."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from tests.test_gpu_parity import _nerfle_pair
+    ref, mine = _nerfle_pair(envmap=True)
+    for m in (ref.first, ref.second):
+        m.act_name = "softplus"
+    for m in (mine.first, mine.second):
+        m.activation = F.softplus
+    g = torch.Generator().manual_seed(9)
+    o = torch.tensor([0.0, 0.2, 1.2]) + 0.1 * torch.randn(1, 6, 5, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, 6, 5, 1, 2, generator=g) - 0.5,
+                               -torch.ones(1, 6, 5, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    w = torch.randn(1, 6, 5, 1, 3, generator=g)
+    loc = (0.3, 1.0, 0.2)
+    random.seed(4)
+    jitter = random.random()
+
+    def oracle(dtype):
+        r = copy.deepcopy(ref).to(dtype)
+        for sub in r.modules():
+            if hasattr(sub, "basis_p"):
+                sub.basis_p = sub.basis_p.to(dtype)
+        light = R.PointLightRef(location=loc)
+        for a in ("scale", "intensity", "location", "const", "linear", "square"):
+            setattr(light, a, getattr(light, a).to(dtype))
+        old = torch.get_default_dtype()
+        torch.set_default_dtype(dtype)
+        try:
+            out = r(rays.to(dtype), None, jitter=jitter, light=light)
+            (out * w.to(dtype)).sum().backward()
+        finally:
+            torch.set_default_dtype(old)
+        return out.detach(), {f"{n}.{k}{i}": getattr(a, "weight" if k == "W" else "bias").grad.double()
+                              for n, m in {"first": r.first, "second": r.second}.items()
+                              for i, a in enumerate([m.init, *m.layers, m.out]) for k in ("W", "b")}
+    want_img, want = oracle(torch.float64)
+    _, ref32 = oracle(torch.float32)
+    set_precision("fp32")
+    random.seed(4)
+    got_img = mine(rays.cuda(), PointLights(location=list(loc), device="cuda"))
+    assert got_img.requires_grad
+    assert (got_img.detach().cpu().double() - want_img).abs().max().item() <= 1e-4
+    (got_img * w.cuda()).sum().backward()
+    bad = []
+    for n, m in {"first": mine.first, "second": mine.second}.items():
+        for i, a in enumerate(m._linears()):
+            for k in ("W", "b"):
+                g64 = want[f"{n}.{k}{i}"]
+                gb = getattr(a, "weight" if k == "W" else "bias").grad.detach().cpu().double()
+                err = (gb - g64).abs().max().item()
+                e32 = (ref32[f"{n}.{k}{i}"] - g64).abs().max().item()
+                if err > max(2e-3 * g64.abs().max().item(), 4 * e32) + 1e-9:
+                    bad.append(f"{n}.{k}{i}: err {err:.3g} fp32 {e32:.3g}")
+    assert not bad, "\n".join(bad)
 
 
 @pytest.mark.gpu
