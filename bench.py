@@ -117,6 +117,51 @@ def build_scene(device, samples, seed=0):
                 pt=pt)
 
 
+def shape_mlp_sdf(mlp, radius=0.3, copies=40, seed=0):
+    """Give a randomly initialised SkipConnMLP(8, 256, in 3, out 1) a real zero level set.
+
+    A default-initialised deep softplus MLP is constant to ~1e-3 over the unit ball (its output
+    distribution collapses), so as an SDF every ray "hits" at t = 0.  This sets, in place:
+      * init: 6*copies "carry" units u = +-a_c x_i (a_c in [0.8, 1.2], one scale per copy);
+      * every hidden layer: the carry units pass through exactly, t' = softplus(t) - softplus(-t)
+        (weights +1 / -1 on the unit's pair, 0 on everything else incl. the skip encoding);
+      * out: sum_c k_c (softplus(t) + softplus(-t)) over the carry pairs, k_c = 2 / (a_c^2 copies),
+        minus the constant, so sdf(p) ~= (|p|^2 - radius^2) / 2 (the t^4 term makes the level set
+        slightly non-spherical); the remaining 256 - 6*copies units keep their random weights and
+        feed the output through weights x 0.02.
+    (|p|^2 - r^2)/2 never exceeds |p| - r inside |p| <= 2 - r, so sphere tracing from a camera at
+    distance ~1 never oversteps.  Works on the product SkipConnMLP and the oracle SkipMLP alike
+    (same init / layers / out names); FLOPs and shapes are unchanged."""
+    g = torch.Generator().manual_seed(seed)
+    H = mlp.init.out_features
+    nc = 6 * copies
+    assert nc <= H and mlp.in_size == 3
+    a = 0.8 + 0.4 * torch.rand(copies, generator=g)
+    log2 = math.log(2.0)
+    with torch.no_grad():
+        W = mlp.init.weight
+        W[:nc] = 0
+        mlp.init.bias[:nc] = 0
+        for c in range(copies):
+            for i in range(3):
+                W[6 * c + 2 * i, i] = a[c]
+                W[6 * c + 2 * i + 1, i] = -a[c]
+        for lin in mlp.layers:
+            lin.weight[:nc] = 0
+            lin.bias[:nc] = 0
+            for u in range(0, nc, 2):
+                lin.weight[u, u], lin.weight[u, u + 1] = 1.0, -1.0
+                lin.weight[u + 1, u + 1], lin.weight[u + 1, u] = 1.0, -1.0
+        mlp.out.weight.mul_(0.02)
+        const = 0.0
+        for c in range(copies):
+            k = 2.0 / (float(a[c]) ** 2 * copies)
+            mlp.out.weight[0, 6 * c:6 * c + 6] = k
+            const += k * 6 * log2
+        mlp.out.bias[0] = mlp.out.bias[0] * 0.02 - const - 0.5 * radius * radius
+    return mlp
+
+
 def oracle_scene(scene):
     """The same weights in the CPU oracle (cpu_baseline leg only)."""
     from oracle import pathtracer_ref as R
@@ -276,6 +321,9 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved / peak,
                 "traffic": traffic,
+                "traffic_source": (f"committed PMC pass, profiles/pmc_k_march16.json "
+                                   f"(FETCH_SIZE + WRITE_SIZE, {size}^2 {args.precision}); not "
+                                   "measured in this run") if traffic is not None else None,
                 "flop_per_launch": flop_launch,
                 "avg_kernel_ms": avg_kernel_ms,
                 "launches": k_n,
@@ -336,9 +384,7 @@ def build_other_scene(name, device, samples):
     if name == "dtu":
         sdf = SkipConnMLP(num_layers=8, hidden_size=256, in_size=3, out=1, freqs=16,
                           activation=F.softplus, device="cpu")
-        with torch.no_grad():
-            sdf.out.weight.mul_(0.1)
-            sdf.out.bias.add_(-0.3)  # a surface inside the unit ball
+        shape_mlp_sdf(sdf, radius=0.2)  # random init alone has no zero level set
         comps = [NeuralBSDF(activation=torch.nn.Sigmoid(), device="cpu") for _ in range(10)] + \
                 [Diffuse(preprocess=torch.sigmoid, device="cpu").random() for _ in range(6)]
         bsdf = ComposeSpatialVarying(comps, device="cpu")
@@ -570,9 +616,35 @@ def cpu_train_baseline(sdf, bsdf, lights, size, focal, args, crop=48):
     loss.backward()
     cpu_s = time.perf_counter() - t0
     return {"value": crop * crop * args.samples / cpu_s, "unit": "ray-samples/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": torch.get_num_threads(), **host_cpu(), "kind": "port",
             "sample": f"one view, {crop}x{crop} crop, {args.samples} march steps + scan, forward + "
                       f"backward (oracle/pathtracer_ref.py autograd), {cpu_s:.1f} s"}
+
+
+def host_cpu():
+    """lscpu-style description of the host the CPU baseline ran on: model name, physical cores
+    and logical CPUs of the machine (/proc/cpuinfo), next to ``cores`` = the torch threads the
+    oracle actually used (the box's CPU share: OMP_NUM_THREADS)."""
+    model, phys, logical = None, set(), 0
+    try:
+        with open("/proc/cpuinfo") as fh:
+            pid = core = None
+            for line in fh:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    logical += 1
+                elif k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    core = v
+                    phys.add((pid, core))
+    except OSError:
+        pass
+    return {"cpu_model": model, "physical_cores_on_host": len(phys) or None,
+            "logical_cpus_on_host": logical or None, "threads_used": torch.get_num_threads()}
 
 
 def rr_hit_fraction(rr):
@@ -643,7 +715,8 @@ def cpu_baseline(scene, size, args):
             maxdiff = (got - want.clamp(0, 1)).abs().max().item()
     nra.set_precision(args.precision)
     return {
-        "cpu_baseline": {"value": rate, "unit": "ray-samples/s", "cores": threads, "kind": "port",
+        "cpu_baseline": {"value": rate, "unit": "ray-samples/s", "cores": threads, **host_cpu(),
+                         "kind": "port",
                          "sample": f"{crop}x{crop} crop of the same frame, {args.samples} march steps + "
                                    f"coarse scan + shading, oracle/pathtracer_ref.py, {cpu_s:.1f} s"},
         "psnr_vs_ref": round(psnr[args.precision], 2),

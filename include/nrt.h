@@ -307,6 +307,23 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
                        const float* ts, int32_t S, const float* light, int32_t light_dim,
                        float* rgb, void* workspace, int precision, void* stream);
 
+/* PlainNeRF (shapes/nerf.py:9-74; replaces PlainNeRF.forward, nerf.py:46-74): per ray and depth
+ * ts[s] (the caller's linspace(0.4, 2 + random()*0.1, S)),
+ *   first_out = first(o + ts[s] d, latent[row])            (3 + latent L -> 1 + I)
+ *   rgb_s = tanh(second(dir_to_elev_azim(d), [first_out[1:], latent[row]]))   (2 + (I+L) -> 3)
+ *   sigma = relu(first_out[0] + noise[s * P + p])           (noise NULL: none; the reference
+ *                                                              draws randn * 1e-3, nerf.py:66)
+ * composited with the NeRFLE weights, rgb[p] = (sum_s w_s rgb_s + 1) / 2.  latent is [rows, L]
+ * device memory; ray p uses row p / rays_per_latent (the reference's latent[None, :, None, None,
+ * None] indexes the camera axis of [N, W, H, B] rays: rays_per_latent = W*H*B).
+ * workspace: nrt_plain_nerf_workspace_bytes(first, second, P, S) bytes. */
+size_t nrt_plain_nerf_workspace_bytes(const nrt_mlp* first, const nrt_mlp* second, int64_t P,
+                                      int32_t S);
+int nrt_plain_nerf_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays,
+                           int64_t P, const float* ts, int32_t S, const float* latent,
+                           int64_t rays_per_latent, const float* noise, float* rgb,
+                           void* workspace, int precision, void* stream);
+
 /* NeRFLE's envmap light encoding (nerf.py:183-191): PointLights.envmap (lights.py:81-88) at
  * elev_azim_to_dir (utils.py:478-486) of meshgrid(linspace(0, 180, bins), linspace(0, 45, bins))
  * -> out[bins^2 * 3] (device).  Point lights only (NRT_EUNSUPPORTED otherwise). */

@@ -90,6 +90,8 @@ _SIGNATURES = {
     "nrt_nerfle_workspace_bytes": (ctypes.c_size_t, [_I64, _I32, _I32]),
     "nrt_nerfle_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _I32, _P, _P, _I32, _P]),
     "nrt_light_envmap": (_I32, [_P, _I32, _P, _P]),
+    "nrt_plain_nerf_workspace_bytes": (ctypes.c_size_t, [_P, _P, _I64, _I32]),
+    "nrt_plain_nerf_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _I64, _P, _P, _P, _I32, _P]),
     "nrt_mlp_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_mlp_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "nrt_mlp_grad_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),

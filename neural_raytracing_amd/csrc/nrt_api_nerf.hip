@@ -161,6 +161,87 @@ __global__ void k_nerf_composite_rm(const float* __restrict__ alpha_raw,
 static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // ------------------------------------------------------------------------------------------
+// PlainNeRF (shapes/nerf.py:9-74): latent-conditioned density MLP + direction MLP, tanh colours
+// ------------------------------------------------------------------------------------------
+// first MLP input of sample i = s * P + p: pts (3) and the latent row of the ray's camera
+// (self.latent[None, :, None, None, None, :], nerf.py:52; row = p / rays_per_latent)
+template <int = 0>
+__global__ void k_plain_first_in(const float* __restrict__ rays, int64_t P,
+                                 const float* __restrict__ ts, int S,
+                                 const float* __restrict__ latent, int L, int64_t rays_per_latent,
+                                 float* __restrict__ pts, float* __restrict__ lat1) {
+  const int64_t n = (int64_t)S * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = i / P, p = i - s * P;
+    const float t = ts[s];
+    const float* r = rays + p * 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pts[i * 3 + k] = __fadd_rn(r[k], __fmul_rn(t, r[3 + k]));
+    const float* lr = latent + (p / rays_per_latent) * L;
+    for (int k = 0; k < L; ++k) lat1[i * L + k] = lr[k];
+  }
+}
+
+// second MLP input: x = dir_to_elev_azim(r_d) (utils.py:490-494), latent = [intermediate, latent]
+// (nerf.py:60-64; first_out = [alpha | intermediate (I)])
+template <int = 0>
+__global__ void k_plain_second_in(const float* __restrict__ first_out, int I,
+                                  const float* __restrict__ rays, int64_t P, int S,
+                                  const float* __restrict__ latent, int L, int64_t rays_per_latent,
+                                  float* __restrict__ x2, float* __restrict__ lat2) {
+  const int64_t n = (int64_t)S * P;
+  const int L2 = I + L;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = i % P;
+    float elev, azim;
+    dir_elev_azim(rays[p * 6 + 3], rays[p * 6 + 4], rays[p * 6 + 5], elev, azim);
+    x2[i * 2] = elev;
+    x2[i * 2 + 1] = azim;
+    const float* f = first_out + i * (1 + I);
+    float* o = lat2 + i * L2;
+    for (int k = 0; k < I; ++k) o[k] = f[1 + k];
+    const float* lr = latent + (p / rays_per_latent) * L;
+    for (int k = 0; k < L; ++k) o[I + k] = lr[k];
+  }
+}
+
+// nerf.py:64-74: rgb = tanh(second), sigma = relu(alpha + noise), the NeRFLE weights (absolute
+// depth, rolled cumprod with the last entry 1), out = (sum_s w_s rgb_s + 1) / 2
+template <int = 0>
+__global__ void k_plain_composite(const float* __restrict__ first_out, int astride,
+                                  const float* __restrict__ noise, const float* __restrict__ rgb_raw,
+                                  const float* __restrict__ ts, int64_t P, int S,
+                                  float* __restrict__ out) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    auto alpha_at = [&](int s) {
+      const int64_t i = (int64_t)s * P + p;
+      float a = first_out[i * astride];
+      if (noise) a = a + noise[i];
+      const float sig = fmaxf(a, 0.f);
+      return 1.f - expf(-(sig * ts[s]));
+    };
+    float cp = 1.f;
+    for (int s = 0; s < S; ++s) cp = cp * fmaxf(1.f - alpha_at(s), 1e-10f);
+    const float cp_last = cp;
+    float acc[3] = {0.f, 0.f, 0.f};
+    float prev = 1.f;
+    for (int s = 0; s < S; ++s) {
+      const int64_t i = (int64_t)s * P + p;
+      const float a = alpha_at(s);
+      const float w = s == S - 1 ? a * 1.f : (s == 0 ? a * cp_last : a * prev);
+      prev = prev * fmaxf(1.f - a, 1e-10f);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) acc[k] += w * tanhf(rgb_raw[i * 3 + k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) out[p * 3 + k] = (acc[k] + 1.f) / 2.f;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Fused FP16 NeRFLE sample kernel on the k-outer program engine (ring::KEngine): per wave 32
 // samples (columns, ray-major: sample g = p * S + s); both MLPs, the second MLP's Fourier
 // projection and its input assembly stay in registers; only alpha_raw and rgb_raw (16 B per
@@ -585,6 +666,61 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   k_nerf_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(
       f1, 65, c2, ts, P, S, rgb);
   return check_launch("k_nerf_composite");
+}
+
+size_t nrt_plain_nerf_workspace_bytes(const nrt_mlp* first, const nrt_mlp* second, int64_t P,
+                                      int32_t S) {
+  if (!first || !second) return 0;
+  const size_t n = (size_t)std::max<int64_t>(P, 1) * (size_t)std::max(S, 1);
+  const size_t L1 = (size_t)std::max(first->desc.latent, 0);
+  const size_t L2 = (size_t)std::max(second->desc.latent, 0);
+  const size_t O1 = (size_t)std::max(first->desc.out, 1);
+  return a256(n * 3 * 4) + a256(n * L1 * 4) + a256(n * O1 * 4) + a256(n * 2 * 4) +
+         a256(n * L2 * 4) + a256(n * 3 * 4);
+}
+
+int nrt_plain_nerf_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays,
+                           int64_t P, const float* ts, int32_t S, const float* latent,
+                           int64_t rays_per_latent, const float* noise, float* rgb,
+                           void* workspace, int precision, void* stream) {
+  if (!first || !second || P < 0 || S < 1 || rays_per_latent < 1) {
+    set_error("nrt_plain_nerf_forward: bad argument");
+    return NRT_EINVAL;
+  }
+  if (P == 0) return NRT_OK;
+  if (!rays || !ts || !latent || !rgb || !workspace) {
+    set_error("nrt_plain_nerf_forward: null argument");
+    return NRT_EINVAL;
+  }
+  const int L = first->desc.latent, I = first->desc.out - 1;
+  if (first->desc.in_size != 3 || L < 1 || I < 0 || second->desc.in_size != 2 ||
+      second->desc.latent != I + L || second->desc.out != 3) {
+    set_error("nrt_plain_nerf_forward: expects first 3 (+latent L) -> 1 + I and second 2 "
+              "(+latent I + L) -> 3 (nerf.py:23-39)");
+    return NRT_EINVAL;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const size_t n = (size_t)P * S;
+  char* ws = (char*)workspace;
+  float* pts = (float*)ws;            ws += a256(n * 3 * 4);
+  float* lat1 = (float*)ws;           ws += a256(n * L * 4);
+  float* f1 = (float*)ws;             ws += a256(n * (1 + I) * 4);
+  float* x2 = (float*)ws;             ws += a256(n * 2 * 4);
+  float* lat2 = (float*)ws;           ws += a256(n * (I + L) * 4);
+  float* c2 = (float*)ws;
+  const int blocks = (int)std::min<int64_t>(ceil_div64((int64_t)n, 256), 4096);
+  ProfScope prof("k_plain_nerf", st);
+  k_plain_first_in<><<<dim3(blocks), dim3(256), 0, st>>>(rays, P, ts, S, latent, L,
+                                                          rays_per_latent, pts, lat1);
+  if (int rc = check_launch("k_plain_first_in")) return rc;
+  if (int rc = nrt_mlp_forward(first, pts, lat1, (int64_t)n, f1, precision, stream)) return rc;
+  k_plain_second_in<><<<dim3(blocks), dim3(256), 0, st>>>(f1, I, rays, P, S, latent, L,
+                                                           rays_per_latent, x2, lat2);
+  if (int rc = check_launch("k_plain_second_in")) return rc;
+  if (int rc = nrt_mlp_forward(second, x2, lat2, (int64_t)n, c2, precision, stream)) return rc;
+  k_plain_composite<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 4096)), dim3(256), 0, st>>>(
+      f1, 1 + I, noise, c2, ts, P, S, rgb);
+  return check_launch("k_plain_composite");
 }
 
 }  // extern "C"

@@ -375,11 +375,18 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   return w;
 }
 
+// One rocBLAS handle per (thread, device): a handle is bound to the device that was current when
+// it was created, and rocblas_set_stream + the GEMM sequence that follows must not interleave
+// with another thread's.  Handles live for the process.
 rocblas_handle blas() {
-  static rocblas_handle h = nullptr;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> g(mu);
-  if (!h && rocblas_create_handle(&h) != rocblas_status_success) h = nullptr;
+  thread_local std::vector<std::pair<int, rocblas_handle>> handles;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  for (auto& e : handles)
+    if (e.first == dev) return e.second;
+  rocblas_handle h = nullptr;
+  if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+  handles.emplace_back(dev, h);
   return h;
 }
 

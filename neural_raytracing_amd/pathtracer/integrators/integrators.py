@@ -142,11 +142,13 @@ class Direct(Integrator):
         hit_idx, hit_count, flat = it._nrt_hits
         P = flat.shape[0]
         rgb = result.reshape(P, 3)
-        nb = len(getattr(bsdf, "bsdfs", [bsdf]))
-        weights = torch.zeros(P, nb, device=rays.device)
+        # it.normalized_weights / nonnormalized_weights (bsdfs.py:516-536: sigmoid(sp_var_fn(p))
+        # on EVERY ray, misses included) are evaluated on first access (HipInteraction), so a
+        # render that never reads them pays nothing for them
+        it._nrt_spatial = bsdf
         args = (_lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
                 _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
-                _lib.ptr(rgb), _lib.ptr(weights))
+                _lib.ptr(rgb), None)
         if shadow:
             # sample_emitter_dir_w_isect (scene.py:290-298): shadow ray to the point light,
             # marched like SDF.intersect_test (sdfs.py:162-181); with an occlusion MLP,
@@ -166,7 +168,6 @@ class Direct(Integrator):
         else:
             _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), *args,
                       _lib.precision_code(), _lib.stream())
-        setattr(it, "normalized_weights", weights.reshape(rays.shape[:-1] + (nb,)))
         return result, active, it
 
 

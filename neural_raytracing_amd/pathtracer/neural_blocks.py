@@ -118,6 +118,21 @@ def _mlp_forward(mlp, x, lat, handle=None):
     return y
 
 
+def _save_versions(ctx, params):
+    """The backward kernels read the packed copy of the weights (the training handle, re-packed in
+    place by nrt_mlp_refresh after an optimiser step), not saved tensors, so autograd's own
+    saved-tensor version check cannot see an in-place update: keep the versions and compare."""
+    ctx.param_refs = params
+    ctx.param_versions = tuple(q._version for q in params)
+
+
+def _check_versions(ctx):
+    if tuple(q._version for q in ctx.param_refs) != ctx.param_versions:
+        raise RuntimeError("one of the variables needed for gradient computation has been "
+                           "modified by an inplace operation: a SkipConnMLP weight changed "
+                           "(e.g. optimizer.step()) between this graph's forward and backward")
+
+
 class _MlpFn(torch.autograd.Function):
     """y = SkipConnMLP(x, latent) with gradients for x, latent and every nn.Linear weight and
     bias from nrt_mlp_backward.  basis_p is a plain tensor attribute in the
@@ -130,6 +145,7 @@ class _MlpFn(torch.autograd.Function):
             y = _mlp_forward(mlp, x.detach(), None if lat is None else lat.detach(), handle)
         ctx.mlp = mlp
         ctx.handle = handle  # the packed weights this forward used
+        _save_versions(ctx, params)
         ctx.has_lat = lat is not None
         ctx.save_for_backward(x, lat if lat is not None else x.new_empty(0))
         return y
@@ -137,6 +153,7 @@ class _MlpFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         import ctypes
+        _check_versions(ctx)
         x, lat = ctx.saved_tensors
         lat = lat if ctx.has_lat else None
         mlp = ctx.mlp
@@ -210,12 +227,14 @@ class _InputGradFn(torch.autograd.Function):
             g = _input_grad(mlp, x.detach(), handle)
         ctx.mlp = mlp
         ctx.handle = handle
+        _save_versions(ctx, params)
         ctx.save_for_backward(x)
         return g
 
     @staticmethod
     def backward(ctx, dg):
         import ctypes
+        _check_versions(ctx)
         (x,) = ctx.saved_tensors
         mlp = ctx.mlp
         lib = _lib.load(require_device=True)

@@ -12,6 +12,81 @@ from ..differentiable import needs_grad
 from ..neural_blocks import SkipConnMLP
 
 
+class PlainNeRF(nn.Module):
+    """A latent-conditioned NeRF (nerf.py:9-74), rendered by ``nrt_plain_nerf_forward``.
+
+    Constructor and RNG order follow nerf.py:10-39 (``first``: 3 (+latent) -> 1 + intermediate,
+    ``second``: elev/azim (+intermediate, latent) -> 3, both 5 x 32).  ``forward(rays, lights)``
+    draws ``random.random()`` for ``ts = linspace(0.4, 2 + r*0.1, steps)`` and the density noise
+    ``randn * 1e-3`` per sample (nerf.py:50, :66; on the device, ``noise=`` injects it) and
+    returns ``(rgb + 1) / 2`` with the reference's compositing.  ``lights`` is unused, as there.
+    """
+
+    MAX_SAMPLES_PER_CALL = 1 << 22
+
+    def __init__(self, latent_size: int = 32, intermediate_size: int = 32, steps=32,
+                 device="cuda"):
+        super().__init__()
+        self.latent = None
+        self.latent_size = latent_size
+        self.steps = steps
+        self.first = SkipConnMLP(in_size=3, out=1 + intermediate_size, latent_size=latent_size,
+                                 num_layers=5, hidden_size=32, device=device).to(device)
+        self.second = SkipConnMLP(in_size=2, out=3, latent_size=latent_size + intermediate_size,
+                                  num_layers=5, hidden_size=32, device=device).to(device)
+
+    def assign_latent(self, latent):
+        assert latent.shape[-1] == self.latent_size
+        assert len(latent.shape) == 2, "expected latent in [B, L]"
+        self.latent = latent
+
+    def forward(self, rays, lights=None, noise=None):
+        assert self.latent is not None
+        if not rays.is_cuda:
+            raise _lib.NrtError("PlainNeRF renders on the HIP path only: move it and the rays to "
+                                "the GPU")
+        if needs_grad(self) or (torch.is_grad_enabled() and self.latent.requires_grad):
+            raise _lib.NrtError("PlainNeRF is not on the HIP training path: render it under "
+                                "torch.no_grad()")
+        lead = rays.shape[:-1]
+        if len(lead) < 2 or lead[0] != self.latent.shape[0]:
+            raise _lib.NrtError(f"PlainNeRF: rays {tuple(rays.shape)} must be [N, ..., 6] with "
+                                f"N = latent rows ({self.latent.shape[0]})")
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        dev = flat.device
+        S = self.steps
+        ts = torch.linspace(0.4, 2 + random.random() * 0.1, S).to(dev)
+        if noise is None:
+            noise = torch.randn(S, P, device=dev) * 1e-3
+        noise = noise.reshape(S, P).float().contiguous()
+        latent = self.latent.detach().float().to(dev).contiguous()
+        per = P // lead[0]
+        lib = _lib.load(require_device=True)
+        rgb = torch.empty(P, 3, device=dev)
+        # bounded intermediates: chunks of whole cameras, or pieces of one camera's rays (the
+        # kernel maps chunk ray p to latent row p / rays_per_latent of the chunk's rows)
+        cmax = max(1, self.MAX_SAMPLES_PER_CALL // S)
+        first, second = self.first.nrt(), self.second.nrt()
+        ws = torch.empty(lib.nrt_plain_nerf_workspace_bytes(first, second, min(cmax, P), S),
+                         dtype=torch.uint8, device=dev)
+        r0 = 0
+        while r0 < P:
+            cam = r0 // per
+            if per <= cmax:
+                n = min((cmax // per) * per, P - r0)
+                lat, rpl = latent[cam:cam + n // per], per
+            else:
+                n = min(cmax, (cam + 1) * per - r0)
+                lat, rpl = latent[cam:cam + 1], n
+            _lib.call("nrt_plain_nerf_forward", first, second, _lib.ptr(flat[r0:r0 + n]), n,
+                      _lib.ptr(ts), S, _lib.ptr(lat.contiguous()), rpl,
+                      _lib.ptr(noise[:, r0:r0 + n].contiguous()), _lib.ptr(rgb[r0:r0 + n]),
+                      _lib.ptr(ws), _lib.precision_code(), _lib.stream())
+            r0 += n
+        return rgb.reshape(lead + (3,))
+
+
 class NeRFLE(nn.Module):
     """NeRF with a point-light emitter input (nerf.py:153-214).
 

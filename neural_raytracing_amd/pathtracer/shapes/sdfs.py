@@ -112,6 +112,42 @@ class HipInteraction(MixedInteraction):
             return None
         return self._nrt_raw[hit]
 
+    # ComposeSpatialVarying.eval_and_pdf / normalized_weights (bsdfs.py:515-536) set these on
+    # the interaction for every ray of the tile, misses included; Direct.sample returns before
+    # shading (and sets neither) when nothing was hit (integrators.py:171).  The fused path
+    # evaluates them on first access: sp_var_fn(preprocess(p)) on the HIP MLP kernel.
+    def _spatial_raw(self):
+        d = self.__dict__
+        if "nonnormalized_weights" in d:
+            return d["nonnormalized_weights"]
+        bsdf = d.get("_nrt_spatial")
+        sp = getattr(bsdf, "sp_var_fn", None)
+        if sp is None or not bool(self._nrt_hit_mask.any()):
+            raise AttributeError("nonnormalized_weights")
+        p = self.p
+        w = sp(bsdf.preprocess(p)).reshape(p.shape[:-1] + (len(bsdf.bsdfs),))
+        d["nonnormalized_weights"] = w
+        return w
+
+    @property
+    def nonnormalized_weights(self):
+        return self._spatial_raw()
+
+    @nonnormalized_weights.setter
+    def nonnormalized_weights(self, v):
+        self.__dict__["nonnormalized_weights"] = v
+
+    @property
+    def normalized_weights(self):
+        d = self.__dict__
+        if "normalized_weights" not in d:
+            d["normalized_weights"] = self._spatial_raw().sigmoid()
+        return d["normalized_weights"]
+
+    @normalized_weights.setter
+    def normalized_weights(self, v):
+        self.__dict__["normalized_weights"] = v
+
 
 class SDF:
     """A general SDF shape with sphere-tracing intersection (sdfs.py:89-277)."""

@@ -992,3 +992,53 @@ class NeRFLERef(nn.Module):
         cp[-1, ...] = 1
         w = alpha * cp
         return (w[..., None] * rgb).sum(dim=0)
+
+
+class PlainNeRFRef(nn.Module):
+    """PlainNeRF, nerf.py:9-74: a latent-conditioned NeRF.
+
+    ``first = SkipMLP(3 -> 1 + intermediate, latent)`` (5 x 32), ``second = SkipMLP(2 -> 3,
+    latent = intermediate + latent)`` (5 x 32) on ``dir_to_elev_azim(r_d)``; ``tanh`` colours,
+    ``ts = linspace(0.4, 2 + random()*0.1, steps)``, ``sigma = relu(alpha + randn*1e-3)`` (the
+    noise is injectable: ``noise`` [S, N, W, H, B, 1]), the same rolled-cumprod weights as NeRFLE
+    and the output ``(rgb + 1) / 2``.  ``latent`` is [N, latent_size]: row n conditions camera n
+    (``self.latent[None, :, None, None, None, :]``, :52).
+    """
+
+    def __init__(self, latent_size=32, intermediate_size=32, steps=32):
+        super().__init__()
+        self.latent = None
+        self.latent_size = latent_size
+        self.steps = steps
+        self.first = SkipMLP(in_size=3, out=1 + intermediate_size, latent_size=latent_size,
+                             num_layers=5, hidden_size=32)
+        self.second = SkipMLP(in_size=2, out=3, latent_size=latent_size + intermediate_size,
+                              num_layers=5, hidden_size=32)
+
+    def assign_latent(self, latent):
+        assert latent.shape[-1] == self.latent_size and latent.dim() == 2
+        self.latent = latent
+
+    def forward(self, rays, lights=None, jitter=None, noise=None):
+        r_o, r_d = rays.split([3, 3], dim=-1)
+        if jitter is None:
+            jitter = random.random()
+        ts = torch.linspace(0.4, 2 + jitter * 0.1, self.steps)
+        pts = r_o.unsqueeze(0) + torch.tensordot(ts, r_d, dims=0)
+        latent = self.latent[None, :, None, None, None, :].expand(pts.shape[:-1] + (-1,))
+        first_out = self.first(pts, latent)
+        alpha = first_out[..., 0, None]
+        intermediate = first_out[..., 1:]
+        ea = dir_to_elev_azim(r_d)
+        rgb = self.second(ea[None, ...].expand(latent.shape[:-1] + (2,)),
+                          torch.cat([intermediate, latent], dim=-1)).tanh()
+        if noise is None:
+            noise = torch.randn_like(alpha) * 1e-3
+        sigma = F.relu(alpha + noise).squeeze(-1)
+        alpha = 1 - torch.exp(-sigma * ts[:, None, None, None, None].expand_as(sigma))
+        cp = torch.cumprod((1 - alpha).clamp(min=1e-10), dim=0)
+        cp = torch.roll(cp, 1, 0)
+        cp[-1, ...] = 1
+        w = alpha * cp
+        rgb_out = (w[..., None] * rgb).sum(dim=0)
+        return (rgb_out + 1) / 2

@@ -1,0 +1,385 @@
+"""Parity of the BASELINE.json configurations the first round left untested:
+
+* cfg2 / cfg4's bare ``SkipConnMLP(8, 256, F=16, softplus)`` SDF (``nrt_sdf_create_mlp``) marched by
+  the FP32 ``k_intersect`` and the FP16 ring ``k_march16``: t, hit, throughput and normals;
+* the metric configuration itself (800x800 frame, 64 march steps + the 130-eval scan, 8x256
+  SDF MLP, the nerf_synthetic shading stack) on a 64x64 crop, FP32 and FP16;
+* a DTU-like render (DTUCamera + 8x256 MLP SDF + NeuralBSDF(sigmoid) x 10 + Diffuse(sigmoid) x 6 +
+  LightField + NeRFIntegrator(Direct)) on a crop across the silhouette;
+* NeRFLE at 256 depths (cfg5);
+* PlainNeRF (nerf.py:9-74);
+* ``it.normalized_weights`` on every ray of the fused Direct path (bsdfs.py:515-536).
+
+FP32 bar: 1e-4 abs on pixels / rays whose hit flag agrees; the flip count (rays whose hit flag
+differs between the HIP march and the oracle's, from ulp-level differences at silhouettes) is
+reported (tests/report.py) and bounded.  FP16: PSNR against the oracle.
+"""
+import math
+import random
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import bench
+from oracle import pathtracer_ref as R
+from tests.helpers import copy_mlp, product_mlp_like, seeded
+from tests.report import report
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    yield
+    set_precision("fp32")
+
+
+def _psnr(a, b):
+    mse = ((a.clamp(0, 1) - b.clamp(0, 1)) ** 2).mean().item()
+    return -10 * math.log10(max(mse, 1e-12))
+
+
+# ------------------------------------------------------------------------------------------
+# (a) the bare 8x256 MLP SDF
+# ------------------------------------------------------------------------------------------
+
+def _mlp_sdf_pair(seed=41, radius=0.3):
+    seeded(seed)
+    ref = R.SkipMLP(num_layers=8, hidden_size=256, out=1, freqs=16, activation="softplus")
+    bench.shape_mlp_sdf(ref, radius=radius)
+    return ref, product_mlp_like(ref, "softplus")
+
+
+def _camera_rays(n, seed, eye=(0.0, 0.1, 1.0), spread=0.9):
+    g = torch.Generator().manual_seed(seed)
+    o = torch.tensor(eye).expand(1, n, n, 1, 3)
+    d = F.normalize(torch.cat([torch.rand(1, n, n, 1, 2, generator=g) * spread - spread / 2,
+                               -torch.ones(1, n, n, 1, 1)], -1), dim=-1)
+    return torch.cat([o, d], -1)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_bare_mlp_sdf_march_matches_oracle(prec):
+    """SDF(sdf=SkipConnMLP 8x256) -- the kind cfg2/cfg4 march -- vs MarchedSDF on sdf(p)[..., 0]
+    (sdfs.py:111-160, 232-249; the reference's SDF wants a [...] output, so the bare MLP's single
+    output column is the distance)."""
+    from neural_raytracing_amd import set_precision, _lib
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    ref, mine = _mlp_sdf_pair()
+    rays = _camera_rays(40, 3)
+    set_precision(prec)
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    random.seed(12)
+    with torch.no_grad():
+        it, hit = SDF(sdf=mine, max_steps=64).intersect(rays.cuda(), primary=True)
+    ring_launches = _lib.profile_read("k_normal16")[1]
+    _lib.profile_enable(False)
+    if prec == "fp16":
+        assert ring_launches >= 1, "the FP16 bare-MLP SDF must run on the ring engine"
+    random.seed(12)
+    jit = random.random()
+    with torch.no_grad():
+        rit, rhit = R.MarchedSDF(sdf=lambda p: ref(p)[..., 0], max_steps=64).intersect(
+            rays, primary=True, jitter=jit)
+    hit, rhit = hit.cpu().reshape(-1), rhit.reshape(-1)
+    flips = int((hit != rhit).sum())
+    m = hit & rhit
+    t_err = (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max().item()
+    n_err = (it.n.cpu().reshape(-1, 3)[m] - rit.n.reshape(-1, 3)[m]).abs().max().item()
+    p_err = (it.p.cpu().reshape(-1, 3)[m] - rit.p.reshape(-1, 3)[m]).abs().max().item()
+    thr = (it.throughput.cpu().reshape(-1) - rit.throughput.reshape(-1)).abs()
+    report(f"bare_mlp_sdf_march[{prec}]", rays=hit.numel(), hits=int(rhit.sum()), flips=flips,
+           t_maxabs=t_err, n_maxabs=n_err, p_maxabs=p_err, thr_maxabs=thr.max().item())
+    assert 0.15 < rhit.float().mean() < 0.85
+    if prec == "fp32":
+        assert flips <= 0.005 * hit.numel()
+        assert t_err <= 1e-4 and p_err <= 1e-4 and n_err <= 1e-4
+        # throughput = -1000 sdf(best): 1e-4 abs on sdf is 0.1 here
+        assert (thr <= 0.1).float().mean() >= 0.995
+    else:
+        assert flips <= 0.03 * hit.numel()
+        assert t_err <= 2e-2
+        cos = (it.n.cpu().reshape(-1, 3)[m] * rit.n.reshape(-1, 3)[m]).sum(-1)
+        assert (cos > math.cos(math.radians(2.0))).float().mean() > 0.99
+        assert (thr <= 10.0).float().mean() >= 0.95
+
+
+def test_bare_mlp_sdf_scan_free_matches_oracle():
+    """primary=False (no coarse scan; Path's secondary rays, cfg2's scan-free variant)."""
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    ref, mine = _mlp_sdf_pair(seed=43)
+    rays = _camera_rays(32, 5)
+    with torch.no_grad():
+        it, hit = SDF(sdf=mine, max_steps=64).intersect(rays.cuda(), primary=False)
+        rit, rhit = R.MarchedSDF(sdf=lambda p: ref(p)[..., 0], max_steps=64).intersect(
+            rays, primary=False)
+    hit, rhit = hit.cpu().reshape(-1), rhit.reshape(-1)
+    m = hit & rhit
+    report("bare_mlp_sdf_scan_free[fp32]", rays=hit.numel(), flips=int((hit != rhit).sum()))
+    assert int((hit != rhit).sum()) <= 0.005 * hit.numel()
+    assert (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max().item() <= 1e-4
+
+
+# ------------------------------------------------------------------------------------------
+# (b) the metric configuration at S = 64
+# ------------------------------------------------------------------------------------------
+
+def _hit_masks(prod_shape, oracle_shape, prod_rays, oracle_rays):
+    with torch.no_grad():
+        _, h = prod_shape.intersect(prod_rays, primary=False)
+        o, d = oracle_rays.split(3, dim=-1)
+        _, rh = oracle_shape.march(o, d)
+    return h.cpu().reshape(-1), rh.reshape(-1)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_metric_config_crop_matches_oracle(prec):
+    """bench.py's headline scene (800x800 NeRFCamera frame, SDF = one-sphere prior + 8x256
+    softplus shift MLP, 64 march steps + 130-eval coarse scan, ComposeSpatialVarying of 8
+    NeuralBSDF(Softplus) + 16x256 spatial MLP, LightField 10x256, NeRFIntegrator(Direct)) on the
+    64x64 crop across the silhouette (rows 368.., columns 72..), vs the oracle with the same
+    weights."""
+    import neural_raytracing_amd as nra
+    scene = bench.build_scene("cuda", samples=64, seed=0)
+    pt = scene["pt"]
+    size, crop = 800, 64
+    c0, c1 = (size - crop) // 2, 72
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    c2w = bench.view_c2w(0, 1).unsqueeze(0)
+    osc = bench.oracle_scene(scene)
+    ocam = R.NeRFCameraRef(c2w, focal)
+    random.seed(5)
+    with torch.no_grad():
+        want = R.render(osc["shape"], osc["lights"], ocam, osc["integrator"], osc["bsdf"],
+                        size=size, chunk_size=size, background=0.0, with_noise=0.0,
+                        crop=(c0, c1, crop))
+    cam = pt.cameras.NeRFCamera(cam_to_world=c2w.cuda(), focal=focal)
+    nra.set_precision(prec)
+    random.seed(5)
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(scene["shape"], scene["lights"], cam, scene["integrator"],
+                                     bsdf=scene["bsdf"], size=size, chunk_size=size,
+                                     bundle_size=1, crop_size=crop, uv=(c0, c1), background=0,
+                                     with_noise=0.0)
+    got = got.cpu()
+    assert got.shape == want.shape == (crop, crop, 4)
+    h, rh = _hit_masks(scene["shape"], osc["shape"],
+                       cam.rays_tile(c0, c1, crop, crop, size),
+                       ocam.sample_positions(R._tile_positions(c0, c1, crop), size))
+    agree = (h == rh).reshape(crop, crop)
+    err = (got - want).abs().amax(-1)
+    psnr = _psnr(got, want)
+    report(f"metric_config_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()),
+           flips=int((~agree).sum()), maxabs_agreeing=err[agree].max().item(),
+           pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
+    assert 0.1 < rh.float().mean() < 0.95
+    if prec == "fp32":
+        assert int((~agree).sum()) <= 0.005 * crop * crop
+        assert err[agree].max().item() <= 1e-4
+    else:
+        assert psnr > 40, psnr
+
+
+# ------------------------------------------------------------------------------------------
+# (c) a DTU-like render (cfg4 on a crop)
+# ------------------------------------------------------------------------------------------
+
+def _dtu_oracle(sc):
+    from neural_raytracing_amd.pathtracer.bsdf import NeuralBSDF
+    ref_mlp = R.SkipMLP(num_layers=8, hidden_size=256, out=1, freqs=16, activation="softplus")
+    bench._copy_to_oracle(ref_mlp, sc["shape"].sdf)
+    parts = []
+    for b in sc["bsdf"].bsdfs:
+        if isinstance(b, NeuralBSDF):
+            o = R.NeuralBSDFRef(activation="sigmoid")
+            bench._copy_to_oracle(o.mlp, b.mlp)
+        else:
+            o = R.DiffuseRef(reflectance=b.reflectance.detach().cpu().tolist(),
+                             preprocess="sigmoid")
+        parts.append(o)
+    bsdf = R.SpatialMixBSDF(parts)
+    bench._copy_to_oracle(bsdf.sp_var_fn, sc["bsdf"].sp_var_fn)
+    lights = R.LightFieldRef()
+    bench._copy_to_oracle(lights.light_field_approx, sc["lights"].light_field_approx)
+    with torch.no_grad():
+        lights.color.copy_(sc["lights"].color.detach().cpu())
+    cam = R.DTUCameraRef(sc["cameras"].pose.cpu(), sc["cameras"].intrinsic.cpu())
+    shape = R.MarchedSDF(sdf=lambda p: ref_mlp(p)[..., 0], max_steps=sc["shape"].max_steps)
+    return dict(shape=shape, bsdf=bsdf, lights=lights, camera=cam,
+                integrator=R.NeRFIntegratorRef(R.DirectRef()))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_dtu_like_render_matches_oracle(prec):
+    """cfg4 (dtu.py:91-113 with a synthetic DTU pinhole): DTUCamera (fx = fy = 2890, cx = 800,
+    cy = 600 on the 1600x1200 sensor) + 8x256 MLP SDF + ComposeSpatialVarying([NeuralBSDF(
+    sigmoid) x 10, Diffuse(sigmoid) x 6]) + LightField + NeRFIntegrator(Direct), on a 48x48 crop of
+    the 800x800 frame that straddles the silhouette."""
+    import neural_raytracing_amd as nra
+    import neural_raytracing_amd.pathtracer as pt
+    sc = bench.build_other_scene("dtu", torch.device("cuda"), 64)
+    osc = _dtu_oracle(sc)
+    size, crop, uv = 800, 48, (376, 82)
+    random.seed(6)
+    with torch.no_grad():
+        want = R.render(osc["shape"], osc["lights"], osc["camera"], osc["integrator"], osc["bsdf"],
+                        size=size, chunk_size=size, background=0.0, crop=(uv[0], uv[1], crop))
+    nra.set_precision(prec)
+    random.seed(6)
+    with torch.no_grad():
+        got, _ = pt.pathtrace_sample(sc["shape"], sc["lights"], sc["cameras"], sc["integrator"],
+                                     bsdf=sc["bsdf"], size=size, chunk_size=size, bundle_size=1,
+                                     crop_size=crop, uv=uv, background=0, with_noise=0.0)
+    got = got.cpu()
+    assert got.shape == want.shape == (crop, crop, 4)
+    h, rh = _hit_masks(sc["shape"], osc["shape"], sc["cameras"].rays_tile(uv[0], uv[1], crop, crop, size),
+                       osc["camera"].sample_positions(R._tile_positions(uv[0], uv[1], crop), size))
+    agree = (h == rh).reshape(crop, crop)
+    err = (got - want).abs().amax(-1)
+    psnr = _psnr(got, want)
+    report(f"dtu_like_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()),
+           flips=int((~agree).sum()), maxabs_agreeing=err[agree].max().item(), psnr=psnr)
+    assert 0.1 < rh.float().mean() < 0.9, rh.float().mean()
+    if prec == "fp32":
+        assert int((~agree).sum()) <= 0.005 * crop * crop
+        assert err[agree].max().item() <= 1e-4
+    else:
+        assert psnr > 35, psnr
+
+
+# ------------------------------------------------------------------------------------------
+# (d) NeRFLE at 256 depths (cfg5) and PlainNeRF
+# ------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+def test_nerfle_256_depths_matches_oracle(prec, monkeypatch):
+    """cfg5's depth count: NeRFLE(steps=256) on the fused FP16 kernel / FP32 path vs the oracle."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.shapes import NeRFLE
+    monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
+    seeded(37)
+    ref = R.NeRFLERef(steps=256)
+    mine = NeRFLE(device="cpu", steps=256)
+    copy_mlp(mine.first, ref.first)
+    copy_mlp(mine.second, ref.second)
+    mine = mine.cuda()
+    g = torch.Generator().manual_seed(10)
+    o = torch.tensor([0.0, 0.1, 1.1]) + 0.1 * torch.randn(1, 9, 7, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, 9, 7, 1, 2, generator=g) - 0.5,
+                               -torch.ones(1, 9, 7, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    loc = torch.tensor([[0.0, 1.0, 0.0]])
+    lights = PointLights(location=loc.cuda(), device="cuda")
+    set_precision(prec)
+    random.seed(4)
+    with torch.no_grad():
+        got = mine(rays.cuda(), lights).cpu()
+    random.seed(4)
+    with torch.no_grad():
+        want = ref(rays, loc, jitter=random.random())
+    err = (got - want).abs().max().item()
+    report(f"nerfle_256[{prec}]", rays=rays[..., 0].numel(), maxabs=err)
+    assert err <= (1e-4 if prec == "fp32" else 2e-2), err
+
+
+def _plain_pair(seed=47, steps=32):
+    from neural_raytracing_amd.pathtracer.shapes import PlainNeRF
+    seeded(seed)
+    ref = R.PlainNeRFRef(steps=steps)
+    mine = PlainNeRF(steps=steps, device="cpu")
+    copy_mlp(mine.first, ref.first)
+    copy_mlp(mine.second, ref.second)
+    latent = torch.randn(2, 32)
+    ref.assign_latent(latent)
+    mine = mine.cuda()
+    mine.assign_latent(latent.cuda())
+    return ref, mine
+
+
+@pytest.mark.parametrize("prec,steps", [("fp32", 32), ("fp32", 7), ("fp16", 32)])
+def test_plain_nerf_matches_oracle(prec, steps):
+    """PlainNeRF (nerf.py:9-74): two cameras (latent rows), tanh colours, alpha noise injected
+    into both sides, (rgb + 1) / 2."""
+    from neural_raytracing_amd import set_precision
+    ref, mine = _plain_pair(steps=steps)
+    g = torch.Generator().manual_seed(12)
+    o = torch.tensor([0.0, 0.2, 1.2]) + 0.1 * torch.randn(2, 6, 5, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(2, 6, 5, 1, 2, generator=g) - 0.5,
+                               -torch.ones(2, 6, 5, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    noise = torch.randn(steps, 2, 6, 5, 1, 1, generator=g) * 1e-3
+    set_precision(prec)
+    random.seed(8)
+    with torch.no_grad():
+        got = mine(rays.cuda(), None, noise=noise.cuda()).cpu()
+    random.seed(8)
+    with torch.no_grad():
+        want = ref(rays, None, jitter=random.random(), noise=noise)
+    assert got.shape == want.shape == (2, 6, 5, 1, 3)
+    err = (got - want).abs().max().item()
+    report(f"plain_nerf[{prec},S={steps}]", maxabs=err)
+    assert err <= (1e-4 if prec == "fp32" else 2e-2), err
+
+
+def test_plain_nerf_draws_its_own_noise():
+    """Without injected noise the product draws randn * 1e-3 per sample (nerf.py:66): the result
+    stays within the noise's effect of the noise-free oracle."""
+    ref, mine = _plain_pair(seed=49)
+    rays = _camera_rays(6, 2).expand(2, 6, 6, 1, 6).contiguous()
+    random.seed(1)
+    with torch.no_grad():
+        got = mine(rays.cuda(), None).cpu()
+    random.seed(1)
+    with torch.no_grad():
+        want = ref(rays, None, jitter=random.random(), noise=torch.zeros(32, 2, 6, 6, 1, 1))
+    assert (got - want).abs().max().item() < 5e-2
+
+
+# ------------------------------------------------------------------------------------------
+# it.normalized_weights on every ray (bsdfs.py:515-536)
+# ------------------------------------------------------------------------------------------
+
+def test_direct_normalized_weights_cover_misses():
+    """Direct.sample on the fused kernels leaves it.normalized_weights / nonnormalized_weights to
+    be read (an addition= hook, colocate.py:104): sigmoid(sp_var_fn(p)) on every ray, misses
+    included, as ComposeSpatialVarying.eval_and_pdf sets it."""
+    from tests.test_gpu_parity import _scene_pair
+    ref, mine = _scene_pair()
+    pos = R._tile_positions(100, 90, 24)
+    rays = ref["camera"].sample_positions(pos, 256, 0.0)
+    with torch.no_grad():
+        _, _, rit = ref["integrator"].sample(ref["shape"], rays, ref["bsdf"], ref["lights"],
+                                             jitter=0.25)
+        random.seed(0)
+        _, active, it = mine["integrator"].sample(mine["shape"], rays.cuda(), mine["bsdf"],
+                                                  lights=mine["lights"])
+    assert 0 < active.float().mean() < 1  # hits and misses
+    got = it.normalized_weights.cpu()
+    assert got.shape == rit.normalized_weights.shape == (1, 24, 24, 1, 8)
+    assert (got - rit.normalized_weights).abs().max().item() <= 1e-4
+    raw = it.nonnormalized_weights.cpu()
+    assert torch.allclose(raw.sigmoid(), got, atol=1e-6)
+
+
+def test_mlp_backward_refuses_weights_changed_after_forward():
+    """A graph whose SkipConnMLP weights were updated in place after its forward (an optimiser
+    step between forward and backward, retain_graph reuse) raises like nn.Linear's version check
+    instead of silently differentiating the new weights (the HIP backward reads the re-packed
+    training handle)."""
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    seeded(3)
+    m = SkipConnMLP(num_layers=2, hidden_size=32, out=2, device="cuda")
+    x = torch.rand(64, 3, device="cuda")
+    y = m(x).square().sum()
+    with torch.no_grad():
+        m.out.weight.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        y.backward()
+    y2 = m(x).square().sum()
+    y2.backward()  # a fresh graph is fine
+    assert m.out.weight.grad is not None

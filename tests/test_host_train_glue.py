@@ -79,3 +79,41 @@ def test_needs_grad_follows_autograd_mode():
     for q in s.parameters():
         q.requires_grad_(False)
     assert not D.needs_grad(s)
+
+
+def _jit_float_scale(c, e: float):
+    return c * e
+
+
+def test_conductor_eta_gets_no_gradient_like_the_reference():
+    """Conductor.eval_and_pdf passes F.softplus(self.eta) into fresnel_conductor, which the
+    reference compiles with @torch.jit.script and annotates ``eta_r: float`` (bsdfs.py:327-328,
+    :371): TorchScript converts the 0-d tensor to a Python float, so eta receives no gradient and
+    AdamW never moves it.  The training path keeps that (differentiable.bsdf_eval detaches eta);
+    specular still gets its gradient."""
+    import inspect
+    import torch
+    import torch.nn.functional as F
+    from neural_raytracing_amd.pathtracer.bsdf import Conductor
+    from neural_raytracing_amd.pathtracer.differentiable import bsdf_eval
+
+    # the TorchScript float conversion itself (what the reference's call does)
+    f = torch.jit.script(_jit_float_scale)
+    eta = torch.tensor(1.3, requires_grad=True)
+    c = torch.rand(4, requires_grad=True)
+    f(c, F.softplus(eta)).sum().backward()
+    assert eta.grad is None and c.grad is not None
+
+    cond = Conductor(specular=[0.5, 0.6, 0.7], device="cpu")
+
+    class It:
+        pass
+    it = It()
+    it.wi = F.normalize(torch.tensor([[0.1, 0.2, 0.9]]), dim=-1)
+    it.p = torch.zeros(1, 3)
+    wo = torch.cat([-it.wi[:, :2], it.wi[:, 2:]], -1)  # the mirror direction: above the 0.94 cut
+    f_, _ = bsdf_eval(cond, it, wo, torch.ones(1, dtype=torch.bool))
+    f_.sum().backward()
+    assert cond.eta.grad is None
+    assert cond.specular.grad is not None and cond.specular.grad.abs().sum() > 0
+    assert inspect.signature(Conductor.__init__).parameters["eta"].default == 1.3

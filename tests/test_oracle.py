@@ -158,3 +158,61 @@ def test_product_look_at_matches_oracle():
         ref = R.FoVCameraRef(Ro, To, znear=1.0, zfar=100.0)
         assert torch.equal(cam.get_camera_center(), ref.center())
         assert torch.equal(cam.inverse_full_projection(), ref.inverse_full_projection())
+
+
+def test_plain_nerf_zero_mlps_kat():
+    """PlainNeRF (nerf.py:46-74) with zero-initialised MLPs: rgb = tanh(0) = 0, so every ray
+    composites to (0 + 1) / 2 = 0.5 whatever the weights of the compositing."""
+    torch.manual_seed(0)
+    ref = R.PlainNeRFRef(steps=9)
+    for m in (ref.first, ref.second):
+        for lin in [m.init, *m.layers, m.out]:
+            torch.nn.init.zeros_(lin.weight)
+            torch.nn.init.zeros_(lin.bias)
+    ref.assign_latent(torch.randn(2, 32))
+    rays = torch.cat([torch.zeros(2, 3, 4, 1, 3), F.normalize(torch.randn(2, 3, 4, 1, 3), dim=-1)], -1)
+    out = ref(rays, None, jitter=0.5, noise=torch.rand(9, 2, 3, 4, 1, 1))
+    assert out.shape == (2, 3, 4, 1, 3)
+    assert torch.equal(out, torch.full_like(out, 0.5))
+
+
+def test_plain_nerf_composite_closed_form():
+    """PlainNeRF compositing with a constant density: first MLP out bias alpha_raw = c, no noise,
+    second MLP out bias b (rgb = tanh(b)): w_0 = a_0 prod(1 - a), w_s = a_s prod_{j<s}(1 - a_j),
+    w_{S-1} = a_{S-1}, a_s = 1 - exp(-c t_s) (nerf.py:67-73, the NeRFLE roll quirk)."""
+    torch.manual_seed(1)
+    S, c, b = 5, 0.7, 0.3
+    ref = R.PlainNeRFRef(steps=S)
+    for m in (ref.first, ref.second):
+        for lin in [m.init, *m.layers, m.out]:
+            torch.nn.init.zeros_(lin.weight)
+            torch.nn.init.zeros_(lin.bias)
+    with torch.no_grad():
+        ref.first.out.bias[0] = c
+        ref.second.out.bias.fill_(b)
+    ref.assign_latent(torch.zeros(1, 32))
+    rays = torch.tensor([[0.0, 0.0, 0.0, 0.0, 0.0, -1.0]]).reshape(1, 1, 1, 1, 6)
+    out = ref(rays, None, jitter=0.0, noise=torch.zeros(S, 1, 1, 1, 1, 1))
+    ts = torch.linspace(0.4, 2.0, S).double()
+    a = 1 - torch.exp(-c * ts)
+    q = (1 - a).clamp(min=1e-10)
+    w = [a[0] * q.prod()] + [a[s] * q[:s].prod() for s in range(1, S - 1)] + [a[S - 1]]
+    want = (sum(w) * math.tanh(b) + 1) / 2
+    assert abs(out.reshape(-1)[0].item() - want.item()) < 1e-6
+
+
+def test_shaped_mlp_sdf_level_set():
+    """bench.shape_mlp_sdf: sdf(p) ~= (|p|^2 - r^2) / 2 on a random 8x256 softplus SkipConnMLP
+    (the cfg2 / cfg4 SDF), so it has a zero level set near |p| = r and never oversteps."""
+    import bench
+    torch.manual_seed(0)
+    m = R.SkipMLP(num_layers=8, hidden_size=256, out=1, freqs=16, activation="softplus")
+    bench.shape_mlp_sdf(m, radius=0.3)
+    g = torch.Generator().manual_seed(0)
+    d = F.normalize(torch.randn(256, 3, generator=g), dim=-1)
+    with torch.no_grad():
+        for r in (0.0, 0.3, 0.6, 1.0):
+            v = m(d * r)[..., 0]
+            assert (v - (r * r - 0.09) / 2).abs().max().item() < 0.02, (r, v)
+            if r >= 0.3:  # outside: a lower bound of |p| - r, so sphere tracing never oversteps
+                assert (v <= r - 0.3 + 1e-3).all()

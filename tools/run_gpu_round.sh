@@ -6,7 +6,8 @@ export TMPDIR=/tmp
 STEP=${1:-all}
 mkdir -p gpurun_out
 if [ "$STEP" = all ] || [ "$STEP" = tests ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+  rm -f gpurun_out/parity_report.jsonl
+  NRT_REPORT=gpurun_out/parity_report.jsonl timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 180 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
   rc=$?; echo "TESTS EXIT $rc"; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
   rc=$?; echo "SMOKE EXIT $rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
