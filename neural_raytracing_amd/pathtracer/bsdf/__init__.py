@@ -1,2 +1,2 @@
-from .bsdfs import (BSDF, ComposeSpatialVarying, Conductor, Diffuse, NeuralBSDF,  # noqa: F401
-                    identity, identity_div_pi)
+from .bsdfs import (BSDF, Bidirectional, ComposeSpatialVarying, Conductor, Diffuse,  # noqa: F401
+                    NeuralBSDF, Phong, Plastic, identity, identity_div_pi)

@@ -176,3 +176,96 @@ class ComposeSpatialVarying(BSDF):
         w = self.sp_var_fn(self.preprocess(p)).reshape(p.shape[:-1] + (len(self.bsdfs),))
         setattr(it, "nonnormalized_weights", w)
         return w.sigmoid()
+
+
+# ---- reference BSDFs outside the hot path (import surface of scripts/*.py) ----------------------
+# The drivers import Phong, Plastic and Bidirectional (nerf_synthetic.py:10-12, dtu.py:11-13,
+# colocate.py:10-12) without rendering them.  Their constructors and parameters() follow
+# bsdfs.py:132-149, 238-270 and the Bidirectional wrapper; shading with them is not on the HIP path
+# and raises NrtError, as any unrecognised BSDF does.
+
+class _Unsupported(BSDF):
+    def _component(self):
+        raise _lib.NrtError(f"BSDF {type(self).__name__} has no HIP implementation (supported: "
+                            "NeuralBSDF, Diffuse, Conductor, ComposeSpatialVarying)")
+
+    def eval_and_pdf(self, it, wo, active=True):
+        self._component()
+
+    def sample(self, it, sampler, active=True):
+        self._component()
+
+
+class Phong(_Unsupported):
+    """bsdfs.py:132-189 (constructor, parameters, random)."""
+
+    def __init__(self, diffuse=[0.6, 0.5, 0.7], specular=[0.8, 0.8, 0.8], min_spec=1, device="cuda"):
+        super().__init__()
+        self.diffuse = torch.tensor(diffuse, device=device, requires_grad=True) \
+            if type(diffuse) == list else diffuse
+        self.specular = torch.tensor(specular, device=device, requires_grad=True) \
+            if type(specular) == list else specular
+        self.shine = torch.tensor(40., dtype=torch.float, device=device, requires_grad=True)
+        self.min_spec = min_spec
+
+    def parameters(self):
+        return [self.specular, self.diffuse, self.shine]
+
+    def random(self):
+        self.shine = torch.rand_like(self.shine, requires_grad=True)
+        self.specular = torch.rand_like(self.specular, requires_grad=True)
+        self.diffuse = torch.rand_like(self.diffuse, requires_grad=True)
+        return self
+
+
+def fresnel_diff_refl(eta):
+    """bsdfs.py:220-235 (Mitsuba's diffuse Fresnel reflectance fit)."""
+    if eta < 1:
+        return -1.4399 * (eta * eta) + 0.7099 * eta + 0.6681 + 0.0636 / eta
+    inv = 1 / eta
+    return 0.919317 - 3.4793 * inv + 6.75335 * inv ** 2 - 7.80989 * inv ** 3 + \
+        4.98554 * inv ** 4 - 1.36881 * inv ** 5
+
+
+class Plastic(_Unsupported):
+    """bsdfs.py:238-270 (constructor, parameters, random)."""
+
+    def __init__(self, diffuse=[0.5, 0.5, 0.5], specular=[1., 1., 1.], int_ior: float = 1.49,
+                 ext_ior: float = 1.000277, device="cuda"):
+        super().__init__()
+        self.diffuse = torch.tensor(diffuse, device=device, requires_grad=True) \
+            if type(diffuse) == list else diffuse
+        self.specular = torch.tensor(specular, device=device, requires_grad=True) \
+            if type(specular) == list else specular
+        assert int_ior > 0 and ext_ior > 0
+        self.eta = int_ior / ext_ior
+        self.inv_eta_2 = 1 / (self.eta * self.eta)
+        self.fdr_int = fresnel_diff_refl(1 / self.eta)
+        self.fdr_ext = fresnel_diff_refl(self.eta)
+
+    def spec_sample_weight(self):
+        d = self.diffuse.mean()
+        s = self.specular.mean()
+        return s / (d + s)
+
+    def parameters(self):
+        return [self.diffuse, self.specular]
+
+    def random(self):
+        self.specular = torch.rand_like(self.specular, requires_grad=True)
+        self.diffuse = torch.rand_like(self.diffuse, requires_grad=True)
+        return self
+
+
+class Bidirectional(_Unsupported):
+    """bsdfs.py:409-440: front BSDF for cos(theta_i) > 0, back (default: the front one) with z
+    inverted below the surface."""
+
+    def __init__(self, front, back=None):
+        super().__init__()
+        self.front = front
+        self.back = front if back is None else back
+
+    def parameters(self):
+        from itertools import chain
+        return chain(self.front.parameters(), self.back.parameters())

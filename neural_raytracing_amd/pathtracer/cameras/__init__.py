@@ -1,2 +1,3 @@
 from .cameras import (Camera, DTUCamera, FoVPerspectiveCameras, NeRFCamera,  # noqa: F401
-                      OpenGLPerspectiveCameras, look_at_view_transform)
+                      NeRVCamera, OpenGLPerspectiveCameras, look_at_rotation,
+                      look_at_view_transform)

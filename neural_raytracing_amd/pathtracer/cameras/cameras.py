@@ -84,6 +84,25 @@ def _f32(v, device="cpu"):
     return t.to(device=device, dtype=torch.float32).reshape(-1)
 
 
+def look_at_rotation(camera_position, at=((0, 0, 0),), up=((0, 1, 0),), device="cpu"):
+    """renderer/cameras.py:1313-1360: world -> view rotations [N, 3, 3] of cameras at
+    camera_position looking at ``at`` (columns: x right, y up, z forward)."""
+    C = torch.as_tensor(camera_position, dtype=torch.float32).reshape(-1, 3)
+    at = torch.as_tensor(at, dtype=torch.float32).reshape(-1, 3)
+    up = torch.as_tensor(up, dtype=torch.float32).reshape(-1, 3)
+    n = max(C.shape[0], at.shape[0], up.shape[0])
+    C, at, up = C.expand(n, 3), at.expand(n, 3), up.expand(n, 3)
+    z_axis = F.normalize(at - C, eps=1e-5)
+    x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
+    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
+    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
+    if is_close.any():
+        x_axis = torch.where(is_close, F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5),
+                             x_axis)
+    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
+    return R.transpose(1, 2).to(device)
+
+
 def look_at_view_transform(dist=1.0, elev=0.0, azim=0.0, degrees=True, eye=None,
                            at=((0, 0, 0),), up=((0, 1, 0),), device="cpu"):
     """R [N,3,3], T [N,3] of the look-at world -> view transform (renderer/cameras.py:1363-1422,
@@ -101,16 +120,8 @@ def look_at_view_transform(dist=1.0, elev=0.0, azim=0.0, degrees=True, eye=None,
         C = torch.stack([dist * torch.cos(elev) * torch.sin(azim), dist * torch.sin(elev),
                          dist * torch.cos(elev) * torch.cos(azim)], dim=1).view(-1, 3) + at
     n = max(C.shape[0], at.shape[0], up.shape[0])
-    C, at, up = C.expand(n, 3), at.expand(n, 3), up.expand(n, 3)
-    z_axis = F.normalize(at - C, eps=1e-5)
-    x_axis = F.normalize(torch.cross(up, z_axis, dim=1), eps=1e-5)
-    y_axis = F.normalize(torch.cross(z_axis, x_axis, dim=1), eps=1e-5)
-    is_close = torch.isclose(x_axis, torch.tensor(0.0), atol=5e-3).all(dim=1, keepdim=True)
-    if is_close.any():
-        x_axis = torch.where(is_close, F.normalize(torch.cross(y_axis, z_axis, dim=1), eps=1e-5),
-                             x_axis)
-    R = torch.cat((x_axis[:, None, :], y_axis[:, None, :], z_axis[:, None, :]), dim=1)
-    R = R.transpose(1, 2)
+    C = C.expand(n, 3)
+    R = look_at_rotation(C, at, up)
     T = -torch.bmm(R.transpose(1, 2), C[:, :, None])[:, :, 0]
     return R.to(device), T.to(device)
 
@@ -240,3 +251,21 @@ class DTUCamera(Camera):
         W, H, _ = position_samples.shape
         pos = position_samples.float().contiguous()
         return self.rays_tile(0, 0, W, H, size, positions=pos, bundle_size=bundle_size)
+
+
+@dataclass
+class NeRVCamera(Camera):
+    """cameras.py:103-130 (NeRV dataset): sample_positions returns ``torch.cat([r_o, r_d])`` with
+    ``r_o`` never defined (:130), so the camera cannot produce rays in the reference; kept
+    import-resolvable (train_nerv, training_utils.py:634)."""
+    world_to_cam: torch.Tensor = None
+    loc: torch.Tensor = None
+    focal: float = None
+    device: str = "cuda"
+
+    def __len__(self):
+        return self.world_to_cam.shape[0]
+
+    def sample_positions(self, *args, **kwargs):
+        raise NotImplementedError("NeRVCamera.sample_positions uses an undefined r_o in the "
+                                  "reference (cameras.py:130)")

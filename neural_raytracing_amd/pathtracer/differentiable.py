@@ -123,7 +123,9 @@ def sphere_part(sdf, p):
 def sdf_value(sdf, p):
     """sdf(p) with gradients for the SDF's parameters."""
     from .neural_blocks import SkipConnMLP
+    from .script_modules import resolve
     from .shapes.sdfs import SPHERE_SDF, _is_sphere_sdf
+    sdf = resolve(sdf)
     if sdf is SPHERE_SDF:
         return torch.norm(p, dim=-1) - 1
     if isinstance(sdf, SkipConnMLP):
@@ -139,7 +141,9 @@ def sdf_gradient(sdf, p):
     SDF's parameters (create_graph=True).  ``p`` itself is not differentiated (the reference's
     hit points come from the no-grad march)."""
     from .neural_blocks import SkipConnMLP, input_gradient
+    from .script_modules import resolve
     from .shapes.sdfs import SPHERE_SDF, _is_sphere_sdf
+    sdf = resolve(sdf)
     p = p.detach()
     if sdf is SPHERE_SDF:
         return p / torch.norm(p, dim=-1, keepdim=True)
@@ -172,6 +176,7 @@ def light_sample(lights, it, active):
         dist = None
     elif isinstance(lights, PointLights):
         # lights.py:89-110
+        lights.single()
         loc = lights.location.reshape(-1, 3)[0]
         d = loc - p
         dist = torch.linalg.norm(d, dim=-1, keepdim=True)

@@ -1,2 +1,3 @@
-from .integrators import (Debug, Depth, Direct, Integrator, Mask, NeRFIntegrator,  # noqa: F401
-                          NeRFReproduce, Path)
+from .integrators import (BasisBRDF, Debug, Depth, Direct, Illumination, Integrator,  # noqa: F401
+                          Luminance, Mask, NeRFIntegrator, NeRFReproduce, NeuralApprox, Path,
+                          Silhouette)

@@ -36,6 +36,85 @@ class Debug(Integrator):
         return result, active, si
 
 
+class Silhouette(Integrator):
+    """1 - hit (integrators.py:38-42)."""
+
+    def dims(self):
+        return 1
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        si, active = shapes.intersect(rays)
+        return 1 - active.unsqueeze(-1).float(), active, si
+
+
+class BasisBRDF(Integrator):
+    """The spatial BSDF weights on the hit points (integrators.py:79-90): sigmoid(sp_var_fn(p))
+    of a ComposeSpatialVarying, on the HIP MLP kernel."""
+
+    def __init__(self, multi_basis_bsdf):
+        super().__init__()
+        self.bsdf = multi_basis_bsdf
+
+    def dims(self):
+        return len(self.bsdf.bsdfs)
+
+    def sample(self, shapes, rays, bsdf, **kwargs):
+        results = torch.zeros(*rays.shape[:-1], self.dims(), device=rays.device)
+        it, active = shapes.intersect(rays)
+        if not bool(active.any()):
+            return results, active, it
+        results[active] = self.bsdf.normalized_weights(it.p[active], it)
+        return results, active, it
+
+
+class Illumination(Integrator):
+    """Light direction in the shading frame at the hit points (integrators.py:93-111).  The
+    reference's signature sample(shapes, rays, lights, sampler) collides with pathtrace's keyword
+    call (lights= twice), so it is used by calling sample directly."""
+
+    def dims(self):
+        return 3
+
+    def sample(self, shapes, rays, lights, sampler=None, **kwargs):
+        from ..differentiable import light_sample
+        it, active = shapes.intersect(rays)
+        d, _, _, _ = light_sample(lights, it, active)
+        res = torch.where(active.unsqueeze(-1),
+                          (torch.nn.functional.normalize(it.to_local(d), dim=-1) + 1) / 2,
+                          torch.zeros_like(d))
+        return (1 + res) / 2, active, it
+
+
+class Luminance(Integrator):
+    """Emitter luminance at the hit points (integrators.py:114-136), with the reference's
+    0.2126 r + 0.7152 * 0.0722 b weights."""
+
+    def dims(self):
+        return 3
+
+    def sample(self, shapes, rays, lights, sampler=None, **kwargs):
+        from ..differentiable import light_sample
+        it, active = shapes.intersect(rays)
+        d, le, _, _ = light_sample(lights, it, active)
+        r, _, b = le.split(1, dim=-1)
+        lum = 0.2126 * r + 0.7152 * 0.0722 * b
+        return torch.where(active.unsqueeze(-1), lum.expand_as(d), torch.zeros_like(d)), active, it
+
+
+class NeuralApprox(Integrator):
+    """integrators.py:208-240 (a TwoStageMLP light-transport approximation, off the hot path):
+    import-resolvable for the drivers (dtu.py:16); sampling raises NrtError."""
+
+    def __init__(self, **kwargs):
+        super().__init__(**{k: v for k, v in kwargs.items() if k != "device"})
+
+    def dims(self):
+        return 3
+
+    def sample(self, shape, rays, bsdf, **kwargs):
+        raise _lib.NrtError("NeuralApprox (TwoStageMLP) has no HIP implementation")
+
+
 class Mask(Integrator):
     """Adds the hit mask as a channel (integrators.py:45-54)."""
 

@@ -1,1 +1,1 @@
-from .lights import Light, LightField, PointLights  # noqa: F401
+from .lights import Constant, Light, LightField, PointLights  # noqa: F401

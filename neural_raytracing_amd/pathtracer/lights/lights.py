@@ -55,7 +55,21 @@ class PointLights(Light):
     def spectrum_parameters(self):
         return [self.scale, self.intensity, self.const, self.linear, self.square]
 
+    def single(self):
+        """Raise unless the light is one light for every camera: the reference broadcasts
+        location [L, 3] against the hit points [N, W, H, B, 3] (lights.py:91, :106), so L > 1
+        lights are per-camera lights; the HIP shading kernels take one light per call."""
+        loc = self.location.reshape(-1, 3)
+        inten = self.intensity.reshape(-1, 3)
+        for t in (loc, inten):
+            if t.shape[0] > 1 and not bool((t == t[:1]).all()):
+                raise _lib.NrtError("PointLights with one location / intensity per camera render "
+                                    "one camera per pathtrace call on the HIP path "
+                                    "(main.pathtrace splits the cameras)")
+        return self
+
     def nrt(self):
+        self.single()
         loc = _host(self.location.reshape(-1, 3)[0])
         inten = _host(self.intensity.reshape(-1, 3)[0])
         out = ctypes.c_void_p()
@@ -98,3 +112,16 @@ class LightField(nn.Module):
         h = _Handle(out, "nrt_light_destroy", [mh])
         object.__setattr__(self, "_nrt_light", (key, h))
         return h.value
+
+
+class Constant(Light):
+    """lights.py:114-149: an emitting sphere around the scene.  Its sample_ray reads attributes it
+    never sets (broken in the reference); import-resolvable only, not a HIP light."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        self.args, self.kwargs = args, kwargs
+
+    def nrt(self):
+        raise _lib.NrtError("Constant light has no HIP implementation (supported: LightField, "
+                            "PointLights)")

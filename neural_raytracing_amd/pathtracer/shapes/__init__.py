@@ -1,2 +1,2 @@
 from .nerf import NeRFLE, PlainNeRF  # noqa: F401
-from .sdfs import SDF, SPHERE_SDF, SphereSDF  # noqa: F401
+from .sdfs import SDF, SPHERE_SDF, CapsuleSDF, RoundBoxSDF, SphereSDF  # noqa: F401

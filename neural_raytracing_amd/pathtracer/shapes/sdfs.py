@@ -46,7 +46,9 @@ _UNIT = {}
 
 
 def sdf_handle(sdf):
-    """nrt_sdf for a recognised SDF callable."""
+    """nrt_sdf for a recognised SDF callable (TorchScript modules through script_modules views)."""
+    from ..script_modules import resolve
+    sdf = resolve(sdf)
     if sdf is SPHERE_SDF:
         if "h" not in _UNIT:
             lib = _lib.load()
@@ -76,8 +78,9 @@ def sdf_handle(sdf):
                 mh.value if mh is not None else None, ctypes.byref(out)), "nrt_sdf_create_sphere_blob")
             return _Handle(out, "nrt_sdf_destroy", [mh] if mh is not None else [])
         return _cache(sdf, params, build).value
-    raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP implementation "
-                        "(supported: SPHERE_SDF, SphereSDF, SkipConnMLP)")
+    raise _lib.NrtError(f"SDF callable {getattr(sdf, '__name__', type(sdf).__name__)} has no HIP "
+                        "implementation (supported: SPHERE_SDF, SphereSDF, SkipConnMLP and their "
+                        "TorchScript modules)")
 
 
 def _looks_like_sphere_sdf(m):
@@ -272,3 +275,34 @@ class SDF:
         _lib.call("nrt_sdf_grad", sdf_handle(self.sdf), _lib.ptr(flat), flat.shape[0], _lib.ptr(g),
                   _lib.stream())
         return g.reshape(p.shape)
+
+
+class RoundBoxSDF(nn.Module):
+    """Rounded boxes smooth-min-ed together (sdfs.py:48-68): import-resolvable for the drivers
+    (nerf_synthetic.py:14-16, dtu.py:18-20); constructor and RNG order as the reference.  Not a
+    HIP SDF kind: SDF(sdf=RoundBoxSDF()) raises NrtError when it is marched."""
+
+    def __init__(self, n=2 << 4, device="cuda"):
+        super().__init__()
+        self.centers = nn.Parameter(0.3 * torch.rand(n, 3, device=device, requires_grad=True) - 0.15)
+        self.b = nn.Parameter(0.2 * torch.rand_like(self.centers, requires_grad=True))
+        self.radii = nn.Parameter(0.2 * torch.rand(n, device=device, requires_grad=True) - 0.1)
+        self.tfs = nn.Parameter(torch.zeros(n, 3, 3, device=device, requires_grad=True))
+
+    def forward(self, p):
+        raise _lib.NrtError("RoundBoxSDF has no HIP implementation (supported SDFs: SPHERE_SDF, "
+                            "SphereSDF, SkipConnMLP)")
+
+
+class CapsuleSDF(nn.Module):
+    """Capsules smooth-min-ed together (sdfs.py:72-86): import-resolvable, like RoundBoxSDF."""
+
+    def __init__(self, n=2 << 5, device="cuda"):
+        super().__init__()
+        self.a = nn.Parameter(0.1 * torch.rand(n, 3, device=device, requires_grad=True) - 0.05)
+        self.b = nn.Parameter(0.1 * torch.rand_like(self.a, requires_grad=True) - 0.05)
+        self.radii = nn.Parameter(0.1 * torch.rand(n, device=device, requires_grad=True) - 0.05)
+
+    def forward(self, p):
+        raise _lib.NrtError("CapsuleSDF has no HIP implementation (supported SDFs: SPHERE_SDF, "
+                            "SphereSDF, SkipConnMLP)")

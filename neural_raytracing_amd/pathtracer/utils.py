@@ -123,3 +123,51 @@ def save_image(name, img):
     from PIL import Image
     arr = (img.detach().cpu().clamp(0, 1).numpy() * 255 + 0.5).astype(np.uint8)
     Image.fromarray(arr).save(name)
+
+
+def count_parameters(params):
+    """utils.py:363."""
+    return sum(p.numel() for p in params)
+
+
+def smooth_min(v, k: float = 32, dim: int = 0):
+    """utils.py:386-387 (host form; the HIP SphereSDF evaluates it in-kernel)."""
+    return -torch.exp(-k * v).sum(dim).clamp(min=1e-4).log() / k
+
+
+def depth_image(img):
+    """utils.py:441-445: [depth, mask] -> [d/max d, d/max d, d/max d, mask]."""
+    l, m = img.split(1, dim=-1)
+    l = l / l.max()
+    return torch.cat([l, l, l, m], dim=-1)
+
+
+def heightmap(warp, size=256, device="cuda"):
+    """utils.py:434-439: warp.pdf on a size x size (u, v) grid."""
+    u, v = torch.meshgrid(torch.linspace(0, 1, size, device=device),
+                          torch.linspace(0, 1, size, device=device), indexing="ij")
+    return warp.pdf(torch.stack([u, v], dim=-1))
+
+
+def sphere_examples(bsdf, device="cuda", size=256, chunk_size=128, scale=100):
+    """utils.py:409-431 renders each component of a ComposeSpatialVarying on an analytic unit
+    Sphere (shapes/shapes.py:31-97) lit by pytorch3d.renderer.PointLights -- a mesh-renderer class
+    with no sample_direction and no ``scale`` argument, so the reference call fails as written.
+    Here: the same camera (look_at_view_transform(dist=2, elev=0, azim=0)) and light
+    (location (0, 1, 4), scale) with the pathtracer's PointLights, Direct(), and the unit sphere
+    as SPHERE_SDF marched on the HIP path."""
+    from . import pathtrace
+    from .cameras import OpenGLPerspectiveCameras, look_at_view_transform
+    from .integrators import Direct
+    from .lights import PointLights
+    from .shapes import SDF, SPHERE_SDF
+    sphere = SDF(sdf=SPHERE_SDF, device=device)
+    R, T = look_at_view_transform(dist=2., elev=0, azim=0)
+    cameras = OpenGLPerspectiveCameras(device=device, R=R, T=T)
+    lights = PointLights(device=device, location=[[0., 1., 4.]], scale=scale)
+    out = []
+    for basis in bsdf.bsdfs:
+        out.append(pathtrace(sphere, cameras=cameras, lights=lights, chunk_size=chunk_size,
+                             size=size, bsdf=basis, integrator=Direct(), device=device,
+                             silent=True)[0])
+    return out

@@ -87,22 +87,27 @@ def test_bare_mlp_sdf_march_matches_oracle(prec):
             rays, primary=True, jitter=jit)
     hit, rhit = hit.cpu().reshape(-1), rhit.reshape(-1)
     flips = int((hit != rhit).sum())
-    m = hit & rhit
-    t_err = (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max().item()
+    t, rt = it.t.cpu().reshape(-1), rit.t.reshape(-1)
+    # a "step flip": both hit, but one side stopped a march step earlier because the SDF value
+    # at that step sat within rounding of eps (t then differs by that last step, <= eps)
+    step = (hit & rhit) & ((t - rt).abs() > 1e-4)
+    m = (hit & rhit) & ~step
+    t_err = (t[m] - rt[m]).abs().max().item()
     n_err = (it.n.cpu().reshape(-1, 3)[m] - rit.n.reshape(-1, 3)[m]).abs().max().item()
     p_err = (it.p.cpu().reshape(-1, 3)[m] - rit.p.reshape(-1, 3)[m]).abs().max().item()
     thr = (it.throughput.cpu().reshape(-1) - rit.throughput.reshape(-1)).abs()
     report(f"bare_mlp_sdf_march[{prec}]", rays=hit.numel(), hits=int(rhit.sum()), flips=flips,
-           t_maxabs=t_err, n_maxabs=n_err, p_maxabs=p_err, thr_maxabs=thr.max().item())
+           step_flips=int(step.sum()), t_maxabs=t_err, n_maxabs=n_err, p_maxabs=p_err,
+           thr_maxabs=thr.max().item(), thr_over_0p1=int((thr > 0.1).sum()))
     assert 0.15 < rhit.float().mean() < 0.85
     if prec == "fp32":
-        assert flips <= 0.005 * hit.numel()
+        assert flips + int(step.sum()) <= 0.005 * hit.numel()
         assert t_err <= 1e-4 and p_err <= 1e-4 and n_err <= 1e-4
         # throughput = -1000 sdf(best): 1e-4 abs on sdf is 0.1 here
         assert (thr <= 0.1).float().mean() >= 0.995
     else:
         assert flips <= 0.03 * hit.numel()
-        assert t_err <= 2e-2
+        assert (t - rt)[hit & rhit].abs().max().item() <= 2e-2
         cos = (it.n.cpu().reshape(-1, 3)[m] * rit.n.reshape(-1, 3)[m]).sum(-1)
         assert (cos > math.cos(math.radians(2.0))).float().mean() > 0.99
         assert (thr <= 10.0).float().mean() >= 0.95
@@ -118,22 +123,31 @@ def test_bare_mlp_sdf_scan_free_matches_oracle():
         rit, rhit = R.MarchedSDF(sdf=lambda p: ref(p)[..., 0], max_steps=64).intersect(
             rays, primary=False)
     hit, rhit = hit.cpu().reshape(-1), rhit.reshape(-1)
-    m = hit & rhit
-    report("bare_mlp_sdf_scan_free[fp32]", rays=hit.numel(), flips=int((hit != rhit).sum()))
-    assert int((hit != rhit).sum()) <= 0.005 * hit.numel()
-    assert (it.t.cpu().reshape(-1)[m] - rit.t.reshape(-1)[m]).abs().max().item() <= 1e-4
+    t, rt = it.t.cpu().reshape(-1), rit.t.reshape(-1)
+    step = (hit & rhit) & ((t - rt).abs() > 1e-4)
+    m = (hit & rhit) & ~step
+    report("bare_mlp_sdf_scan_free[fp32]", rays=hit.numel(), flips=int((hit != rhit).sum()),
+           step_flips=int(step.sum()))
+    assert int((hit != rhit).sum()) + int(step.sum()) <= 0.005 * hit.numel()
+    assert (t[m] - rt[m]).abs().max().item() <= 1e-4
 
 
 # ------------------------------------------------------------------------------------------
 # (b) the metric configuration at S = 64
 # ------------------------------------------------------------------------------------------
 
-def _hit_masks(prod_shape, oracle_shape, prod_rays, oracle_rays):
+def _agreement(prod_shape, oracle_shape, prod_rays, oracle_rays):
+    """Per pixel: do the two marches agree (same hit flag, and on hits the same depth to 1e-4,
+    i.e. neither stopped a step early on an SDF value within rounding of eps)?  Returns
+    (agree mask, oracle hit mask, hit flips, step flips)."""
     with torch.no_grad():
-        _, h = prod_shape.intersect(prod_rays, primary=False)
+        it, h = prod_shape.intersect(prod_rays, primary=False)
         o, d = oracle_rays.split(3, dim=-1)
-        _, rh = oracle_shape.march(o, d)
-    return h.cpu().reshape(-1), rh.reshape(-1)
+        rt, rh = oracle_shape.march(o, d)
+    h, rh = h.cpu().reshape(-1), rh.reshape(-1)
+    t, rt = it.t.cpu().reshape(-1), rt.reshape(-1)
+    step = (h & rh) & ((t - rt).abs() > 1e-4)
+    return (h == rh) & ~step, rh, int((h != rh).sum()), int(step.sum())
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp16"])
@@ -167,14 +181,14 @@ def test_metric_config_crop_matches_oracle(prec):
                                      with_noise=0.0)
     got = got.cpu()
     assert got.shape == want.shape == (crop, crop, 4)
-    h, rh = _hit_masks(scene["shape"], osc["shape"],
-                       cam.rays_tile(c0, c1, crop, crop, size),
-                       ocam.sample_positions(R._tile_positions(c0, c1, crop), size))
-    agree = (h == rh).reshape(crop, crop)
+    agree, rh, flips, steps = _agreement(scene["shape"], osc["shape"],
+                                         cam.rays_tile(c0, c1, crop, crop, size),
+                                         ocam.sample_positions(R._tile_positions(c0, c1, crop), size))
+    agree = agree.reshape(crop, crop)
     err = (got - want).abs().amax(-1)
     psnr = _psnr(got, want)
-    report(f"metric_config_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()),
-           flips=int((~agree).sum()), maxabs_agreeing=err[agree].max().item(),
+    report(f"metric_config_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()), flips=flips,
+           step_flips=steps, maxabs_agreeing=err[agree].max().item(),
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.95
     if prec == "fp32":
@@ -236,19 +250,21 @@ def test_dtu_like_render_matches_oracle(prec):
                                      crop_size=crop, uv=uv, background=0, with_noise=0.0)
     got = got.cpu()
     assert got.shape == want.shape == (crop, crop, 4)
-    h, rh = _hit_masks(sc["shape"], osc["shape"], sc["cameras"].rays_tile(uv[0], uv[1], crop, crop, size),
-                       osc["camera"].sample_positions(R._tile_positions(uv[0], uv[1], crop), size))
-    agree = (h == rh).reshape(crop, crop)
+    agree, rh, flips, steps = _agreement(
+        sc["shape"], osc["shape"], sc["cameras"].rays_tile(uv[0], uv[1], crop, crop, size),
+        osc["camera"].sample_positions(R._tile_positions(uv[0], uv[1], crop), size))
+    agree = agree.reshape(crop, crop)
     err = (got - want).abs().amax(-1)
     psnr = _psnr(got, want)
-    report(f"dtu_like_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()),
-           flips=int((~agree).sum()), maxabs_agreeing=err[agree].max().item(), psnr=psnr)
+    report(f"dtu_like_crop[{prec}]", pixels=crop * crop, hits=int(rh.sum()), flips=flips,
+           step_flips=steps, maxabs_agreeing=err[agree].max().item(),
+           pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.9, rh.float().mean()
     if prec == "fp32":
         assert int((~agree).sum()) <= 0.005 * crop * crop
         assert err[agree].max().item() <= 1e-4
     else:
-        assert psnr > 35, psnr
+        assert psnr > 40, psnr
 
 
 # ------------------------------------------------------------------------------------------
@@ -292,6 +308,8 @@ def _plain_pair(seed=47, steps=32):
     seeded(seed)
     ref = R.PlainNeRFRef(steps=steps)
     mine = PlainNeRF(steps=steps, device="cpu")
+    with torch.no_grad():  # a visible density (random init gives relu(alpha) = 0 almost everywhere)
+        ref.first.out.bias[0] += 1.5
     copy_mlp(mine.first, ref.first)
     copy_mlp(mine.second, ref.second)
     latent = torch.randn(2, 32)
@@ -321,6 +339,7 @@ def test_plain_nerf_matches_oracle(prec, steps):
     with torch.no_grad():
         want = ref(rays, None, jitter=random.random(), noise=noise)
     assert got.shape == want.shape == (2, 6, 5, 1, 3)
+    assert (want - 0.5).abs().mean() > 1e-2  # the composite is not the trivial (0 + 1) / 2
     err = (got - want).abs().max().item()
     report(f"plain_nerf[{prec},S={steps}]", maxabs=err)
     assert err <= (1e-4 if prec == "fp32" else 2e-2), err
@@ -350,14 +369,14 @@ def test_direct_normalized_weights_cover_misses():
     included, as ComposeSpatialVarying.eval_and_pdf sets it."""
     from tests.test_gpu_parity import _scene_pair
     ref, mine = _scene_pair()
-    pos = R._tile_positions(100, 90, 24)
+    pos = R._tile_positions(36, 100, 24)  # across the top silhouette of the blob
     rays = ref["camera"].sample_positions(pos, 256, 0.0)
     with torch.no_grad():
-        _, _, rit = ref["integrator"].sample(ref["shape"], rays, ref["bsdf"], ref["lights"],
-                                             jitter=0.25)
+        _, _, rit = ref["integrator"].sub.sample(ref["shape"], rays, ref["bsdf"], ref["lights"],
+                                                 jitter=0.25)
         random.seed(0)
-        _, active, it = mine["integrator"].sample(mine["shape"], rays.cuda(), mine["bsdf"],
-                                                  lights=mine["lights"])
+        _, active, it = mine["integrator"].sub_integrator.sample(
+            mine["shape"], rays.cuda(), mine["bsdf"], lights=mine["lights"])
     assert 0 < active.float().mean() < 1  # hits and misses
     got = it.normalized_weights.cpu()
     assert got.shape == rit.normalized_weights.shape == (1, 24, 24, 1, 8)
@@ -373,7 +392,7 @@ def test_mlp_backward_refuses_weights_changed_after_forward():
     training handle)."""
     from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
     seeded(3)
-    m = SkipConnMLP(num_layers=2, hidden_size=32, out=2, device="cuda")
+    m = SkipConnMLP(num_layers=2, hidden_size=32, out=2, device="cuda").cuda()
     x = torch.rand(64, 3, device="cuda")
     y = m(x).square().sum()
     with torch.no_grad():
