@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crop", type=int, default=128, help="side of the CPU-baseline crop")
     ap.add_argument("--no-fp32-check", action="store_true")
+    ap.add_argument("--no-extra-legs", action="store_true",
+                    help="skip the FP32 (reference precision) and scan-free timing legs")
     ap.add_argument("--scene", default="nerf_synthetic",
                     choices=["nerf_synthetic", "colocate", "dtu", "nerfle", "train"],
                     help="nerf_synthetic = the BASELINE metric (default); the others are "
@@ -291,6 +293,8 @@ def main():
         extra["hit_fraction"] = round(hit_frac, 4)
         if not args.no_fp32_check and args.precision == "fp16":
             extra["psnr_fp16_vs_fp32"] = round(psnr_vs_fp32(scene, cameras, size), 2)
+        if not args.no_extra_legs:
+            extra.update(extra_legs(scene, cameras, size, args, rows))
         if not args.no_cpu_baseline:
             extra.update(cpu_baseline(scene, size, args))
 
@@ -342,6 +346,68 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def _time_frames(render, steps, warmup, kernels):
+    """Wall time of `steps` renders after `warmup`, and the HIP-event time of each kernel."""
+    from neural_raytracing_amd import _lib
+    for _ in range(warmup):
+        render()
+    torch.cuda.synchronize()
+    _lib.profile_reset()
+    _lib.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        render()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    return elapsed, {k: _lib.profile_read(k) for k in kernels}
+
+
+def extra_legs(scene, cameras, size, args, rows):
+    """The same frame at the reference's precision (FP32: every MLP on exact-f32 MFMA, the
+    1e-4 parity path) and without the 130-eval coarse scan (SURVEY §8d cfg2 asks for both)."""
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.render import RowRenderer
+    out = {}
+    S = args.samples
+    frame_rays = len(rows) * size * len(cameras)
+    # FP32 leg: k_intersect (exact-f32 MFMA march + scan) on the 157.3 TF FP32 matrix peak
+    nra.set_precision("fp32")
+    rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
+                     size, rows, background=0.0, with_noise=1e-3, device=cameras.cam_to_world.device)
+    steps = 2
+    el, ks = _time_frames(rr.render, steps, 1, ["k_intersect"])
+    k_ms = ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)
+    flop = frame_rays * (S + SCAN_EVALS) * FLOP_SDF_8x256  # march + scan + sdf(best): one launch
+    ach = flop / (k_ms * 1e-3) / 1e12
+    out["fp32"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
+                   "ms_per_step": 1000 * el / steps, "steps": steps,
+                   "roofline": {"bound": "mfma", "kernel": "k_intersect", "achieved": ach,
+                                "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                                "frac": ach / PEAK_TFLOPS["fp32"], "avg_kernel_ms": k_ms,
+                                "flop_per_launch": flop}}
+    nra.set_precision(args.precision)
+    # scan-free leg: Direct with training = False (the reference's Path / primary=False march)
+    direct = Direct()
+    direct.training = False
+    rr = RowRenderer(scene["shape"], scene["lights"], cameras, NeRFIntegrator(direct),
+                     scene["bsdf"], size, rows, background=0.0, with_noise=1e-3,
+                     device=cameras.cam_to_world.device)
+    steps = 3
+    el, ks = _time_frames(rr.render, steps, 1, ["k_march16"])
+    k_ms = ks["k_march16"][0] / max(ks["k_march16"][1], 1)
+    flop = frame_rays * S * FLOP_SDF_8x256
+    ach = flop / (k_ms * 1e-3) / 1e12
+    out["scan_free"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
+                        "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": args.precision,
+                        "roofline": {"bound": "mfma", "kernel": "k_march16", "achieved": ach,
+                                     "peak": PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
+                                     "frac": ach / PEAK_TFLOPS[args.precision],
+                                     "avg_kernel_ms": k_ms, "flop_per_launch": flop}}
+    return out
 
 
 FLOP_SHIFT_8x128 = 331_200      # SphereSDF shift MLP per evaluation (SURVEY §8d)
