@@ -151,7 +151,8 @@ static size_t grad_ws_aligned(const nrt_sdf* s) { return (grad_workspace_bytes(s
 
 size_t nrt_intersect_workspace_bytes(const nrt_sdf* s, int64_t P) {
   if (!s) return 0;
-  return grad_ws_aligned(s) + (ring_supported(s) ? ring_march_ws_bytes(std::max<int64_t>(P, 0)) : 0) + 256;
+  const bool keys = ring_supported(s) || ring32_supported(s);
+  return grad_ws_aligned(s) + (keys ? ring_march_ws_bytes(std::max<int64_t>(P, 0)) : 0) + 256;
 }
 
 int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_march_params* a,
@@ -194,10 +195,13 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   int rc0 = NRT_OK;
   // FP16 SDF MLPs of width 128/256 with F = 16/32 run the block-cooperative ring kernel
   const bool ring16 = f16 && ring_supported(s) && std::getenv("NRT_NO_RING") == nullptr;
-  if (ring16) {
+  // ... and FP32 SDF MLPs of those widths the FP32 ring kernel (refreshed training handles too)
+  const bool ring32 = !f16 && ring32_supported(s) && std::getenv("NRT_NO_RING32") == nullptr;
+  if (ring16 || ring32) {
     ProfScope prof("k_intersect", st);
     auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
-    rc0 = ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
+    rc0 = ring16 ? ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
+                 : ring_march32(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
     if (!rc0 && ma.scan_idx) {
       k_keys_index<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, st>>>(keys, P, ma.scan_idx);
       rc0 = check_launch("k_keys_index");

@@ -72,6 +72,12 @@ struct MlpDev {
   int nk_chunks;
   int kc;
   int nk_frags;                    // fragments in streamk16 (without tail)
+  // FP32 weight stream of the FP32 ring engine (ring32, v_mfma_f32_16x16x4_f32 on 16-ray
+  // tiles): chunks of 32 output rows in consumption order, unfolded weights (exact FP32
+  // arithmetic); element order in nrt_internal.h ring32_walk.
+  const float4* stream32;
+  int stream32_bytes;
+  const float* bias32;             // [layer][bias16_stride], unfolded
 };
 
 // A shading "program": the MLPs one kernel evaluates per ray batch, concatenated into one
@@ -1190,4 +1196,271 @@ __device__ __forceinline__ float tile_row(const f16v& o, int j, int lane) {
 }
 
 }  // namespace ring
+
+// ------------------------------------------------------------------------------------------
+// FP32 block-cooperative engine (ring32): the reference-precision SDF MLP on the LDS ring.
+// ------------------------------------------------------------------------------------------
+// v_mfma_f32_16x16x4_f32 (exact f32: each MFMA adds 4 fma products per output, same as a VALU
+// fma chain) on 16-ray tiles: lane (g = lane >> 4, j = lane & 15) serves ray j, and the four lane
+// groups split the K dimension.  The 16x16 accumulator of a 16-row sub-block holds row 4 g + reg
+// of ray j in register reg -- exactly the B operand of four k-steps of the next layer, so a whole
+// layer's activations stay in registers: H / 4 floats per lane (64 for H = 256), in the k order
+// the packer permutes W's columns to (nrt_internal.h ring32_walk).  32x32x2 tiles would need H / 2
+// per lane and twice that with the next layer's outputs, which is more than a wave can hold.
+// The weights stream through a 2-slot LDS ring shared by the WV waves of the block: chunk = 32
+// output rows of one layer (two sub-blocks = two independent MFMA chains); at the start of chunk
+// c every wave waits for its own LDS-DMA pieces of chunk c, the block barrier makes all of them
+// visible and retires everyone's reads of chunk c - 1, and the waves then DMA chunk c + 1 into
+// the slot chunk c - 1 used.  The activation (torch's exact softplus / leaky_relu) of chunk c - 1's
+// accumulators runs in the MFMA gaps of chunk c.  Layer count and skip period are runtime values.
+namespace ring32 {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// KH = H / 4 hidden k-steps, KE = ke / 4 encoding k-steps (ke = encoding slots padded to 16)
+template <int KH, int KE, int WV>
+struct Engine {
+  static constexpr int QH = KH / 4, QE = KE / 4;        // quads per sub-block
+  static constexpr int MAXQ = 2 * (QH + QE);            // largest chunk (a skip layer's), KiB
+  static constexpr int MAXL = (MAXQ + WV - 1) / WV;     // DMA pieces per wave per chunk
+  static constexpr int SLOTQ = MAXL * WV;
+  static constexpr int RING_BYTES = 2 * SLOTQ * 1024;
+  static constexpr int kOutOfRange = 0x40000000;
+  // LDS of one block: ring | basis (float4 per frequency) | biases | sphere table
+  static size_t lds_bytes(int F, size_t bias_bytes, size_t sphere_bytes) {
+    return RING_BYTES + (size_t)F * 16 + bias_bytes + sphere_bytes;
+  }
+  const float4* ring;
+  uint32_t ring_lds;
+  const float* lbias;
+  const float4* lbasis;
+  const float4* lspheres;   // [n][4] float4: (I+T) rows, centre, radius (SdfDev layout)
+  const void* sbase;
+  int sbytes, bstride;
+  int off, next_off;        // quad offset of the current / next chunk in stream32 (wave-uniform)
+  int slot;
+  int lane, wv;
+
+  // DMA chunk (quad offset qoff, nq quads) into ring slot s: wave wv moves quads wv + WV q
+  __device__ __forceinline__ void issue(int qoff, int nq, int s) {
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    const uint64_t sp = (uint64_t)(uintptr_t)sbase;
+    const uint64_t spu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)spu, 0, __builtin_amdgcn_readfirstlane(sbytes), 0x00020000);
+    const int q0 = __builtin_amdgcn_readfirstlane(qoff) + w;
+    const uint32_t dst0 = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)(s * SLOTQ * 1024)) +
+                          (uint32_t)w * 1024u;
+    const int n = __builtin_amdgcn_readfirstlane(nq);
+#pragma unroll
+    for (int q = 0; q < MAXL; ++q) {
+      const bool own = w + WV * q < n;  // fixed count per wave: pieces past the chunk load nothing
+      ring::lds_dma16(r, own ? lane * 16 : kOutOfRange + lane * 16, (q0 + WV * q) * 1024,
+                      dst0 + (uint32_t)(WV * q * 1024));
+    }
+  }
+
+  // block-wide; afterwards chunk 0 (the init layer's first, nq0 quads) is in flight to slot 0
+  __device__ __forceinline__ void init(const MlpDev& m, const SdfDev& s, char* lds, int nq0) {
+    ring = reinterpret_cast<const float4*>(lds);
+    ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+    char* p = lds + RING_BYTES;
+    const int F = m.freqs;
+    float4* lq = reinterpret_cast<float4*>(p);
+    for (int q = threadIdx.x; q < F; q += blockDim.x)
+      lq[q] = make_float4(m.basis[q], m.basis[F + q], m.basis[2 * F + q], 0.f);
+    lbasis = lq;
+    p += (size_t)F * 16;
+    float* lb = reinterpret_cast<float*>(p);
+    const int nb = (m.n_hidden + 2) * m.bias16_stride;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) lb[i] = m.bias32[i];
+    lbias = lb;
+    p += (size_t)nb * 4;
+    float4* ls = reinterpret_cast<float4*>(p);
+    if (s.kind == 2)
+      for (int i = threadIdx.x; i < s.n_spheres * 4; i += blockDim.x)
+        ls[i] = reinterpret_cast<const float4*>(s.spheres)[i];
+    lspheres = ls;
+    bstride = m.bias16_stride;
+    sbase = m.stream32;
+    sbytes = m.stream32_bytes;
+    lane = threadIdx.x & 63;
+    wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    off = 0;
+    slot = 0;
+    issue(0, nq0, 0);
+    __syncthreads();
+  }
+  // start of the current chunk (nq quads): wait for it, then DMA the next one (nq_next quads; at
+  // offset 0 when `wrap`, i.e. the next evaluation's first chunk); returns this lane's A base
+  __device__ __forceinline__ const float4* begin(int nq, int nq_next, bool wrap) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    next_off = wrap ? 0 : off + nq;
+    issue(next_off, nq_next, slot ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    return ring + slot * SLOTQ * 64 + lane;
+  }
+  __device__ __forceinline__ void end() {
+    off = next_off;
+    slot ^= 1;
+  }
+  // the DMA issued by the last begin() must land before the block's LDS is released
+  __device__ __forceinline__ void drain() { __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0)); }
+  // acc[reg] = bias[layer][16 sb + 4 g + reg]
+  __device__ __forceinline__ f4v bias_at(int layer, int sb) const {
+    const float4 q = *reinterpret_cast<const float4*>(lbias + layer * bstride + 16 * sb + 4 * (lane >> 4));
+    return f4v{q.x, q.y, q.z, q.w};
+  }
+};
+
+// torch's activation in exact FP32 (act_fwd<false>) with the code a template argument
+template <int ACT>
+__device__ __forceinline__ float act(float x) { return act_fwd<false>(x, ACT); }
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 16 rays, every lane of a ray gets
+// the value.  Every wave of the block must call it the same number of times.
+template <int KH, int KE, int WV, int ACT>
+__device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, float x0, float x1,
+                                      float x2) {
+  using En = Engine<KH, KE, WV>;
+  constexpr int QH = En::QH, QE = En::QE;
+  constexpr int NC = KH / 8;  // 32-row chunks per layer
+  const int g = E.lane >> 4;
+  const int F = m.freqs, L = m.n_hidden, SK = m.skip;
+  // encoding: k-step e of lane group g is slot 4 e + g: sin / cos of projection (4e + g) / 2
+  // (utils.py:37-40, same fma order and accurate sincosf as the FP32 slab path), then x, zeros
+  float eraw[KE], eact[KE];
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const int slot = 4 * e + g;
+    float v = 0.f;
+    if (slot < 2 * F) {
+      const float4 b = E.lbasis[slot >> 1];
+      float pr = x0 * b.x;
+      pr = fmaf(x1, b.y, pr);
+      pr = fmaf(x2, b.z, pr);
+      float sn, cs;
+      sincosf(pr, &sn, &cs);
+      v = (slot & 1) ? cs : sn;
+    } else if (slot == 2 * F) {
+      v = x0;
+    } else if (slot == 2 * F + 1) {
+      v = x1;
+    } else if (slot == 2 * F + 2) {
+      v = x2;
+    }
+    eraw[e] = v;
+    eact[e] = act<ACT>(v);
+  }
+  auto chunk_q = [&](int i) {  // quads of hidden layer i's chunks (i == L: the out layer)
+    if (i >= L) return QH;
+    return 2 * QH + ((i != L - 1 && i % SK == 0) ? 2 * QE : 0);
+  };
+  float src[KH], dst[KH];
+  f4v pend0, pend1;
+  auto retire = [&](int ib) {  // activation of chunk ib's accumulators into dst
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dst[8 * ib + r] = act<ACT>(pend0[r]);
+      dst[8 * ib + 4 + r] = act<ACT>(pend1[r]);
+    }
+  };
+  // init layer (neural_blocks.py:80): raw encoding in
+#pragma unroll
+  for (int ib = 0; ib < NC; ++ib) {
+    const float4* A = E.begin(2 * QE, ib + 1 < NC ? 2 * QE : chunk_q(0), false);
+    f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
+    if (ib > 0) retire(ib - 1);
+#pragma unroll
+    for (int u = 0; u < QE; ++u) {
+      const float4 w0 = A[(2 * u) * 64], w1 = A[(2 * u + 1) * 64];
+      a0 = mfma4(w0.x, eraw[4 * u], a0); a1 = mfma4(w1.x, eraw[4 * u], a1);
+      a0 = mfma4(w0.y, eraw[4 * u + 1], a0); a1 = mfma4(w1.y, eraw[4 * u + 1], a1);
+      a0 = mfma4(w0.z, eraw[4 * u + 2], a0); a1 = mfma4(w1.z, eraw[4 * u + 2], a1);
+      a0 = mfma4(w0.w, eraw[4 * u + 3], a0); a1 = mfma4(w1.w, eraw[4 * u + 3], a1);
+    }
+    pend0 = a0; pend1 = a1;
+    E.end();
+  }
+  retire(NC - 1);
+  // hidden layers: x = layer(act(cat[x, enc] if skip else x)) (neural_blocks.py:81-84)
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int k = 0; k < KH; ++k) src[k] = dst[k];
+    const bool skip = i != L - 1 && i % SK == 0;
+    const int nq = chunk_q(i);
+#pragma unroll
+    for (int ib = 0; ib < NC; ++ib) {
+      const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
+      f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
+      if (ib > 0) retire(ib - 1);
+#pragma unroll
+      for (int u = 0; u < QH; ++u) {
+        const float4 w0 = A[(2 * u) * 64], w1 = A[(2 * u + 1) * 64];
+        a0 = mfma4(w0.x, src[4 * u], a0); a1 = mfma4(w1.x, src[4 * u], a1);
+        a0 = mfma4(w0.y, src[4 * u + 1], a0); a1 = mfma4(w1.y, src[4 * u + 1], a1);
+        a0 = mfma4(w0.z, src[4 * u + 2], a0); a1 = mfma4(w1.z, src[4 * u + 2], a1);
+        a0 = mfma4(w0.w, src[4 * u + 3], a0); a1 = mfma4(w1.w, src[4 * u + 3], a1);
+      }
+      if (skip) {
+#pragma unroll
+        for (int u = 0; u < QE; ++u) {
+          const float4 w0 = A[(2 * (QH + u)) * 64], w1 = A[(2 * (QH + u) + 1) * 64];
+          a0 = mfma4(w0.x, eact[4 * u], a0); a1 = mfma4(w1.x, eact[4 * u], a1);
+          a0 = mfma4(w0.y, eact[4 * u + 1], a0); a1 = mfma4(w1.y, eact[4 * u + 1], a1);
+          a0 = mfma4(w0.z, eact[4 * u + 2], a0); a1 = mfma4(w1.z, eact[4 * u + 2], a1);
+          a0 = mfma4(w0.w, eact[4 * u + 3], a0); a1 = mfma4(w1.w, eact[4 * u + 3], a1);
+        }
+      }
+      pend0 = a0; pend1 = a1;
+      E.end();
+    }
+    retire(NC - 1);
+  }
+  // out layer (neural_blocks.py:86): one 16-row sub-block, two half chains (k-steps of even /
+  // odd quads) so consecutive MFMAs are independent; row 0 of ray j sits in register 0 of lane j
+  const float4* A = E.begin(QH, 2 * QE, true);
+  f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < QH; u += 2) {
+    const float4 w0 = A[u * 64], w1 = A[(u + 1) * 64];
+    o0 = mfma4(w0.x, dst[4 * u], o0); o1 = mfma4(w1.x, dst[4 * u + 4], o1);
+    o0 = mfma4(w0.y, dst[4 * u + 1], o0); o1 = mfma4(w1.y, dst[4 * u + 5], o1);
+    o0 = mfma4(w0.z, dst[4 * u + 2], o0); o1 = mfma4(w1.z, dst[4 * u + 6], o1);
+    o0 = mfma4(w0.w, dst[4 * u + 3], o0); o1 = mfma4(w1.w, dst[4 * u + 7], o1);
+  }
+  E.end();
+  const float o = o0[0] + o1[0];
+  return __shfl(o, E.lane & 15);
+}
+
+// sphere blob part of a SphereSDF (sdfs.py:37-43, utils.py:386-387) for a 16-ray tile: lane group
+// g sums exp(-k d_i) over spheres i = g, g + 4, ... from the LDS table, the four partial sums are
+// combined with two butterfly adds (commutative, so every lane gets the same bits)
+__device__ __forceinline__ float spheres_value16(const SdfDev& s, const float4* sp, int lane,
+                                                 float x, float y, float z) {
+  float acc = 0.f;
+  for (int i = lane >> 4; i < s.n_spheres; i += 4) {
+    const float4 r0 = sp[4 * i], r1 = sp[4 * i + 1], r2 = sp[4 * i + 2], r3 = sp[4 * i + 3];
+    // row-major (I+T): r0 = (m00 m01 m02 m10), r1 = (m11 m12 m20 m21), r2 = (m22 cx cy cz), r3 = (r ...)
+    const float qx = fmaf(r0.z, z, fmaf(r0.y, y, r0.x * x)) - r2.y;
+    const float qy = fmaf(r1.y, z, fmaf(r1.x, y, r0.w * x)) - r2.z;
+    const float qz = fmaf(r2.x, z, fmaf(r1.w, y, r1.z * x)) - r2.w;
+    const float d = sqrtf(qx * qx + qy * qy + qz * qz) - r3.x;
+    acc += expf(-s.k * d);
+  }
+  acc += __shfl_xor(acc, 16);
+  acc += __shfl_xor(acc, 32);
+  return -logf(fmaxf(acc, 1e-4f)) / s.k;
+}
+
+}  // namespace ring32
 }  // namespace nrt

@@ -110,6 +110,39 @@ struct ProfScope {
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 int max_hidden(const nrt_mlp* m);
+
+// Element order of the FP32 ring stream (MlpDev::stream32, consumed by nrt_device.h ring32 with
+// v_mfma_f32_16x16x4_f32 on 16-ray tiles).  Shared by the packer (values, nrt_pack.hip) and the
+// refresh map (source indices, nrt_refresh.hip).  f(layer, row, pos) is called once per stream
+// float, in order; pos is the layer input: hidden feature k in [0, H) or H + encoding slot; rows
+// past the layer's R are padding.
+//   chunk = 32 output rows (2 sub-blocks of 16) of one layer; the out layer is one chunk of one
+//   sub-block (rows 0..15).  A chunk is quads u = 0 .. qh + qe - 1 (qh = H / 16 hidden, qe =
+//   ke / 16 encoding quads), each quad [sub-block b][lane][t] = 1 KiB per sub-block: lane (g =
+//   lane >> 4, i = lane & 15) holds A[row 16 b + i][k = g] of k-steps 4u + t.  Hidden k-step s
+//   takes feature 16 (s >> 2) + 4 g + (s & 3) in lane group g -- register s & 3 of sub-block s >> 2
+//   of the previous layer's 16x16 accumulator -- and encoding k-step e takes slot 4 e + g.
+struct Ring32Layer {
+  int R;
+  bool hid, enc;
+};
+template <class F>
+inline void ring32_walk(const std::vector<Ring32Layer>& ls, int H, int ke, F&& f) {
+  for (size_t l = 0; l < ls.size(); ++l) {
+    const bool out = l + 1 == ls.size();
+    const int nsub = out ? 1 : 2, nch = out ? 1 : (ls[l].R + 31) / 32;
+    const int qh = ls[l].hid ? H / 16 : 0, qe = ls[l].enc ? ke / 16 : 0;
+    for (int c = 0; c < nch; ++c)
+      for (int u = 0; u < qh + qe; ++u)
+        for (int b = 0; b < nsub; ++b)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int t = 0; t < 4; ++t) {
+              const int s = 4 * u + t, g = lane >> 4;
+              const int pos = u < qh ? 16 * (s >> 2) + 4 * g + (s & 3) : H + 4 * (s - 4 * qh) + g;
+              f((int)l, 32 * c + 16 * b + (lane & 15), pos);
+            }
+  }
+}
 }  // namespace nrt
 
 #define NRT_HIP(call)                                         \

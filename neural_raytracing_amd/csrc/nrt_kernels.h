@@ -374,23 +374,53 @@ __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
   return ((uint64_t)b << 32) | (uint32_t)idx;
 }
 
-template <int NB, int NE, int WV, bool FOLD, int MODE>
-__device__ __forceinline__ void march16_body(
+// The SDF evaluator of a ring march: FP16 (32-ray tiles, ring::eval, fast sphere exp) or FP32
+// (16-ray tiles, ring32::eval, torch-exact transcendentals).  RPW rays per wave; lane l serves
+// ray l & (RPW - 1) and the other lanes of that ray mirror its state.
+template <int NB, int NE, int WV, bool FOLD>
+struct RingPol16 {
+  static constexpr int RPW = 32, WAVES = WV;
+  using Eng = ring::Engine<NB, NE, WV>;
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev&, const MlpDev& m, char* lds) { E.init(m, lds); }
+  __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
+    const float d = (s.kind == 2) ? spheres_value<true>(s, x, y, z) : 0.f;
+    return d + ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, x, y, z);
+  }
+  __device__ __forceinline__ static void finish(Eng&) {}
+};
+template <int KH, int KE, int WV, int ACT>
+struct RingPol32 {
+  static constexpr int RPW = 16, WAVES = WV;
+  using Eng = ring32::Engine<KH, KE, WV>;
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds) {
+    E.init(m, s, lds, 2 * Eng::QE);
+  }
+  __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
+    const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
+    return d + ring32::eval<KH, KE, WV, ACT>(E, m, x, y, z);
+  }
+  __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
+};
+
+template <class Pol, int MODE>
+__device__ __forceinline__ void march_body(
     const SdfDev s, const MlpDev m, const float* __restrict__ rays, int64_t P, MarchArgs a,
     float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
     float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,
     unsigned long long* __restrict__ keys) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   constexpr int mode = MODE;
-  const int lane = lane_id(), r = lane & 31;
+  constexpr int RPW = Pol::RPW, WV = Pol::WAVES;
+  constexpr uint32_t kRayMask = RPW == 32 ? 0xffffffffu : ((1u << RPW) - 1u);
+  const int lane = lane_id(), r = lane & (RPW - 1);
   const int64_t nw = (int64_t)gridDim.x * WV;
   const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t R = w < P ? (P - 1 - w) / nw + 1 : 0;  // rays owned by this wave
   const bool scan = mode == 0 && a.primary;
   const int64_t J = mode == 0 ? R * (scan ? 1 + kScanSegs : 1) : R;
   const uint32_t lt = (1u << r) - 1u;
-  ring::Engine<NB, NE, WV> E;
-  E.init(m, smem_c);
+  typename Pol::Eng E;
+  Pol::init(E, s, m, smem_c);
   // lane state: kind -1 = wants a job, -2 = list exhausted, 0 march, 1 scan segment, 2 sdf(best)
   int kind = -1;
   int64_t ray = 0;
@@ -405,7 +435,7 @@ __device__ __forceinline__ void march16_body(
       if (kind == 0) {
         // sdfs.py:119-131: a march ends on a hit, when t leaves [0, max_t) or after max_steps
         if (ended || !(t < a.max_t) || i >= a.max_steps) {
-          if (lane < 32) {
+          if (lane < RPW) {
             t_out[ray] = t;
             hit_out[ray] = hit ? 1 : 0;
             p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
@@ -418,13 +448,13 @@ __device__ __forceinline__ void march16_body(
         }
       } else if (kind == 1) {
         if (j > jend) {
-          if (lane < 32) atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
+          if (lane < RPW) atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
           kind = -1;
         }
       } else if (kind == 2) {
         if (ended) kind = -1;
       }
-      const uint32_t want = (uint32_t)__ballot(kind == -1);
+      const uint32_t want = (uint32_t)__ballot(kind == -1) & kRayMask;
       if (want == 0u) break;
       if (cursor >= J) {
         if (kind == -1) kind = -2;
@@ -474,8 +504,7 @@ __device__ __forceinline__ void march16_body(
         pz = __fadd_rn(oz, __fmul_rn(ts, dz));
       }
     }
-    float d = (s.kind == 2) ? spheres_value<true>(s, px, py, pz) : 0.f;
-    d += ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, px, py, pz);
+    const float d = Pol::sdf(E, s, m, px, py, pz);
     if (kind == 0) {
       if (d <= a.eps) { hit = true; ended = true; }
       else t = t + d;
@@ -489,10 +518,11 @@ __device__ __forceinline__ void march16_body(
       }
       ++j;
     } else if (kind == 2) {
-      if (lane < 32) thr_out[ray] = -1000.f * d;
+      if (lane < RPW) thr_out[ray] = -1000.f * d;
       ended = true;
     }
   }
+  Pol::finish(E);
 }
 
 // the two passes as separately named kernels (profiles time the march + scan launch alone)
@@ -501,14 +531,26 @@ __device__ __forceinline__ void march16_body(
       float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,     \
       float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,    \
       unsigned long long* __restrict__ keys
+#define NRT_MARCH_PASS t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys
 template <int NB, int NE, int WV, bool FOLD>
 __global__ void __launch_bounds__(64 * WV, 2) k_march16(NRT_MARCH_ARGS) {
-  march16_body<NB, NE, WV, FOLD, 0>(s, m, rays, P, a, t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys);
+  march_body<RingPol16<NB, NE, WV, FOLD>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 template <int NB, int NE, int WV, bool FOLD>
 __global__ void __launch_bounds__(64 * WV, 2) k_scan_best16(NRT_MARCH_ARGS) {
-  march16_body<NB, NE, WV, FOLD, 1>(s, m, rays, P, a, t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys);
+  march_body<RingPol16<NB, NE, WV, FOLD>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
+// FP32 (reference precision): one block of WV waves per CU (the ring takes most of the LDS), two
+// waves per SIMD
+template <int KH, int KE, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_march32(NRT_MARCH_ARGS) {
+  march_body<RingPol32<KH, KE, WV, ACT>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+template <int KH, int KE, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_scan_best32(NRT_MARCH_ARGS) {
+  march_body<RingPol32<KH, KE, WV, ACT>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+#undef NRT_MARCH_PASS
 #undef NRT_MARCH_ARGS
 
 // coarse-scan argmin index of each ray from the ring march's 64-bit keys ([ordered min | idx])

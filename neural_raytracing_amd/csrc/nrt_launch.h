@@ -117,6 +117,30 @@ int ring_dispatch(const nrt_sdf* s, F&& f) {
 int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                int32_t* cnt, unsigned long long* keys, hipStream_t st);
+
+// ---- FP32 ring engine (nrt_ring_march32.hip) ----
+// SDF MLPs with a compiled FP32 ring kernel: hidden 128 / 256, F = 16 / 32 with 3 inputs and no
+// latent (ke = 48 / 80), <= 16 outputs, softplus or leaky_relu; any layer count and skip period.
+// Refreshed handles qualify (nrt_mlp_refresh re-gathers stream32).
+constexpr int kRing32Waves = 8;
+inline size_t ring32_bias_bytes(const nrt_sdf* s) {
+  return (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
+}
+inline size_t ring32_sphere_bytes(const nrt_sdf* s) {
+  return s->host_dev.kind == 2 ? (size_t)s->host_dev.n_spheres * 64 : 0;
+}
+inline bool ring32_supported(const nrt_sdf* s) {
+  if (!s->mlp) return false;
+  const MlpDev& m = s->mlp->host_dev;
+  const int act = s->mlp->desc.activation;
+  if (!((m.hidden == 128 || m.hidden == 256) && (m.ke == 48 || m.ke == 80) && m.in_size == 3 &&
+        m.latent == 0 && m.out <= 16 && (act == NRT_ACT_SOFTPLUS || act == NRT_ACT_LEAKY_RELU)))
+    return false;
+  return ring32_sphere_bytes(s) + ring32_bias_bytes(s) <= 48 * 1024;
+}
+int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                 int32_t* cnt, unsigned long long* keys, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
 inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,

@@ -240,6 +240,23 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   }
   const int nk_frags = (int)(streamk.size() / (64 * 8));
   streamk.resize(streamk.size() + (size_t)64 * 64 * 8, (_Float16)0.f);
+
+  // ---- FP32 ring stream (nrt_device.h ring32, v_mfma_f32_16x16x4_f32 on 16-ray tiles)
+  std::vector<float> stream32;
+  {
+    std::vector<Ring32Layer> rl;
+    for (const Layer& ly : layers) rl.push_back({ly.R, ly.hidden_in, ly.enc_in});
+    ring32_walk(rl, H, ke, [&](int l, int row, int pos) {
+      const Layer& ly = layers[l];
+      const int col = pos < H ? col_of_hidden(pos) : col_of_slot(ly, pos - H);
+      stream32.push_back(wval(ly, row, col));
+    });
+  }
+  std::vector<float> bias32(layers.size() * (size_t)bstride, 0.f);
+  for (size_t l = 0; l < layers.size(); ++l)
+    for (int r = 0; r < layers[l].R; ++r) bias32[l * bstride + r] = layers[l].b[r];
+  size_t off_stream32 = blob.add(stream32.data(), stream32.size() * sizeof(float));
+  size_t off_b32 = blob.add(bias32.data(), bias32.size() * sizeof(float));
   size_t off_streamk = blob.add(streamk.data(), streamk.size() * sizeof(_Float16));
   size_t off_coffk = blob.add(chunkk_off.data(), chunkk_off.size() * sizeof(int));
   size_t off_stream = blob.add(stream.data(), stream.size() * sizeof(_Float16));
@@ -280,6 +297,9 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   md.nk_chunks = (int)chunkk_off.size();
   md.kc = kc;
   md.nk_frags = nk_frags;
+  md.stream32 = reinterpret_cast<const float4*>(base + off_stream32);
+  md.stream32_bytes = (int)(stream32.size() * sizeof(float));
+  md.bias32 = reinterpret_cast<const float*>(base + off_b32);
   m->host_dev = md;
   NRT_HIP(hipMalloc(&m->dev, sizeof(MlpDev)));
   NRT_HIP(hipMemcpy(m->dev, &md, sizeof(MlpDev), hipMemcpyHostToDevice));

@@ -4,8 +4,9 @@
 // every optimiser step.  nrt_mlp_refresh instead gathers the caller's device weights into the
 // fragment arrays the training kernels read -- FP16 / FP32 A fragments, FP32 W^T fragments,
 // padded biases, out.weight row 0 -- through a per-element index map built once on the host by
-// the same loops as nrt_pack.hip.  The FP16 ring / program streams are not refreshed; a refreshed
-// handle refuses those paths (ring_supported, build_program).
+// the same loops as nrt_pack.hip.  The FP32 ring stream is refreshed too (the FP32 march of a
+// training loop runs on it); the FP16 ring / program streams are not, and a refreshed handle
+// refuses those paths (ring_supported, build_program).
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -118,6 +119,21 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
   }
   begin((void*)md.wout_row0, false);  // out.weight[0, :]
   for (int k = 0; k < H; ++k) map.push_back(idx(ls.back(), 0, k));
+  end();
+  {  // FP32 ring stream (same walk as the packer)
+    std::vector<Ring32Layer> rl;
+    for (const Ly& l : ls) rl.push_back({l.R, l.hid, l.enc});
+    begin((void*)md.stream32, false);
+    ring32_walk(rl, H, ke, [&](int li, int row, int pos) {
+      const Ly& l = ls[li];
+      map.push_back(idx(l, row, pos < H ? pos : col_slot(l, pos - H)));
+    });
+    end();
+  }
+  begin((void*)md.bias32, false);  // [layer][bias16_stride]
+  for (size_t li = 0; li < ls.size(); ++li)
+    for (int r = 0; r < md.bias16_stride; ++r)
+      map.push_back(r < ls[li].R ? (int)(ls[li].boff + r) : -1);
   end();
 }
 

@@ -1,0 +1,57 @@
+// FP32 (reference-precision) march + coarse scan on the block-cooperative LDS weight ring
+// (k_march32 / k_scan_best32, nrt_device.h ring32): same job lists and persistent grid as the
+// FP16 ring march (nrt_ring_march.hip), 16-ray tiles, torch-exact transcendentals.
+#include "nrt_launch.h"
+
+namespace nrt {
+
+int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                 int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+  const MlpDev& md = s->mlp->host_dev;
+  const size_t extra = (size_t)md.freqs * 16 + ring32_bias_bytes(s) + ring32_sphere_bytes(s);
+  int dev = 0, cus = 0;
+  NRT_HIP(hipGetDevice(&dev));
+  NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  const bool scan = ma.primary != 0;
+  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
+  auto run = [&]<int KH, int KE, int ACT>() -> int {
+    constexpr int WV = kRing32Waves;
+    auto launch = [&](auto kern, const char* name) -> int {
+      const size_t lds = ring32::Engine<KH, KE, WV>::RING_BYTES + extra;
+      if (int rc = set_lds(kern, lds)) return rc;
+      int per_cu = 0;
+      NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WV, lds));
+      const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
+      int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * WV)));
+      if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
+      ProfScope prof(name, st);
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, p, n,
+                                                     raw_n, thr, keys);
+      return check_launch(name);
+    };
+    if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32")) return rc;
+    if (scan) return launch(k_scan_best32<KH, KE, WV, ACT>, "k_scan_best32");
+    return NRT_OK;
+  };
+  const bool sp = s->mlp->desc.activation == NRT_ACT_SOFTPLUS;
+  int rc = NRT_EINVAL;
+#define NRT_R32(H, KEV)                                                                   \
+  if (md.hidden == H && md.ke == 4 * KEV)                                                 \
+    rc = sp ? run.template operator()<H / 4, KEV, ACT_SOFTPLUS>()                         \
+            : run.template operator()<H / 4, KEV, ACT_LEAKY>();                           \
+  else
+  NRT_R32(256, 12) NRT_R32(256, 20) NRT_R32(128, 12) NRT_R32(128, 20) {
+    set_error("FP32 ring engine: unsupported SDF configuration");
+    return NRT_EINVAL;
+  }
+#undef NRT_R32
+  if (rc) return rc;
+  if (idx) {
+    k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
+    if (int rc2 = check_launch("k_hit_list")) return rc2;
+  }
+  return NRT_OK;
+}
+
+}  // namespace nrt

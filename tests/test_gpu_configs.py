@@ -380,7 +380,17 @@ def test_direct_normalized_weights_cover_misses():
     assert 0 < active.float().mean() < 1  # hits and misses
     got = it.normalized_weights.cpu()
     assert got.shape == rit.normalized_weights.shape == (1, 24, 24, 1, 8)
-    assert (got - rit.normalized_weights).abs().max().item() <= 1e-4
+    err = (got - rit.normalized_weights).abs().amax(-1).reshape(-1)
+    # a miss's p = o + t d sits after up to 48 march steps whose t sums differ in the last ulps
+    # (FP32 summation order of the SDF MLP): the weights there follow p's error through
+    # sp_var_fn (Fourier features of sigma 32), so the bound on misses is 1e-4 + 100 |dp|
+    dp = (it.p.cpu() - rit.p).abs().amax(-1).reshape(-1)
+    hit = active.cpu().reshape(-1).bool()
+    report("normalized_weights_all_rays[fp32]", rays=hit.numel(), hits=int(hit.sum()),
+           hit_maxabs=err[hit].max().item(), miss_maxabs=err[~hit].max().item(),
+           miss_dp_maxabs=dp[~hit].max().item())
+    assert err[hit].max().item() <= 1e-4
+    assert (err[~hit] <= 1e-4 + 100 * dp[~hit]).all()
     raw = it.nonnormalized_weights.cpu()
     assert torch.allclose(raw.sigmoid(), got, atol=1e-6)
 

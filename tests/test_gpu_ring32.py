@@ -1,0 +1,207 @@
+"""The FP32 ring march (k_march32 / k_scan_best32, nrt_device.h ring32): reference-precision sphere
+tracing + coarse scan with the SDF MLP on v_mfma_f32_16x16x4_f32 and the weights streamed through
+the block's LDS ring.
+
+* against the oracle (sdfs.py:111-160, 232-249) on the configurations it serves: SphereSDF(n=128)
+  + 8x128 F=32 shift (the training SDF), the bare 8x256 F=16 MLP SDF, leaky_relu shifts;
+* against the FP32 slab kernel k_intersect (NRT_NO_RING32=1) on the same inputs;
+* independent of the persistent grid's size (NRT_MARCH_BLOCKS);
+* after nrt_mlp_refresh (the training handle re-gathers stream32 on the device) the march equals a
+  freshly packed handle's.
+FP32 bar: 1e-4 abs on rays whose hit flag and step count agree; flips reported and bounded.
+"""
+import os
+import random
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import bench
+from oracle import pathtracer_ref as R
+from tests.helpers import copy_mlp, product_mlp_like, seeded
+from tests.report import report
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    yield
+    set_precision("fp32")
+    os.environ.pop("NRT_NO_RING32", None)
+    os.environ.pop("NRT_MARCH_BLOCKS", None)
+
+
+def _rays(n, seed, eye=(0.0, 0.1, 1.0), spread=0.9):
+    g = torch.Generator().manual_seed(seed)
+    o = torch.tensor(eye).expand(1, n, n, 1, 3)
+    d = F.normalize(torch.cat([torch.rand(1, n, n, 1, 2, generator=g) * spread - spread / 2,
+                               -torch.ones(1, n, n, 1, 1)], -1), dim=-1)
+    return torch.cat([o, d], -1)
+
+
+def _blob(n, hidden, freqs, act, seed=5):
+    """oracle SphereBlobSDF + the product SphereSDF with the same tensors; the shift gets a
+    visible residual (out weights x0.05) so the MLP part shapes the surface."""
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.shapes import SphereSDF
+    seeded(seed)
+    ref = R.SphereBlobSDF(n=n, shift_hidden=hidden, shift_freqs=freqs, shift_zero_init=False)
+    if act != "softplus":
+        ref.shift = R.SkipMLP(num_layers=8, hidden_size=hidden, out=1, freqs=freqs, activation=act)
+    with torch.no_grad():
+        ref.radii.add_(0.12)
+        ref.tfs.copy_(0.05 * torch.randn_like(ref.tfs))
+        ref.shift.out.weight.mul_(0.05)
+        ref.shift.out.bias.mul_(0.05)
+    mine = SphereSDF(n=n, device="cpu")
+    kw = {"activation": F.softplus} if act == "softplus" else {}
+    mine.shift = SkipConnMLP(num_layers=8, hidden_size=hidden, in_size=3, out=1, freqs=freqs,
+                             device="cpu", **kw)
+    with torch.no_grad():
+        mine.centers.copy_(ref.centers)
+        mine.radii.copy_(ref.radii)
+        mine.tfs.copy_(ref.tfs)
+    copy_mlp(mine.shift, ref.shift)
+    return ref, mine.cuda()
+
+
+def _march(sdf, rays, primary=True, steps=64, seed=12):
+    """(it, hit, kernel launches of k_march32) of SDF.intersect on the HIP path."""
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    random.seed(seed)
+    with torch.no_grad():
+        it, hit = SDF(sdf=sdf, max_steps=steps).intersect(rays.cuda(), primary=primary)
+    n32 = _lib.profile_read("k_march32")[1]
+    _lib.profile_enable(False)
+    return it, hit, n32
+
+
+def _intersect_raw(sh, rays, max_steps):
+    """nrt_sdf_intersect (FP32, primary) on a raw handle: (t, hit, p, n, throughput)."""
+    import ctypes
+    from neural_raytracing_amd import _lib
+    P, dev = rays.shape[0], rays.device
+    t = torch.empty(P, device=dev)
+    hit = torch.empty(P, dtype=torch.uint8, device=dev)
+    p, n, raw, wi = (torch.empty(P, 3, device=dev) for _ in range(4))
+    thr = torch.empty(P, device=dev)
+    idx = torch.empty(P, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    lib = _lib.load(require_device=True)
+    ws = torch.empty(max(lib.nrt_intersect_workspace_bytes(sh, P), 1), dtype=torch.uint8, device=dev)
+    mp = _lib.MarchParams(max_steps, 5e-3, 10.0, 1, 2.2, _lib.NRT_FP32)
+    _lib.call("nrt_sdf_intersect", sh, _lib.ptr(rays), P, ctypes.byref(mp), _lib.ptr(t),
+              _lib.ptr(hit), _lib.ptr(p), _lib.ptr(n), _lib.ptr(raw), _lib.ptr(wi), _lib.ptr(thr),
+              _lib.ptr(idx), _lib.ptr(cnt), _lib.ptr(ws), _lib.stream())
+    torch.cuda.synchronize()
+    return t, hit, p, n, thr
+
+
+def _compare(name, it, hit, rit, rhit, tol=1e-4, flip_frac=0.005):
+    hit, rhit = hit.cpu().reshape(-1), rhit.cpu().reshape(-1)
+    t, rt = it.t.cpu().reshape(-1), rit.t.cpu().reshape(-1)
+    step = (hit & rhit) & ((t - rt).abs() > tol)
+    m = (hit & rhit) & ~step
+    flips = int((hit != rhit).sum())
+    errs = {
+        "t_maxabs": (t[m] - rt[m]).abs().max().item() if m.any() else 0.0,
+        "n_maxabs": (it.n.cpu().reshape(-1, 3)[m] - rit.n.cpu().reshape(-1, 3)[m]).abs().max().item() if m.any() else 0.0,
+    }
+    thr = None
+    if getattr(it, "throughput", None) is not None and getattr(rit, "throughput", None) is not None:
+        thr = (it.throughput.cpu().reshape(-1) - rit.throughput.cpu().reshape(-1)).abs()
+        errs["thr_maxabs"] = thr.max().item()
+    report(name, rays=hit.numel(), hits=int(rhit.sum()), flips=flips, step_flips=int(step.sum()),
+           **errs)
+    assert flips + int(step.sum()) <= flip_frac * hit.numel(), (flips, int(step.sum()))
+    assert errs["t_maxabs"] <= tol and errs["n_maxabs"] <= tol
+    if thr is not None:  # -1000 sdf(best): 1e-4 on the sdf is 0.1
+        assert (thr <= 0.1).float().mean() >= 0.995
+    return m
+
+
+@pytest.mark.parametrize("hidden,freqs,act", [(128, 32, "softplus"), (256, 16, "softplus"),
+                                              (128, 16, "leaky_relu"), (256, 32, "leaky_relu")])
+def test_ring32_sphere_sdf_matches_oracle(hidden, freqs, act):
+    ref, mine = _blob(128, hidden, freqs, act)
+    rays = _rays(36, 7, eye=(0.0, 0.2, 1.1))
+    it, hit, n32 = _march(mine, rays)
+    assert n32 >= 1, "the FP32 ring kernel did not run"
+    random.seed(12)
+    jit = random.random()
+    with torch.no_grad():
+        rit, rhit = R.MarchedSDF(sdf=ref, max_steps=64).intersect(rays, primary=True, jitter=jit)
+    assert 0.1 < rhit.float().mean() < 0.9
+    _compare(f"ring32_sphere_sdf_vs_oracle[{hidden},{freqs},{act}]", it, hit, rit, rhit)
+
+
+def test_ring32_bare_mlp_matches_slab_kernel():
+    """k_march32 vs the FP32 slab k_intersect on the bare 8x256 MLP SDF (cfg2 / cfg4 kind)."""
+    seeded(41)
+    ref = R.SkipMLP(num_layers=8, hidden_size=256, out=1, freqs=16, activation="softplus")
+    bench.shape_mlp_sdf(ref, radius=0.3)
+    mine = product_mlp_like(ref, "softplus")
+    rays = _rays(40, 3)
+    it, hit, n32 = _march(mine, rays)
+    assert n32 >= 1
+    os.environ["NRT_NO_RING32"] = "1"
+    sit, shit, n32b = _march(mine, rays)
+    assert n32b == 0
+    _compare("ring32_vs_slab[bare 8x256]", it, hit, sit, shit)
+    # the coarse-scan argmin (throughput's sample) agrees on all but rounding ties
+    assert (it.throughput - sit.throughput).abs().le(0.1).float().mean().item() >= 0.995
+
+
+def test_ring32_independent_of_grid_size():
+    """The job lists are per wave and the scan merge is an order-independent min: any persistent
+    grid gives bit-identical results."""
+    _, mine = _blob(128, 128, 32, "softplus", seed=9)
+    rays = _rays(24, 11, eye=(0.0, 0.2, 1.1))
+    base, bh, _ = _march(mine, rays)
+    for blocks in ("1", "5"):
+        os.environ["NRT_MARCH_BLOCKS"] = blocks
+        it, h, _ = _march(mine, rays)
+        assert torch.equal(h, bh)
+        assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)
+        assert torch.equal(it.p, base.p) and torch.equal(it.n, base.n)
+
+
+def test_ring32_after_device_refresh_matches_fresh_pack():
+    """nrt_mlp_refresh re-gathers stream32 / bias32 on the device: a handle refreshed to new
+    weights marches exactly like a handle packed from them on the host."""
+    import ctypes
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer._handles import train_handle, mlp_handle
+    _, mine = _blob(64, 128, 32, "softplus", seed=13)
+    mlp = mine.shift
+    th = train_handle(mlp)  # packed from the current weights
+    with torch.no_grad():
+        for lin in mlp._linears():
+            lin.weight.add_(0.01 * torch.randn_like(lin.weight))
+            lin.bias.add_(0.01 * torch.randn_like(lin.bias))
+    th2 = train_handle(mlp)  # same handle, refreshed on the device
+    assert th2 is th
+    fresh = mlp_handle(mlp)  # host-packed from the new weights
+    assert fresh is not th
+    rays = _rays(24, 17, eye=(0.0, 0.2, 1.1)).cuda().reshape(-1, 6).contiguous()
+    P = rays.shape[0]
+    c, r, t = (x.detach().cpu().contiguous() for x in (mine.centers, mine.radii, mine.tfs))
+    outs = []
+    for h in (th, fresh):
+        sh = ctypes.c_void_p()
+        _lib.check(_lib.load().nrt_sdf_create_sphere_blob(
+            c.shape[0], c.data_ptr(), r.data_ptr(), t.data_ptr(), 32.0, h.value, ctypes.byref(sh)),
+            "nrt_sdf_create_sphere_blob")
+        try:
+            outs.append(_intersect_raw(sh, rays, max_steps=64))
+        finally:
+            _lib.load().nrt_sdf_destroy(sh)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
