@@ -258,8 +258,10 @@ def main():
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
-        k_ms, k_n = _lib.profile_read("k_march16")
+        march_kernel = "k_march16" if args.precision == "fp16" else "k_march32"
+        k_ms, k_n = _lib.profile_read(march_kernel)
         i_ms, i_n = _lib.profile_read("k_intersect")
+        evals = _lib.profile_evals()
         if world > 1:
             t = torch.tensor([elapsed], device=device)
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -276,6 +278,10 @@ def main():
     avg_kernel_ms = k_ms / max(k_n, 1)
     achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
+    # executed work of the march launch: evaluations the job lists actually ran (counted on the
+    # device while profiling), less the sdf(best) pass's one per ray
+    exec_flop = (evals / max(args.steps, 1) - rays_per_rank) * FLOP_SDF_8x256
+    exec_achieved = exec_flop / (avg_kernel_ms * 1e-3) / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
     if os.path.exists(pmc_path):
@@ -324,7 +330,7 @@ def main():
             },
             "roofline": {
                 "bound": "mfma",
-                "kernel": "k_march16",
+                "kernel": march_kernel,
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",
@@ -334,6 +340,11 @@ def main():
                                    f"(FETCH_SIZE + WRITE_SIZE, {size}^2 {args.precision}); not "
                                    "measured in this run") if traffic is not None else None,
                 "flop_per_launch": flop_launch,
+                "flop_basis": "algorithmic: every ray at every march step and scan point "
+                              "(sdfs.py:119-131, 232-249)",
+                "executed_flop_per_launch": exec_flop,
+                "executed_achieved": exec_achieved,
+                "executed_frac": exec_achieved / peak,
                 "avg_kernel_ms": avg_kernel_ms,
                 "launches": k_n,
                 "intersect_ms": i_ms / max(i_n, 1),
@@ -374,21 +385,26 @@ def extra_legs(scene, cameras, size, args, rows):
     out = {}
     S = args.samples
     frame_rays = len(rows) * size * len(cameras)
-    # FP32 leg: k_intersect (exact-f32 MFMA march + scan) on the 157.3 TF FP32 matrix peak
+    # FP32 leg: k_march32 (exact-f32 MFMA march + scan on the LDS ring) on the 157.3 TF FP32
+    # matrix peak
+    from neural_raytracing_amd import _lib
     nra.set_precision("fp32")
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
                      size, rows, background=0.0, with_noise=1e-3, device=cameras.cam_to_world.device)
     steps = 2
-    el, ks = _time_frames(rr.render, steps, 1, ["k_intersect"])
-    k_ms = ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)
-    flop = frame_rays * (S + SCAN_EVALS) * FLOP_SDF_8x256  # march + scan + sdf(best): one launch
+    el, ks = _time_frames(rr.render, steps, 1, ["k_march32", "k_intersect"])
+    evals = _lib.profile_evals()
+    k_ms = ks["k_march32"][0] / max(ks["k_march32"][1], 1)
+    flop = frame_rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256  # march + scan launch
     ach = flop / (k_ms * 1e-3) / 1e12
+    exe = (evals / steps - frame_rays) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
     out["fp32"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                    "ms_per_step": 1000 * el / steps, "steps": steps,
-                   "roofline": {"bound": "mfma", "kernel": "k_intersect", "achieved": ach,
+                   "roofline": {"bound": "mfma", "kernel": "k_march32", "achieved": ach,
                                 "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
                                 "frac": ach / PEAK_TFLOPS["fp32"], "avg_kernel_ms": k_ms,
-                                "flop_per_launch": flop}}
+                                "flop_per_launch": flop, "executed_frac": exe / PEAK_TFLOPS["fp32"],
+                                "intersect_ms": ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)}}
     nra.set_precision(args.precision)
     # scan-free leg: Direct with training = False (the reference's Path / primary=False march)
     direct = Direct()
@@ -398,15 +414,21 @@ def extra_legs(scene, cameras, size, args, rows):
                      device=cameras.cam_to_world.device)
     steps = 3
     el, ks = _time_frames(rr.render, steps, 1, ["k_march16"])
+    evals = _lib.profile_evals()
     k_ms = ks["k_march16"][0] / max(ks["k_march16"][1], 1)
     flop = frame_rays * S * FLOP_SDF_8x256
     ach = flop / (k_ms * 1e-3) / 1e12
+    # without the scan a ray stops at its hit (or at max_t): the algorithmic count (every ray at
+    # every step, as the reference evaluates) is far above what the job lists execute
+    exe = (evals / steps) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
     out["scan_free"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                         "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": args.precision,
                         "roofline": {"bound": "mfma", "kernel": "k_march16", "achieved": ach,
                                      "peak": PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
                                      "frac": ach / PEAK_TFLOPS[args.precision],
-                                     "avg_kernel_ms": k_ms, "flop_per_launch": flop}}
+                                     "avg_kernel_ms": k_ms, "flop_per_launch": flop,
+                                     "executed_frac": exe / PEAK_TFLOPS[args.precision],
+                                     "executed_evals_per_ray": evals / steps / frame_rays}}
     return out
 
 

@@ -338,6 +338,24 @@ int nrt_light_envmap(const nrt_light* light, int32_t bins, float* out, void* str
 void nrt_profile_enable(int on);
 void nrt_profile_reset(void);
 int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
+/* SDF evaluations (ray x point) the ring marches (k_march16 / k_scan_best16 / k_march32 /
+ * k_scan_best32) executed while profiling was enabled, since the last nrt_profile_reset: the
+ * executed work behind the algorithmic count (every ray at every march step and scan point,
+ * sdfs.py:119-131, 232-249), which the lane-level job lists lower.  Synchronises. */
+int nrt_profile_evals(uint64_t* evals);
+
+/* ---------------------------------------------------------------------------------------
+ * Diagnostic environment variables (A/B and schedule tests; none is set in normal use, and
+ * each one only selects between two implementations that the parity tests hold to the same
+ * oracle bar, or changes the grid size of a schedule-independent kernel):
+ *   NRT_NO_RING       FP16 SDF march / normals on the per-wave kernels instead of the LDS ring
+ *   NRT_NO_RING32     FP32 SDF march on the per-wave slab kernel k_intersect instead of k_march32
+ *   NRT_F32_NORMALS   FP32 backward normals after an FP16 ring march (instead of k_normal16)
+ *   NRT_MARCH_BLOCKS  persistent-grid size of the ring marches (results are bit-identical)
+ *   NRT_NO_PROGRAM    FP16 shading MLPs per component instead of the fused program kernel
+ *   NRT_NERF_UNFUSED  FP16 NeRFLE on separate MLP launches instead of k_nerfle16
+ *   NRT_MAX_WAVES     waves per block (1..4) of the per-wave kernels
+ * ------------------------------------------------------------------------------------- */
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,7 @@ _SIGNATURES = {
     "nrt_profile_reset": (None, []),
     "nrt_profile_read": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_I64)]),
+    "nrt_profile_evals": (_I32, [ctypes.POINTER(ctypes.c_uint64)]),
     "nrt_composite": (_I32, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _I32, _I32, _I32,
                              _I32, _I32, _P]),
 }
@@ -181,6 +182,14 @@ def profile_enable(on=True):
 
 def profile_reset():
     load().nrt_profile_reset()
+
+
+def profile_evals():
+    """SDF evaluations (ray x point) the ring marches executed since the last reset while profiling
+    was enabled: the executed work behind an algorithmic FLOP count."""
+    v = ctypes.c_uint64()
+    check(load().nrt_profile_evals(ctypes.byref(v)), "nrt_profile_evals")
+    return v.value
 
 
 def profile_read(name):

@@ -177,6 +177,7 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   ma.primary = a->primary;
   ma.step = a->scan_max_t / 128.0;
   ma.scan_idx = a->primary ? a->scan_index : nullptr;
+  ma.evals = profile_eval_counter();
   // the normal pass needs the list of hit rays; use the caller's or a workspace-backed one
   int32_t* idx = hit_idx;
   int32_t* cnt = hit_count;

@@ -37,17 +37,48 @@ ProfScope::~ProfScope() {
   g_recs.push_back({name, start, stop});
 }
 
+static unsigned long long* g_evals[64] = {};
+
+unsigned long long* profile_eval_counter() {
+  if (!g_prof) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!g_evals[dev]) {
+    if (hipMalloc(&g_evals[dev], sizeof(unsigned long long)) != hipSuccess) { g_evals[dev] = nullptr; return nullptr; }
+    if (hipMemset(g_evals[dev], 0, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+  }
+  return g_evals[dev];
+}
+
 }  // namespace nrt
 
 using namespace nrt;
 
 extern "C" {
 
-void nrt_profile_enable(int on) { nrt::g_prof = on != 0; }
+void nrt_profile_enable(int on) {
+  nrt::g_prof = on != 0;
+  if (nrt::g_prof) (void)nrt::profile_eval_counter();  // allocate outside any timed region
+}
 
 void nrt_profile_reset(void) {
   for (auto& r : nrt::g_recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   nrt::g_recs.clear();
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && nrt::g_evals[dev])
+    (void)hipMemset(nrt::g_evals[dev], 0, sizeof(unsigned long long));
+}
+
+int nrt_profile_evals(uint64_t* evals) {
+  if (!evals) { set_error("nrt_profile_evals: null argument"); return NRT_EINVAL; }
+  *evals = 0;
+  int dev = 0;
+  NRT_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64 || !nrt::g_evals[dev]) return NRT_OK;
+  unsigned long long v = 0;
+  NRT_HIP(hipMemcpy(&v, nrt::g_evals[dev], sizeof(v), hipMemcpyDeviceToHost));
+  *evals = v;
+  return NRT_OK;
 }
 
 int nrt_profile_read(const char* name, double* total_ms, int64_t* launches) {

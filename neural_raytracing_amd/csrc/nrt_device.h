@@ -1321,9 +1321,54 @@ struct Engine {
   }
 };
 
-// torch's activation in exact FP32 (act_fwd<false>) with the code a template argument
+// F.softplus (beta 1, threshold 20) in FP32 on the hardware transcendentals: max(x, 0) +
+// log1p(e), e = exp(-|x|) in (0, 1], with log1p(e) = log(u) e / (u - 1), u = fl(1 + e) -- the
+// classic compensation of the rounding of 1 + e (Goldberg), accurate to a few ulp with the ~1-ulp
+// v_exp / v_log / v_rcp.  ~12 VALU against ~100 for ocml's log1pf(expf(x)) (double-float
+// arithmetic), which left the FP32 march VALU-bound: one chunk's activations (8 per lane) cost as
+// much issue time as its 128 MFMAs.
+__device__ __forceinline__ float softplus_f32(float x) {
+  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+  const float u = 1.f + e;
+  const float d = u - 1.f;
+  const float l1p = d == 0.f ? e : (__builtin_amdgcn_logf(u) * kLn2) * (e * __builtin_amdgcn_rcpf(d));
+  return x > 20.f ? x : fmaxf(x, 0.f) + l1p;
+}
+
+// the MLP activation with the code a template argument (torch semantics, FP32)
 template <int ACT>
-__device__ __forceinline__ float act(float x) { return act_fwd<false>(x, ACT); }
+__device__ __forceinline__ float act(float x) {
+  if (ACT == ACT_SOFTPLUS) return softplus_f32(x);
+  return act_fwd<false>(x, ACT);
+}
+
+// One segment of a two-sub-block chunk: NQ quads at ring positions P0 + 2u + b (sub-block b),
+// k-step 4u + t takes B[4u + t]; chains a0 / a1 alternate, so consecutive MFMAs are independent.
+// Each quad's two LDS reads are issued one quad ahead of its MFMAs.  side(u) runs before quad
+// u + 1's reads in program order: the previous chunk's activations, one element per quad, each
+// pinned by an empty volatile asm (which LDS reads cannot cross), so they spread over the chunk
+// instead of running as one block at its start while the MFMA pipe idles.
+template <int NQ, int P0, int BO, int NBV, class Side>
+__device__ __forceinline__ void seg2(const float4* A, const float (&B)[NBV], f4v& a0, f4v& a1,
+                                     Side&& side) {
+  float4 w0 = A[P0 * 64], w1 = A[(P0 + 1) * 64];
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    side(u);  // side work of quad u (program order pins it between the LDS reads)
+    float4 n0 = w0, n1 = w1;
+    if (u + 1 < NQ) { n0 = A[(P0 + 2 * u + 2) * 64]; n1 = A[(P0 + 2 * u + 3) * 64]; }
+    a0 = mfma4(w0.x, B[BO + 4 * u], a0); a1 = mfma4(w1.x, B[BO + 4 * u], a1);
+    a0 = mfma4(w0.y, B[BO + 4 * u + 1], a0); a1 = mfma4(w1.y, B[BO + 4 * u + 1], a1);
+    a0 = mfma4(w0.z, B[BO + 4 * u + 2], a0); a1 = mfma4(w1.z, B[BO + 4 * u + 2], a1);
+    a0 = mfma4(w0.w, B[BO + 4 * u + 3], a0); a1 = mfma4(w1.w, B[BO + 4 * u + 3], a1);
+    w0 = n0; w1 = n1;
+  }
+}
+template <int NQ, int P0, int BO, int NBV>
+__device__ __forceinline__ void seg2(const float4* A, const float (&B)[NBV], f4v& a0, f4v& a1) {
+  seg2<NQ, P0, BO>(A, B, a0, a1, [](int) {});
+}
 
 // One SkipConnMLP evaluation (output row 0) for the wave's 16 rays, every lane of a ray gets
 // the value.  Every wave of the block must call it the same number of times.
@@ -1333,6 +1378,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   using En = Engine<KH, KE, WV>;
   constexpr int QH = En::QH, QE = En::QE;
   constexpr int NC = KH / 8;  // 32-row chunks per layer
+  static_assert(QH >= 8, "hidden chunks must have a quad per pending activation");
   const int g = E.lane >> 4;
   const int F = m.freqs, L = m.n_hidden, SK = m.skip;
   // encoding: k-step e of lane group g is slot 4 e + g: sin / cos of projection (4e + g) / 2
@@ -1366,12 +1412,18 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   };
   float src[KH], dst[KH];
   f4v pend0, pend1;
-  auto retire = [&](int ib) {  // activation of chunk ib's accumulators into dst
+  // activation of chunk ib's accumulators into dst.  The empty asm pins each result inside the
+  // chunk that computes it: dst is read only by the next layer, so the compiler would otherwise
+  // sink every chunk's activations to the end of the layer, out of the MFMA gaps.
+  auto retire1 = [&](int ib, int k) {  // element k (< 8) of chunk ib
+    const int r = k & 3;
+    float& d = dst[8 * ib + k];
+    d = act<ACT>(k < 4 ? pend0[r] : pend1[r]);
+    asm volatile("" : "+v"(d));
+  };
+  auto retire = [&](int ib) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dst[8 * ib + r] = act<ACT>(pend0[r]);
-      dst[8 * ib + 4 + r] = act<ACT>(pend1[r]);
-    }
+    for (int k = 0; k < 8; ++k) retire1(ib, k);
   };
   // init layer (neural_blocks.py:80): raw encoding in
 #pragma unroll
@@ -1379,14 +1431,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
     const float4* A = E.begin(2 * QE, ib + 1 < NC ? 2 * QE : chunk_q(0), false);
     f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
     if (ib > 0) retire(ib - 1);
-#pragma unroll
-    for (int u = 0; u < QE; ++u) {
-      const float4 w0 = A[(2 * u) * 64], w1 = A[(2 * u + 1) * 64];
-      a0 = mfma4(w0.x, eraw[4 * u], a0); a1 = mfma4(w1.x, eraw[4 * u], a1);
-      a0 = mfma4(w0.y, eraw[4 * u + 1], a0); a1 = mfma4(w1.y, eraw[4 * u + 1], a1);
-      a0 = mfma4(w0.z, eraw[4 * u + 2], a0); a1 = mfma4(w1.z, eraw[4 * u + 2], a1);
-      a0 = mfma4(w0.w, eraw[4 * u + 3], a0); a1 = mfma4(w1.w, eraw[4 * u + 3], a1);
-    }
+    seg2<QE, 0, 0>(A, eraw, a0, a1);
     pend0 = a0; pend1 = a1;
     E.end();
   }
@@ -1401,25 +1446,11 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
     for (int ib = 0; ib < NC; ++ib) {
       const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
       f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
-      if (ib > 0) retire(ib - 1);
-#pragma unroll
-      for (int u = 0; u < QH; ++u) {
-        const float4 w0 = A[(2 * u) * 64], w1 = A[(2 * u + 1) * 64];
-        a0 = mfma4(w0.x, src[4 * u], a0); a1 = mfma4(w1.x, src[4 * u], a1);
-        a0 = mfma4(w0.y, src[4 * u + 1], a0); a1 = mfma4(w1.y, src[4 * u + 1], a1);
-        a0 = mfma4(w0.z, src[4 * u + 2], a0); a1 = mfma4(w1.z, src[4 * u + 2], a1);
-        a0 = mfma4(w0.w, src[4 * u + 3], a0); a1 = mfma4(w1.w, src[4 * u + 3], a1);
-      }
-      if (skip) {
-#pragma unroll
-        for (int u = 0; u < QE; ++u) {
-          const float4 w0 = A[(2 * (QH + u)) * 64], w1 = A[(2 * (QH + u) + 1) * 64];
-          a0 = mfma4(w0.x, eact[4 * u], a0); a1 = mfma4(w1.x, eact[4 * u], a1);
-          a0 = mfma4(w0.y, eact[4 * u + 1], a0); a1 = mfma4(w1.y, eact[4 * u + 1], a1);
-          a0 = mfma4(w0.z, eact[4 * u + 2], a0); a1 = mfma4(w1.z, eact[4 * u + 2], a1);
-          a0 = mfma4(w0.w, eact[4 * u + 3], a0); a1 = mfma4(w1.w, eact[4 * u + 3], a1);
-        }
-      }
+      // the previous chunk's activations: one per quad over the first 8 quads (QH >= 8)
+      seg2<QH, 0, 0>(A, src, a0, a1, [&](int u) {
+        if (ib > 0 && u < 8) retire1(ib - 1, u);
+      });
+      if (skip) seg2<QE, 2 * QH, 0>(A, eact, a0, a1);
       pend0 = a0; pend1 = a1;
       E.end();
     }
@@ -1429,13 +1460,18 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   // odd quads) so consecutive MFMAs are independent; row 0 of ray j sits in register 0 of lane j
   const float4* A = E.begin(QH, 2 * QE, true);
   f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+  {
+    float4 w0 = A[0], w1 = A[64];
 #pragma unroll
-  for (int u = 0; u < QH; u += 2) {
-    const float4 w0 = A[u * 64], w1 = A[(u + 1) * 64];
-    o0 = mfma4(w0.x, dst[4 * u], o0); o1 = mfma4(w1.x, dst[4 * u + 4], o1);
-    o0 = mfma4(w0.y, dst[4 * u + 1], o0); o1 = mfma4(w1.y, dst[4 * u + 5], o1);
-    o0 = mfma4(w0.z, dst[4 * u + 2], o0); o1 = mfma4(w1.z, dst[4 * u + 6], o1);
-    o0 = mfma4(w0.w, dst[4 * u + 3], o0); o1 = mfma4(w1.w, dst[4 * u + 7], o1);
+    for (int u = 0; u < QH; u += 2) {
+      float4 n0 = w0, n1 = w1;
+      if (u + 2 < QH) { n0 = A[(u + 2) * 64]; n1 = A[(u + 3) * 64]; }
+      o0 = mfma4(w0.x, dst[4 * u], o0); o1 = mfma4(w1.x, dst[4 * u + 4], o1);
+      o0 = mfma4(w0.y, dst[4 * u + 1], o0); o1 = mfma4(w1.y, dst[4 * u + 5], o1);
+      o0 = mfma4(w0.z, dst[4 * u + 2], o0); o1 = mfma4(w1.z, dst[4 * u + 6], o1);
+      o0 = mfma4(w0.w, dst[4 * u + 3], o0); o1 = mfma4(w1.w, dst[4 * u + 7], o1);
+      w0 = n0; w1 = n1;
+    }
   }
   E.end();
   const float o = o0[0] + o1[0];

@@ -110,6 +110,9 @@ struct ProfScope {
 void set_error(const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
 int max_hidden(const nrt_mlp* m);
+// device counter of executed ray-evaluations of the ring marches while profiling is enabled
+// (nullptr otherwise); read and cleared by nrt_profile_evals / nrt_profile_reset
+unsigned long long* profile_eval_counter();
 
 // Element order of the FP32 ring stream (MlpDev::stream32, consumed by nrt_device.h ring32 with
 // v_mfma_f32_16x16x4_f32 on 16-ray tiles).  Shared by the packer (values, nrt_pack.hip) and the

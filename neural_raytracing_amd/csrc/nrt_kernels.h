@@ -253,6 +253,7 @@ struct MarchArgs {
   int primary;
   double step;  // scan step = scan_max_t / 128 (python float)
   int32_t* scan_idx;  // optional [P] coarse-scan argmin output
+  unsigned long long* evals = nullptr;  // profiling: ray-evaluations executed (nrt_profile_evals)
 };
 
 template <bool F16, int NB>
@@ -505,6 +506,10 @@ __device__ __forceinline__ void march_body(
       }
     }
     const float d = Pol::sdf(E, s, m, px, py, pz);
+    if (a.evals) {  // profiling only: the SDF evaluations this wave-evaluation did for live jobs
+      const uint32_t busy = (uint32_t)__ballot(kind >= 0) & kRayMask;
+      if (lane == 0) atomicAdd(a.evals, (unsigned long long)__popc(busy));
+    }
     if (kind == 0) {
       if (d <= a.eps) { hit = true; ended = true; }
       else t = t + d;
