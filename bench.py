@@ -217,12 +217,18 @@ def main():
 
     import neural_raytracing_amd as nra
     from neural_raytracing_amd import _lib
-    from neural_raytracing_amd.pathtracer.render import RowRenderer, gather_rows, row_shard
+    from neural_raytracing_amd.pathtracer.render import RowRenderer, row_shard
     _lib.load(require_device=True)
     nra.set_precision(args.precision)
 
     size = args.size
     scene = build_scene(device, args.samples)
+    if world > 1:
+        # every rank built the scene from the same seed; broadcasting rank 0's tensors makes the
+        # replication explicit (a model loaded from file on rank 0 is replicated the same way)
+        from neural_raytracing_amd.pathtracer.render import broadcast_module
+        for key in ("shape", "bsdf", "lights"):
+            broadcast_module(scene[key])
     pt = scene["pt"]
     focal = float(0.5 * size / math.tan(0.5 * 0.6911))
     c2w = torch.stack([view_c2w(i, world) for i in range(world)]).to(device)
@@ -230,16 +236,7 @@ def main():
     rows = row_shard(size, rank, world, args.tile_rows)
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
                      size, rows, background=0.0, with_noise=1e-3, device=device)
-    full = torch.zeros(world, size, size, 4, device=device)
-    rows_idx = torch.tensor(rows, dtype=torch.long, device=device)
-
-    def step():
-        img = rr.render()
-        if world > 1:
-            gather_rows(img, size, rank, world, args.tile_rows, out=full)
-        else:
-            full.index_copy_(1, rows_idx, img)
-        return full
+    step = make_step(rr.render, rows, size, rank, world, args.tile_rows, device)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -262,10 +259,7 @@ def main():
         k_ms, k_n = _lib.profile_read(march_kernel)
         i_ms, i_n = _lib.profile_read("k_intersect")
         evals = _lib.profile_evals()
-        if world > 1:
-            t = torch.tensor([elapsed], device=device)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            elapsed = t.item()
+        elapsed = max_over_ranks(elapsed, world, device)
 
     ms_step = 1000 * elapsed / args.steps
     rays_per_rank = len(rows) * size * world  # this rank's rows of every view
@@ -357,6 +351,35 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def make_step(render, rows, size, rank, world, tile_rows, device, channels=4):
+    """One bench step's frame assembly: `render()` gives this rank's rows of every view
+    ([world, len(rows), size, channels]); the step returns the full [world, size, size, channels]
+    frames on every rank -- a RowGather all-gather (RCCL) for world > 1, an index copy on one GPU.
+    The buffers and index tensors are built here, once."""
+    from neural_raytracing_amd.pathtracer.render import RowGather
+    full = torch.zeros(world, size, size, channels, device=device)
+    rows_idx = torch.tensor(rows, dtype=torch.long, device=device)
+    gather = RowGather(size, rank, world, tile_rows, (world, size, channels), device) if world > 1 else None
+
+    def step():
+        img = render()
+        if gather is not None:
+            gather(img, full)
+        else:
+            full.index_copy_(1, rows_idx, img)
+        return full
+    return step
+
+
+def max_over_ranks(elapsed, world, device):
+    """The bench's time: the slowest rank's (all-reduce MAX), on every rank."""
+    if world <= 1:
+        return elapsed
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return t.item()
 
 
 def _time_frames(render, steps, warmup, kernels):

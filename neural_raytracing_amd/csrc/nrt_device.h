@@ -33,6 +33,13 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxLin = 20;  // init + up to 18 hidden + out
 
+// Row blocks (of 32 output rows) per hidden-layer chunk of the FP16 ring stream (MlpDev::stream16):
+// two independent MFMA chains per chunk, half the block barriers of one-row-block chunks.
+#ifndef NRT_RING_RB
+#define NRT_RING_RB 2
+#endif
+constexpr int kRingRB = NRT_RING_RB;
+
 enum { ACT_LEAKY = 0, ACT_SOFTPLUS = 1, ACT_NONE = 2, ACT_SIGMOID = 3, ACT_RELU = 4 };
 
 // Device descriptor of a packed SkipConnMLP (built by nrt_mlp_create, lives in device memory).
@@ -586,24 +593,29 @@ __device__ __forceinline__ float sp2(float x) {
 // is unrolled, and each wave loads and stores only the fragments a chunk has.
 template <int NB, int NE, int L, int SK>
 struct Sched {
-  static constexpr int NCH = 2 + L * NB;
+  static constexpr int RB = NB % kRingRB == 0 ? kRingRB : 1;  // row blocks per hidden chunk
+  static constexpr int G = NB / RB;                             // hidden chunks per layer
+  static constexpr int NCH = 2 + L * G;
   static constexpr bool skip(int i) { return i != L - 1 && i % SK == 0; }
   static constexpr int size(int c) {
-    return c == 0 ? NB * NE : (c == NCH - 1 ? 2 * NB : 2 * NB + (skip((c - 1) / NB) ? NE : 0));
+    return c == 0 ? NB * NE : (c == NCH - 1 ? 2 * NB : RB * (2 * NB + (skip((c - 1) / G) ? NE : 0)));
   }
   // skip layers among hidden layers 0..i-1 (i <= L - 1, so layer L - 1 is never counted)
   static constexpr int skips_before(int i) { return (i + SK - 1) / SK; }
   // closed form (no loops: it must fold to a constant inside the unrolled evaluation)
   static constexpr int offset(int c) {
     if (c == 0) return 0;
-    const int i = (c - 1) / NB, ib = (c - 1) % NB;
-    return NB * NE + (c - 1) * 2 * NB + NE * NB * skips_before(i) + (skip(i) ? ib * NE : 0);
+    const int i = (c - 1) / G, j = (c - 1) % G;
+    return NB * NE + i * 2 * NB * NB + NE * NB * skips_before(i) +
+           (i < L ? j * RB * (2 * NB + (skip(i) ? NE : 0)) : 0);
   }
-  static constexpr int max_size() { return NB * NE > 2 * NB + NE ? NB * NE : 2 * NB + NE; }
+  static constexpr int max_size() {
+    return NB * NE > RB * (2 * NB + NE) ? NB * NE : RB * (2 * NB + NE);
+  }
 };
 
 #ifndef NRT_RING_DEPTH
-#define NRT_RING_DEPTH 4  // ring slots = chunks in flight + 1 (the one being read)
+#define NRT_RING_DEPTH (kRingRB > 1 ? 3 : 4)  // ring slots = chunks in flight + 1 (the one read)
 #endif
 
 template <int NB, int NE, int WV>
@@ -641,8 +653,17 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Written as asm so hipcc neither drains it with vmcnt(0) before every ring read (it cannot
 // tell the DMA target from the slot being read) nor counts it: the engine waits for it itself.
 // M0 is compiler-reserved, so it is saved and restored inside the statement.
+#ifndef NRT_M0
+#define NRT_M0 0  // 1: pass the LDS address through an "{m0}" operand (no save / restore)
+#endif
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t srd, int voff, int soff,
                                           uint32_t lds_addr) {
+  if (NRT_M0) {
+    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                 :
+                 : "v"(voff), "s"(srd), "{m0}"(lds_addr), "s"(soff));
+    return;
+  }
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -795,12 +816,50 @@ __device__ __forceinline__ void chain_schedule() {
   __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
 }
 
+#ifndef NRT_SP2
+#define NRT_SP2 0  // softplus of the folded FP16 ring: 0 exp+log, 1 f32 polynomial, 2 packed f16
+#endif
+// log2(1 + y) on [0, 1] = y Q(y), Q a degree-4 least-squares fit on Chebyshev nodes (max abs error
+// 5.9e-5 in f32, below the f16 the activation is rounded to)
+__device__ __forceinline__ float sp2_poly(float x) {
+  const float y = __builtin_amdgcn_exp2f(-fabsf(x));
+  float q = fmaf(0.05994559f, y, -0.22771265f);
+  q = fmaf(q, y, 0.44227418f);
+  q = fmaf(q, y, -0.7170639f);
+  q = fmaf(q, y, 1.4426156f);
+  return fmaf(q, y, __int_as_float(max(__float_as_int(x), 0)));
+}
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2v sp2_pk(float a, float b) {
+  const h2v x = {(_Float16)a, (_Float16)b};
+  const h2v na = -__builtin_elementwise_abs(x);
+  const h2v y = __builtin_elementwise_exp2(na);
+  h2v q = __builtin_elementwise_fma(h2v{(_Float16)0.05994559f, (_Float16)0.05994559f}, y,
+                                    h2v{(_Float16)-0.22771265f, (_Float16)-0.22771265f});
+  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)0.44227418f, (_Float16)0.44227418f});
+  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)-0.7170639f, (_Float16)-0.7170639f});
+  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)1.4426156f, (_Float16)1.4426156f});
+  return __builtin_elementwise_fma(q, y, __builtin_elementwise_max(x, h2v{(_Float16)0.f, (_Float16)0.f}));
+}
+
 template <bool FOLD>
 __device__ __forceinline__ void act_pack1(const f16v& acc, h8& lo, h8& hi, int act) {
+  if (FOLD && NRT_SP2 == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const h2v l = sp2_pk(acc[j], acc[j + 1]), h = sp2_pk(acc[8 + j], acc[9 + j]);
+      lo[j] = l[0]; lo[j + 1] = l[1];
+      hi[j] = h[0]; hi[j + 1] = h[1];
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float a = acc[j], b = acc[8 + j];
-    if (FOLD) { a = sp2(a); b = sp2(b); }
+    if (FOLD) {
+      if (NRT_SP2 == 1) { a = sp2_poly(a); b = sp2_poly(b); }
+      else { a = sp2(a); b = sp2(b); }
+    }
     else { a = act_fwd<true>(a, act); b = act_fwd<true>(b, act); }
     lo[j] = (_Float16)a;
     hi[j] = (_Float16)b;
@@ -912,24 +971,35 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
     return b;
   };
   h8 hv[2][2 * NB];
-  // Software pipeline: the region of chunk k (between two barriers) holds chunk k's MFMA chain
-  // and the activation of chunk k-1's accumulator (`pend`), so the scheduler can put that VALU
-  // work into the MFMA gaps.  A pending tile that the current chain consumes (last row block of
-  // the previous layer, k-steps 2NB-2 / 2NB-1) is ordered by the register dependency.
-  f16v pend;
-  // init layer: one chunk of NB row blocks x NE k-steps over the raw encoding
+  // Software pipeline: the region of chunk k (between two barriers) holds chunk k's MFMA chains
+  // (RB row blocks, one independent chain each) and the activation of chunk k-1's accumulators
+  // (`pend`), so the scheduler can put that VALU work into the MFMA gaps.  A pending tile that
+  // the current chains consume (last row blocks of the previous layer) is ordered by the
+  // register dependency.
+  using S = typename Engine<NB, NE, WV>::S;
+  constexpr int RB = S::RB, G = S::G;
+  f16v pend[RB];
+  // init layer: one chunk of NB row blocks x NE k-steps over the raw encoding, RB at a time
   {
     const h8* A = E.template begin<0>();
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) {
-      f16v acc = bias(0, ib);
+    for (int ib0 = 0; ib0 < NB; ib0 += RB) {
+      f16v acc[RB];
 #pragma unroll
-      for (int s = 0; s < NE; ++s) {
-        acc = mfma16(A[(ib * NE + s) * 64], eraw[s], acc);
-        E.template dma_at<0>(ib * NE + s, NB * NE);
-      }
-      if (ib > 0) act_pack<FOLD, TAN>(pend, hv[0][2 * ib - 2], hv[0][2 * ib - 1], m.act, value);
-      pend = acc;
+      for (int b = 0; b < RB; ++b) acc[b] = bias(0, ib0 + b);
+#pragma unroll
+      for (int s = 0; s < NE; ++s)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+          acc[b] = mfma16(A[((ib0 + b) * NE + s) * 64], eraw[s], acc[b]);
+          E.template dma_at<0>((ib0 + b) * NE + s, NB * NE);
+        }
+      if (ib0 > 0)
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+          act_pack<FOLD, TAN>(pend[b], hv[0][2 * (ib0 - RB + b)], hv[0][2 * (ib0 - RB + b) + 1], m.act, value);
+#pragma unroll
+      for (int b = 0; b < RB; ++b) pend[b] = acc[b];
     }
     E.end();
   }
@@ -937,37 +1007,63 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
     constexpr int i = I;
     constexpr int src = i & 1, dst = src ^ 1;
     constexpr bool skip = (i != L - 1) && (i % SK) == 0;
-    static_for<NB>([&](auto IB) {
-      constexpr int ib = IB;
-      const h8* A = E.template begin<1 + i * NB + ib>();
-      f16v acc = bias(1 + i, ib);
-      if constexpr (ib == 0) act_pack<FOLD, TAN>(pend, hv[src][2 * NB - 2], hv[src][2 * NB - 1], m.act, value);
-      constexpr int nm = 2 * NB + (skip ? NE : 0);
+    static_for<G>([&](auto J) {
+      constexpr int j = J;
+      const h8* A = E.template begin<1 + i * G + j>();
+      f16v acc[RB];
 #pragma unroll
-      for (int s = 0; s < 2 * NB; ++s) {
-        acc = mfma16((NRT_EXP & 16) ? hv[src][(s + 1) % (2 * NB)] : A[s * 64], hv[src][s], acc);
-        E.template dma_at<1 + i * NB + ib>(s, nm);
-      }
+      for (int b = 0; b < RB; ++b) acc[b] = bias(1 + i, RB * j + b);
+      if constexpr (j == 0)
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+          act_pack<FOLD, TAN>(pend[b], hv[src][2 * (NB - RB + b)], hv[src][2 * (NB - RB + b) + 1], m.act, value);
+      constexpr int nm = RB * (2 * NB + (skip ? NE : 0));
+#pragma unroll
+      for (int s = 0; s < 2 * NB; ++s)
+#pragma unroll
+        for (int b = 0; b < RB; ++b) {
+          acc[b] = mfma16((NRT_EXP & 16) ? hv[src][(s + 1) % (2 * NB)] : A[(s * RB + b) * 64], hv[src][s], acc[b]);
+          E.template dma_at<1 + i * G + j>(s * RB + b, nm);
+        }
       if (skip) {
 #pragma unroll
-        for (int s = 0; s < NE; ++s) {
-          acc = mfma16(A[(2 * NB + s) * 64], eact[s], acc);
-          E.template dma_at<1 + i * NB + ib>(2 * NB + s, nm);
-        }
+        for (int s = 0; s < NE; ++s)
+#pragma unroll
+          for (int b = 0; b < RB; ++b) {
+            acc[b] = mfma16(A[((2 * NB + s) * RB + b) * 64], eact[s], acc[b]);
+            E.template dma_at<1 + i * G + j>((2 * NB + s) * RB + b, nm);
+          }
       }
-      if constexpr (ib > 0) act_pack<FOLD, TAN>(pend, hv[dst][2 * ib - 2], hv[dst][2 * ib - 1], m.act, value);
-      pend = acc;
+      if constexpr (j > 0)
+#pragma unroll
+        for (int b = 0; b < RB; ++b)
+          act_pack<FOLD, TAN>(pend[b], hv[dst][2 * (RB * (j - 1) + b)], hv[dst][2 * (RB * (j - 1) + b) + 1], m.act, value);
+#pragma unroll
+      for (int b = 0; b < RB; ++b) pend[b] = acc[b];
+      // keep each A read about two MFMAs ahead of its MFMA (left alone, hipcc hoists a chunk's
+      // reads and runs out of registers)
+      if (RB > 1) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * RB + 2, 0);
+#pragma unroll
+        for (int k = 0; k < nm - 2; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
       E.end();
     });
   });
   // out layer (one 32-row block; output row 0 sits in register 0 of the h == 0 lanes)
-  const h8* A = E.template begin<1 + L * NB>();
+  const h8* A = E.template begin<1 + L * G>();
   f16v acc = bias(L + 1, 0);
-  act_pack<FOLD, TAN>(pend, hv[L & 1][2 * NB - 2], hv[L & 1][2 * NB - 1], m.act, value);
+#pragma unroll
+  for (int b = 0; b < RB; ++b)
+    act_pack<FOLD, TAN>(pend[b], hv[L & 1][2 * (NB - RB + b)], hv[L & 1][2 * (NB - RB + b) + 1], m.act, value);
 #pragma unroll
   for (int s = 0; s < 2 * NB; ++s) {
     acc = mfma16(A[s * 64], hv[L & 1][s], acc);
-    E.template dma_at<1 + L * NB>(s, 2 * NB);
+    E.template dma_at<1 + L * G>(s, 2 * NB);
   }
   E.end();
   return __shfl(acc[0], E.lane & 31);

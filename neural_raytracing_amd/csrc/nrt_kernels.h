@@ -367,6 +367,9 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
 // smallest value and, among equal values, the first sample -- the reference's strict-< update.
 // A second launch (mode 1) evaluates sdf(best) for the throughput.  Lanes l and l + 32 carry the
 // same ray (the MFMA K halves) and run identical state machines.
+#ifndef NRT_KEY_SCOPE
+#define NRT_KEY_SCOPE 0
+#endif
 constexpr int kScanSegs = 8;  // sample j in [0, 128]: segment 0 = [0, 16], segment q = [16q+1, 16q+16]
 
 __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
@@ -449,7 +452,15 @@ __device__ __forceinline__ void march_body(
         }
       } else if (kind == 1) {
         if (j > jend) {
-          if (lane < RPW) atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
+          // all segments of a ray are in this wave's list: the merge never crosses a workgroup
+          // (NRT_KEY_SCOPE 1 keeps it in the XCD's L2 instead of the memory-side atomic unit)
+          if (lane < RPW) {
+            if (NRT_KEY_SCOPE == 1)
+              __hip_atomic_fetch_min(keys + ray, (unsigned long long)scan_key(best, idx),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+              atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
+          }
           kind = -1;
         }
       } else if (kind == 2) {
@@ -538,11 +549,11 @@ __device__ __forceinline__ void march_body(
       unsigned long long* __restrict__ keys
 #define NRT_MARCH_PASS t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys
 template <int NB, int NE, int WV, bool FOLD>
-__global__ void __launch_bounds__(64 * WV, 2) k_march16(NRT_MARCH_ARGS) {
+__global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_march16(NRT_MARCH_ARGS) {
   march_body<RingPol16<NB, NE, WV, FOLD>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 template <int NB, int NE, int WV, bool FOLD>
-__global__ void __launch_bounds__(64 * WV, 2) k_scan_best16(NRT_MARCH_ARGS) {
+__global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_scan_best16(NRT_MARCH_ARGS) {
   march_body<RingPol16<NB, NE, WV, FOLD>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 // FP32 (reference precision): one block of WV waves per CU (the ring takes most of the LDS), two
@@ -589,7 +600,7 @@ __global__ void k_hit_list(const uint8_t* __restrict__ hit, int64_t P, int32_t* 
 // normalize(g, 1e-6), p += 5 eps n (sdfs.py:156-157, autograd normal sdfs.py:184-197).
 // Blocks stride over the (device-counted) hit list together; the loop bound is block-uniform.
 template <int NB, int NE, int WV, bool FOLD>
-__global__ void __launch_bounds__(64 * WV, 2) k_normal16(
+__global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_normal16(
     const SdfDev s, const MlpDev m, const int32_t* __restrict__ index,
     const int32_t* __restrict__ count, int64_t M, float* __restrict__ grad,
     float* __restrict__ n_out, float* __restrict__ p_io, float offset_eps) {

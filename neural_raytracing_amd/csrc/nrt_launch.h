@@ -94,7 +94,10 @@ inline size_t ring_bias_bytes(const nrt_sdf* s) {
 }
 
 // kWV waves per block share one LDS weight ring
-constexpr int kRingWaves = 8;
+#ifndef NRT_RING_WAVES
+#define NRT_RING_WAVES 8
+#endif
+constexpr int kRingWaves = NRT_RING_WAVES;
 
 // call F.template operator()<NB, NE, FOLD>() for the SDF's ring configuration
 template <class F>

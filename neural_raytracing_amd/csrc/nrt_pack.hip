@@ -190,18 +190,30 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
     const int nrb = (ly.R + 31) / 32;
     const int ks_h = ly.hidden_in ? 2 * NB : 0;
     const int ks_e = ly.enc_in ? ke / 16 : 0;
-    for (int ib = 0; ib < nrb; ++ib) {
-      chunk_off.push_back((int)(stream.size() / (64 * 8)));
-      for (int s2 = 0; s2 < ks_h + ks_e; ++s2)
-        for (int lane = 0; lane < 64; ++lane) {
-          int i = lane & 31, hf = lane >> 5;
-          for (int j = 0; j < 8; ++j) {
-            int col;
-            if (s2 < ks_h) col = col_of_hidden(32 * (s2 >> 1) + 16 * (s2 & 1) + 8 * (j >> 2) + 4 * hf + (j & 3));
-            else col = col_of_slot(ly, 16 * (s2 - ks_h) + 8 * hf + j);
-            stream.push_back((_Float16)(wscale * wval(ly, 32 * ib + i, col)));
-          }
+    auto frag = [&](int s2, int ib) {
+      for (int lane = 0; lane < 64; ++lane) {
+        int i = lane & 31, hf = lane >> 5;
+        for (int j = 0; j < 8; ++j) {
+          int col;
+          if (s2 < ks_h) col = col_of_hidden(32 * (s2 >> 1) + 16 * (s2 & 1) + 8 * (j >> 2) + 4 * hf + (j & 3));
+          else col = col_of_slot(ly, 16 * (s2 - ks_h) + 8 * hf + j);
+          stream.push_back((_Float16)(wscale * wval(ly, 32 * ib + i, col)));
         }
+      }
+    };
+    if (is_init || is_out || NB % kRingRB != 0) {
+      // init: one chunk [row block][k-step]; out: one chunk of row block 0
+      for (int ib = 0; ib < nrb; ++ib) {
+        chunk_off.push_back((int)(stream.size() / (64 * 8)));
+        for (int s2 = 0; s2 < ks_h + ks_e; ++s2) frag(s2, ib);
+      }
+    } else {
+      // hidden layers: chunks of kRingRB row blocks, fragments [k-step][row block of the chunk]
+      for (int c = 0; c < nrb / kRingRB; ++c) {
+        chunk_off.push_back((int)(stream.size() / (64 * 8)));
+        for (int s2 = 0; s2 < ks_h + ks_e; ++s2)
+          for (int b = 0; b < kRingRB; ++b) frag(s2, kRingRB * c + b);
+      }
     }
     for (int r = 0; r < ly.R; ++r) bias16[l * bstride + r] = bscale * ly.b[r];
   }

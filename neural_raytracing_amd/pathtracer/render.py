@@ -149,24 +149,81 @@ class RowRenderer:
         return self.image
 
 
-def gather_rows(local, size, rank, world, tile_rows, out=None, group=None):
-    """All-gather every rank's row slab ([N, R_rank, W, C]) and assemble [N, size, W, C].
+class RowGather:
+    """The multi-GPU frame assembly: every rank's row slab ([N, R_rank, W, C]) ->
+    the full [N, size, W, C] frame on every rank, by one ``all_gather_into_tensor`` of
+    equal-sized (padded) slabs -- the only collective of the path (RCCL over xGMI on the box,
+    gloo in the CPU tests).  The shard table, padded staging buffers and per-rank row-index
+    tensors are built once per frame shape, not per step."""
 
-    One ``all_gather_into_tensor`` of equal-sized (padded) slabs -- the only collective of the
-    multi-GPU path (RCCL over xGMI on the box, gloo in the CPU tests).
-    """
-    import torch.distributed as dist
-    shards = [row_shard(size, r, world, tile_rows) for r in range(world)]
-    max_rows = max(len(s) for s in shards)
-    N, R, W, C = local.shape
-    slab = local.new_zeros(N, max_rows, W, C)
-    slab[:, :R] = local
-    buf = local.new_empty(world * N, max_rows, W, C)
-    dist.all_gather_into_tensor(buf, slab, group=group)
-    buf = buf.view(world, N, max_rows, W, C)
+    def __init__(self, size, rank, world, tile_rows, shape, device, dtype=torch.float32,
+                 group=None):
+        N, W, C = shape
+        self.size, self.rank, self.world, self.group = size, rank, world, group
+        self.shards = [row_shard(size, r, world, tile_rows) for r in range(world)]
+        self.max_rows = max(len(s) for s in self.shards)
+        self.slab = torch.zeros(N, self.max_rows, W, C, device=device, dtype=dtype)
+        self.buf = torch.empty(world * N, self.max_rows, W, C, device=device, dtype=dtype)
+        self.idx = [torch.tensor(rows, device=device, dtype=torch.long) for rows in self.shards]
+
+    def __call__(self, local, out):
+        import torch.distributed as dist
+        R = local.shape[1]
+        if R != len(self.shards[self.rank]):
+            raise ValueError(f"rank {self.rank} renders {R} rows, its shard has "
+                             f"{len(self.shards[self.rank])}")
+        self.slab[:, :R].copy_(local)
+        dist.all_gather_into_tensor(self.buf, self.slab, group=self.group)
+        buf = self.buf.view(self.world, *self.slab.shape)
+        for r, idx in enumerate(self.idx):
+            out.index_copy_(1, idx, buf[r, :, :idx.numel()])
+        return out
+
+
+_GATHERS = {}
+
+
+def gather_rows(local, size, rank, world, tile_rows, out=None, group=None):
+    """All-gather every rank's row slab ([N, R_rank, W, C]) and assemble [N, size, W, C]
+    (a cached RowGather per frame shape / device / group)."""
+    N, _, W, C = local.shape
+    key = (size, rank, world, tile_rows, N, W, C, local.device, local.dtype, group)
+    g = _GATHERS.get(key)
+    if g is None:
+        g = _GATHERS[key] = RowGather(size, rank, world, tile_rows, (N, W, C), local.device,
+                                      local.dtype, group)
     if out is None:
         out = local.new_empty(N, size, W, C)
-    for r, rows in enumerate(shards):
-        idx = torch.tensor(rows, device=local.device, dtype=torch.long)
-        out.index_copy_(1, idx, buf[r, :, :len(rows)])
-    return out
+    return g(local, out)
+
+
+def broadcast_module(module, src=0, group=None):
+    """Make every rank's copy of `module` (its parameters and buffers) equal to rank `src`'s,
+    in place: a model loaded from file on one rank (or initialised from different seeds) is
+    replicated before the row-sharded render, so every shard is rendered by the same weights.
+    Tensors are coalesced by dtype into one flat broadcast each (no per-parameter collective)."""
+    import torch.distributed as dist
+    tensors = [t for t in list(module.parameters()) + list(module.buffers())]
+    # basis_p and other plain tensor attributes of the package's MLPs are not buffers
+    for m in module.modules():
+        for v in vars(m).values():
+            if isinstance(v, torch.Tensor) and not isinstance(v, torch.nn.Parameter):
+                tensors.append(v)
+    seen, uniq = set(), []
+    for t in tensors:
+        if id(t) not in seen:
+            seen.add(id(t))
+            uniq.append(t)
+    by_dtype = {}
+    for t in uniq:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    with torch.no_grad():
+        for (dtype, device), ts in by_dtype.items():
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            dist.broadcast(flat, src=src, group=group)
+            off = 0
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+    return module

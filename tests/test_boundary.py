@@ -140,3 +140,87 @@ def test_gather_rows_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def _spawn(target, world, timeout=180):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=timeout) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def _bench_step_worker(rank, world, port, q):
+    """bench.make_step / max_over_ranks with a stub row renderer: every rank renders only its
+    shard's rows (a function of view, row, column), several steps, uneven shards."""
+    import torch.distributed as dist
+    import bench
+    from neural_raytracing_amd.pathtracer.render import row_shard
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    size, tile = 37, 4  # 37 rows over tiles of 4: ranks get different row counts
+    rows = row_shard(size, rank, world, tile)
+    calls = {"n": 0}
+    v = torch.arange(world).view(world, 1, 1, 1).float()
+    r = torch.tensor(rows).view(1, -1, 1, 1).float()
+    c = torch.arange(size).view(1, 1, size, 1).float()
+    ch = torch.arange(4).view(1, 1, 1, 4).float()
+
+    def render():  # [views, my rows, size, 4]
+        calls["n"] += 1
+        return 1000 * v + 10 * r + 0.01 * c + 0.001 * ch + calls["n"]
+
+    step = bench.make_step(render, rows, size, rank, world, tile, torch.device("cpu"))
+    ok = True
+    rr = torch.arange(size).view(1, -1, 1, 1).float()
+    for k in range(1, 4):
+        full = step()
+        want = 1000 * v + 10 * rr + 0.01 * c + 0.001 * ch + k
+        ok = ok and bool(torch.equal(full, want))
+    el = bench.max_over_ranks(float(rank + 1), world, torch.device("cpu"))
+    q.put((rank, (ok, el)))
+    dist.destroy_process_group()
+
+
+def test_bench_step_assembly_gloo_world2():
+    """The multi-rank bookkeeping of bench.py (frame assembly across uneven row shards, repeated
+    steps through the cached buffers, MAX of the elapsed times) run on gloo, world size 2."""
+    res = _spawn(_bench_step_worker, 2)
+    assert res == {0: (True, 2.0), 1: (True, 2.0)}
+
+
+def _broadcast_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.render import broadcast_module
+    from neural_raytracing_amd.pathtracer.shapes import SphereSDF
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    torch.manual_seed(100 + rank)  # every rank a different model
+    m = torch.nn.ModuleList([SphereSDF(n=8, device="cpu"),
+                             SkipConnMLP(num_layers=3, hidden_size=32, freqs=4, device="cpu")])
+    versions = [p._version for p in m.parameters()]
+    broadcast_module(m)
+    flat = torch.cat([t.reshape(-1) for t in list(m.parameters()) + [m[1].basis_p, m[0].shift.basis_p]])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    bumped = all(p._version > v for p, v in zip(m.parameters(), versions))
+    q.put((rank, (all(torch.equal(g, gathered[0]) for g in gathered), bumped)))
+    dist.destroy_process_group()
+
+
+def test_broadcast_module_gloo_world2():
+    """broadcast_module replicates rank 0's parameters and tensor attributes (basis_p) on every
+    rank, in place (version counters move, so packed handles are rebuilt)."""
+    res = _spawn(_broadcast_worker, 2)
+    assert res == {0: (True, True), 1: (True, True)}

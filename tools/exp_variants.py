@@ -40,5 +40,6 @@ for i, (name, _) in enumerate(variants):
     lib = os.path.join(out, f"libnrt_hip_{name}.so")
     mine = objs[i * len(VARIED):(i + 1) * len(VARIED)]
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", lib,
-                    *mine, *others], check=True)
+                    *mine, *others, "-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"],
+                   check=True)
     print(lib)
