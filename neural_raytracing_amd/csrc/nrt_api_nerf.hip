@@ -258,8 +258,16 @@ __global__ void k_plain_composite(const float* __restrict__ first_out, int astri
 // pair order); e2..e7 = the first MLP's output tiles in accumulator order (row 1 + k = latent k;
 // row 0 and rows > 64 have zero weight); e8 = (r_d, light) in half 0.
 // ------------------------------------------------------------------------------------------
-constexpr int kNerfWaves = 8;
-constexpr int kNerfMaxF = 32;  // fragments per ring slot (3 slots: 96 KiB of LDS)
+#ifndef NRT_NERF_WAVES
+#define NRT_NERF_WAVES 8
+#endif
+#ifndef NRT_NERF_MAXF
+#define NRT_NERF_MAXF 32
+#endif
+constexpr int kNerfWaves = NRT_NERF_WAVES;
+constexpr int kNerfMaxF = NRT_NERF_MAXF;  // fragments per ring slot (3 slots: 96 KiB of LDS at 32)
+constexpr int kNerfKC1 = kNerfMaxF / 4;   // k-steps per chunk of the first MLP (4 row blocks)
+constexpr int kNerfKC2 = kNerfMaxF / 2;   // ... of the second MLP (2 row blocks)
 constexpr int kNerfL1 = 5, kNerfL2 = 8, kNerfSkip = 3;  // nerf.py:162-172 (SkipConnMLP skip 3)
 
 // acc[ib] += W[ib] * [b1[0..KS1), b2[0..KS2)] over chunks of KC k-steps
@@ -270,7 +278,13 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
   static_assert(KC * NB <= Eng::MAXF, "chunk larger than a ring slot");
   constexpr int KS = KS1 + KS2;
   constexpr int NCH = (KS + KC - 1) / KC;
-  constexpr int W = 4;  // A fragments in flight (LDS latency cover)
+#ifndef NRT_NERF_W
+#define NRT_NERF_W 4
+#endif
+#ifndef NRT_NERF_SB
+#define NRT_NERF_SB 1
+#endif
+  constexpr int W = NRT_NERF_W;  // A fragments in flight (LDS latency cover)
 #pragma unroll
   for (int cc = 0; cc < NCH; ++cc) {
     const h8* A = E.begin();
@@ -286,7 +300,7 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
         const h8 b = s < KS1 ? b1[s < KS1 ? s : 0] : b2[s >= KS1 ? s - KS1 : 0];
         acc[ib] = mfma16(a[m % W], b, acc[ib]);
         if (m + W < nf) a[m % W] = A[(m + W) * 64];
-        __builtin_amdgcn_sched_barrier(0);
+        if (NRT_NERF_SB) __builtin_amdgcn_sched_barrier(0);
       }
     }
     E.end();
@@ -307,7 +321,7 @@ __device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, float x0,
   for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<-1>(basis, s, NE - 1, h, x0, x1, x2);
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
-  nerf_layer<NB, NE, 0, 8>(E, acc, enc, enc);
+  nerf_layer<NB, NE, 0, kNerfKC1>(E, acc, enc, enc);
 #pragma unroll
   for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<ACT_LEAKY>(basis, s, NE - 1, h, x0, x1, x2);
 #pragma unroll
@@ -315,13 +329,13 @@ __device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, float x0,
     ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 1 + i, ib, h);
-    nerf_layer<NB, 2 * NB, 0, 8>(E, acc, hv, hv);
-    if (i != L - 1 && (i % SKIP) == 0) nerf_layer<NB, NE, 0, 8>(E, acc, enc, enc);
+    nerf_layer<NB, 2 * NB, 0, kNerfKC1>(E, acc, hv, hv);
+    if (i != L - 1 && (i % SKIP) == 0) nerf_layer<NB, NE, 0, kNerfKC1>(E, acc, enc, enc);
   }
   ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
   for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(pm, L + 1, ob, h);
-  nerf_layer<3, 2 * NB, 0, 8>(E, o, hv, hv);
+  nerf_layer<3, 2 * NB, 0, kNerfKC1>(E, o, hv, hv);
 }
 
 __device__ __forceinline__ h8 h8_of(const float (&v)[8]) {
@@ -417,18 +431,18 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     h8 hv[2 * NB];
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
-    nerf_layer<NB, 9, 0, 16>(E, acc, e, e);
+    nerf_layer<NB, 9, 0, kNerfKC2>(E, acc, e, e);
 #pragma unroll
     for (int i = 0; i < kNerfL2; ++i) {
       ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 1 + i, ib, h);
-      if (i != kNerfL2 - 1 && (i % kNerfSkip) == 0) nerf_layer<NB, 2 * NB, 9, 16>(E, acc, hv, ea);
-      else nerf_layer<NB, 2 * NB, 0, 16>(E, acc, hv, hv);
+      if (i != kNerfL2 - 1 && (i % kNerfSkip) == 0) nerf_layer<NB, 2 * NB, 9, kNerfKC2>(E, acc, hv, ea);
+      else nerf_layer<NB, 2 * NB, 0, kNerfKC2>(E, acc, hv, hv);
     }
     ring::kact<NB, ACT_LEAKY>(acc, hv);
     f16v out[1] = {E.bias_at(m2, kNerfL2 + 1, 0, h)};
-    nerf_layer<1, 2 * NB, 0, 16>(E, out, hv, hv);
+    nerf_layer<1, 2 * NB, 0, kNerfKC2>(E, out, hv, hv);
     if (valid && h == 0) {
       alpha_raw[g] = o[0][0];
       rgb_raw[g * 3] = out[0][0]; rgb_raw[g * 3 + 1] = out[0][1]; rgb_raw[g * 3 + 2] = out[0][2];
@@ -463,13 +477,14 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
     int base = 0;
     coff.push_back(base);  // init: 3 encoding k-steps x 4 row blocks
     base += 3 * 4;
+    static_assert(kNerfKC1 >= 3 && 8 % kNerfKC1 == 0, "first-MLP chunking");
     for (int i = 0; i < a.n_hidden; ++i) {
       const bool skip = i != a.n_hidden - 1 && (i % a.skip) == 0;
-      coff.push_back(base);  // 8 hidden k-steps
+      for (int st = 0; st < 8; st += kNerfKC1) coff.push_back(base + st * 4);  // 8 hidden k-steps
       if (skip) coff.push_back(base + 8 * 4);  // + 3 encoding k-steps
       base += (8 + (skip ? 3 : 0)) * 4;
     }
-    coff.push_back(base);  // out: 8 k-steps x 3 row blocks
+    for (int st = 0; st < 8; st += kNerfKC1) coff.push_back(base + st * 3);  // out: 8 x 3 blocks
     base += 8 * 3;
     if (base != a.nk_frags) {
       set_error("build_nerf_program: unexpected first-MLP stream layout");
@@ -538,7 +553,7 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
         }
         frags.push_back(fr);
       }
-    for (int st = 0; st < ks; st += 16) coff.push_back(base + st * nrb);
+    for (int st = 0; st < ks; st += kNerfKC2) coff.push_back(base + st * nrb);
   }
   const size_t nfr = frags.size();
   frags.resize(nfr + 64);
@@ -635,14 +650,14 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     auto kern = k_nerfle16<kNerfWaves>;
     const size_t lds = ring::KEngine<kNerfWaves, kNerfMaxF>::lds_bytes(pd);
     if (int rc = set_lds(kern, lds)) return rc;
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    }
+    int dev = 0, cus = 0, per_cu = 0;
+    NRT_HIP(hipGetDevice(&dev));
+    NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kNerfWaves, lds));
+    // persistent grid: every resident block slot (independent blocks on a CU run out of phase,
+    // so one block's layer-boundary bubbles are filled by the other's MFMAs)
     const int64_t want = ceil_div64((int64_t)n, 32 * kNerfWaves);
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, cus));
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)std::max(per_cu, 1) * cus));
     ProfScope prof("k_nerfle", st);
     kern<<<dim3(blocks), dim3(64 * kNerfWaves), lds, st>>>(pd, rays, P, ts, S, light, alpha, rgb_raw);
     if (int rc = check_launch("k_nerfle16")) return rc;

@@ -160,6 +160,18 @@ def sdf_gradient(sdf, p):
 
 # ---- shading (integrators.py:139-206 with emitter_samples=1, bsdf_samples=0) -----------------
 
+def _per_camera(t, p):
+    """A [L, 3] light tensor broadcast like the reference's t[:, None, None, None, :] against
+    points p [N, ..., 3]: one row for every camera, or row n for camera n (L == N)."""
+    rows = t.reshape(-1, 3).to(p.device)
+    if rows.shape[0] == 1 or p.dim() < 2:
+        return rows[0]
+    if rows.shape[0] != p.shape[0]:
+        raise _lib.NrtError(f"PointLights with {rows.shape[0]} locations / intensities for "
+                            f"{p.shape[0]} cameras")
+    return rows.reshape(rows.shape[0], *([1] * (p.dim() - 2)), 3)
+
+
 def light_sample(lights, it, active):
     """lights.sample_direction + sample_emitter_dir_wo_isect (scene.py:321-324)
     -> (d, Le, pdf, dist); dist is None for a LightField (lights.py:181-183)."""
@@ -175,16 +187,16 @@ def light_sample(lights, it, active):
         pdf = torch.ones(p.shape[:-1], device=p.device)
         dist = None
     elif isinstance(lights, PointLights):
-        # lights.py:89-110
-        lights.single()
-        loc = lights.location.reshape(-1, 3)[0]
+        # lights.py:89-110: location[:, None, None, None, :] against p [N, W, H, B, 3] (one
+        # light, or one per camera)
+        loc = _per_camera(lights.location, p)
         d = loc - p
         dist = torch.linalg.norm(d, dim=-1, keepdim=True)
         d = F.normalize(d, eps=1e-6, dim=-1)
         fall = lights.const.clamp(min=1e-6).to(p.device) + \
             lights.linear.clamp(min=1e-6).to(p.device) * dist + \
             lights.square.clamp(min=1e-6).to(p.device) * dist.square()
-        color = lights.intensity.reshape(-1, 3)[0]
+        color = _per_camera(lights.intensity, p)
         le = lights.scale.to(p.device) * F.normalize(color, dim=-1) / fall.clamp(min=1e-6)
         pdf = torch.ones(p.shape[:-1], device=p.device)
     else:

@@ -225,17 +225,41 @@ class Direct(Integrator):
         # on EVERY ray, misses included) are evaluated on first access (HipInteraction), so a
         # render that never reads them pays nothing for them
         it._nrt_spatial = bsdf
+        per_cam = getattr(lights, "per_camera", lambda: None)()
+        if per_cam is not None:
+            # one point light per camera (lights.py:91 broadcasts location[n] over camera n's
+            # rays): camera n's rays are the contiguous block n of the [N, W, H, B] order, shaded
+            # with its own light over its own hit list
+            N = rays.shape[0]
+            if per_cam != N or P % N:
+                raise _lib.NrtError(f"PointLights with {per_cam} lights for {N} cameras")
+            Q = P // N
+            act = active.reshape(N, Q)
+            for n in range(N):
+                idx_n = torch.nonzero(act[n]).reshape(-1).to(torch.int32)
+                cnt_n = torch.tensor([idx_n.numel()], dtype=torch.int32, device=rays.device)
+                sl = slice(n * Q, (n + 1) * Q)
+                args = (_lib.ptr(it.p.reshape(P, 3)[sl]), _lib.ptr(it.n.reshape(P, 3)[sl]),
+                        _lib.ptr(it.wi.reshape(P, 3)[sl]), _lib.ptr(idx_n), _lib.ptr(cnt_n), Q,
+                        _lib.ptr(rgb[sl]), None)
+                self._shade(shapes, bsdf, lights.camera(n), shadow, occ, args, Q, rays.device)
+            return result, active, it
         args = (_lib.ptr(it.p.reshape(P, 3)), _lib.ptr(it.n.reshape(P, 3)),
                 _lib.ptr(it.wi.reshape(P, 3)), _lib.ptr(hit_idx), _lib.ptr(hit_count), P,
                 _lib.ptr(rgb), None)
+        self._shade(shapes, bsdf, lights, shadow, occ, args, P, rays.device)
+        return result, active, it
+
+    @staticmethod
+    def _shade(shapes, bsdf, lights, shadow, occ, args, P, device):
+        """nrt_shade_direct[_shadowed | _learned_occ] over one hit list."""
         if shadow:
             # sample_emitter_dir_w_isect (scene.py:290-298): shadow ray to the point light,
             # marched like SDF.intersect_test (sdfs.py:162-181); with an occlusion MLP,
             # sample_emitter_dir_w_learned_occ (scene.py:301-319)
             from ..shapes.sdfs import sdf_handle
             lib = _lib.load(require_device=True)
-            ws = torch.empty(lib.nrt_shadow_workspace_bytes(P), dtype=torch.uint8,
-                             device=rays.device)
+            ws = torch.empty(lib.nrt_shadow_workspace_bytes(P), dtype=torch.uint8, device=device)
             head = (_bsdf_handle(bsdf), _light_handle(lights), sdf_handle(shapes.sdf))
             steps = (int(shapes.max_steps), float(shapes.epsilon))
             if occ is None:
@@ -247,7 +271,6 @@ class Direct(Integrator):
         else:
             _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), *args,
                       _lib.precision_code(), _lib.stream())
-        return result, active, it
 
 
 class Path(Integrator):

@@ -55,17 +55,39 @@ class PointLights(Light):
     def spectrum_parameters(self):
         return [self.scale, self.intensity, self.const, self.linear, self.square]
 
-    def single(self):
-        """Raise unless the light is one light for every camera: the reference broadcasts
-        location [L, 3] against the hit points [N, W, H, B, 3] (lights.py:91, :106), so L > 1
-        lights are per-camera lights; the HIP shading kernels take one light per call."""
+    def per_camera(self):
+        """None when this is one light for every camera, else the number of lights L: the
+        reference broadcasts location[:, None, None, None, :] and intensity (lights.py:91, :106)
+        against the hit points [N, W, H, B, 3], so L > 1 distinct lights are one per camera
+        (colocate.py:109 moves one light onto each of the N cameras of a batch)."""
         loc = self.location.reshape(-1, 3)
         inten = self.intensity.reshape(-1, 3)
+        L = max(loc.shape[0], inten.shape[0])
         for t in (loc, inten):
             if t.shape[0] > 1 and not bool((t == t[:1]).all()):
-                raise _lib.NrtError("PointLights with one location / intensity per camera render "
-                                    "one camera per pathtrace call on the HIP path "
-                                    "(main.pathtrace splits the cameras)")
+                return L
+        return None
+
+    def camera(self, n):
+        """The light camera n sees (a PointLights of location[n], intensity[n]; rows broadcast
+        when there is one), sharing the falloff tensors."""
+        v = PointLights.__new__(PointLights)
+        nn.Module.__init__(v)
+        loc = self.location.reshape(-1, 3)
+        inten = self.intensity.reshape(-1, 3)
+        v.device = self.device
+        v.location = loc[n if loc.shape[0] > 1 else 0].reshape(1, 3)
+        v.intensity = inten[n if inten.shape[0] > 1 else 0].reshape(1, 3)
+        v.scale, v.const, v.linear, v.square = self.scale, self.const, self.linear, self.square
+        return v
+
+    def single(self):
+        """Raise unless the light is one light for every camera (the HIP shading kernels take
+        one light per call; per-camera lights are split per camera by the callers that support
+        them, Direct and its training path)."""
+        if self.per_camera() is not None:
+            raise _lib.NrtError("PointLights with one location / intensity per camera are "
+                                "supported by Direct (and its training path), not here")
         return self
 
     def nrt(self):

@@ -69,6 +69,8 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     fused = _fused(integrator, cameras, w_isect, addition)
     if needs_grad(shapes, bsdf, lights):
         fused = None  # training: integrator.sample carries the gradients
+    if getattr(lights, "per_camera", lambda: None)() is not None:
+        fused = None  # one light per camera: Direct.sample shades camera by camera
     for ij in range(len(xs) * len(ys)):
         i, j = divmod(ij, len(ys))
         x0, y0 = xs[j], ys[i]

@@ -412,3 +412,68 @@ def test_mlp_backward_refuses_weights_changed_after_forward():
     y2 = m(x).square().sum()
     y2.backward()  # a fresh graph is fine
     assert m.out.weight.grad is not None
+
+
+# ------------------------------------------------------------------------------------------
+# one point light per camera (colocate.py:109: light.location = cameras.get_camera_center() * 1.05
+# for the N = 4 cameras of each training batch; lights.py:91, :106 broadcast location[n] over
+# camera n)
+# ------------------------------------------------------------------------------------------
+
+class _OracleCams:
+    """Several one-camera oracle FoV cameras as one batch (rays concatenated along N)."""
+
+    def __init__(self, cams):
+        self.cams = cams
+
+    def __len__(self):
+        return len(self.cams)
+
+    def sample_positions(self, *args, **kwargs):
+        return torch.cat([c.sample_positions(*args, **kwargs) for c in self.cams], dim=0)
+
+
+@pytest.mark.parametrize("mode", ["fused", "autograd"])
+def test_point_light_per_camera_matches_oracle(mode):
+    """Two FoV cameras, each with its own co-located point light, through pathtrace on the fused
+    Direct kernels (shaded camera by camera) and on the training path (autograd on: the light
+    location broadcast per camera in torch), vs the oracle."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.cameras import OpenGLPerspectiveCameras
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from tests.test_gpu_parity import _colocate_pair
+    ref, mine = _colocate_pair()
+    cams, Rs, Ts = [], [], []
+    for elev, azim in ((30.0, 45.0), (10.0, -60.0)):
+        Rm, Tm = R.look_at_view_transform_ref(dist=1.0, elev=elev, azim=azim)
+        cams.append(R.FoVCameraRef(Rm, Tm, znear=1.0, zfar=100.0))
+        Rs.append(Rm)
+        Ts.append(Tm)
+    locs = torch.cat([c.center() * 1.05 for c in cams])  # [2, 3]
+    ref_lights = R.PointLightRef(location=locs.reshape(-1).tolist(), scale=5.0)
+    random.seed(17)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref_lights, _OracleCams(cams), R.DirectRef(), ref["bsdf"],
+                        size=64, chunk_size=32, background=0.5, with_noise=0.0)
+    lights = PointLights(location=locs.cuda(), scale=5.0, device="cuda")
+    assert lights.per_camera() == 2
+    camera = OpenGLPerspectiveCameras(R=torch.cat(Rs), T=torch.cat(Ts), device="cuda")
+    random.seed(17)
+    ctx = torch.no_grad() if mode == "fused" else torch.enable_grad()
+    with ctx:
+        got, _ = pt.pathtrace(mine["shape"], lights, camera, Direct(), bsdf=mine["bsdf"], size=64,
+                              chunk_size=32, bundle_size=1, background=0.5, with_noise=0.0)
+    got = got.detach().cpu()
+    assert got.shape == want.shape == (2, 64, 64, 3)
+    err = (got - want).abs().amax(-1)
+    report(f"point_light_per_camera[{mode}]", pixels=err.numel(),
+           over_1e4=int((err > 1e-4).sum()), maxabs=err.max().item())
+    assert (err <= 1e-4).float().mean() >= 0.995
+    # the second camera is lit by its own light: rendering it with the first light differs
+    random.seed(17)
+    with torch.no_grad():
+        other = R.render(ref["shape"], R.PointLightRef(location=locs[0].tolist(), scale=5.0),
+                         _OracleCams(cams), R.DirectRef(), ref["bsdf"], size=64, chunk_size=32,
+                         background=0.5, with_noise=0.0)
+    assert (other[1] - want[1]).abs().max() > 1e-2

@@ -117,3 +117,34 @@ def test_conductor_eta_gets_no_gradient_like_the_reference():
     assert cond.eta.grad is None
     assert cond.specular.grad is not None and cond.specular.grad.abs().sum() > 0
     assert inspect.signature(Conductor.__init__).parameters["eta"].default == 1.3
+
+
+def test_point_light_per_camera_broadcast_matches_oracle():
+    """PointLights with one location / intensity per camera (colocate.py:109): the training
+    path's light sample broadcasts row n over camera n like lights.py:91, :106 (the oracle's
+    PointLightRef.sample_direction); one row broadcasts to every camera."""
+    from neural_raytracing_amd.pathtracer import differentiable as D
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+
+    class It:
+        pass
+    torch.manual_seed(5)
+    p = torch.randn(3, 4, 5, 1, 3)
+    active = torch.rand(3, 4, 5, 1) > 0.3
+    it = It()
+    it.p = p
+    locs = torch.randn(3, 3)
+    inten = torch.rand(3, 3) + 0.1
+    mine = PointLights(location=locs, intensity=inten, scale=5.0, device="cpu")
+    assert mine.per_camera() == 3
+    d, le, pdf, dist = D.light_sample(mine, it, active)
+    ref = R.PointLightRef(location=locs.reshape(-1).tolist(), scale=5.0)
+    ref.intensity = inten.clone()
+    rs, rle = ref.sample_direction(it, active)
+    assert torch.allclose(d, rs.d, atol=1e-6) and torch.allclose(dist, rs.dist, atol=1e-6)
+    assert torch.allclose(le, rle, atol=1e-6)
+    v = mine.camera(1)
+    assert torch.equal(v.location, locs[1:2]) and torch.equal(v.intensity, inten[1:2])
+    assert v.per_camera() is None
+    one = PointLights(location=locs[:1].expand(3, 3).clone(), scale=5.0, device="cpu")
+    assert one.per_camera() is None

@@ -2,7 +2,7 @@
 #   bash tools/exp_run.sh e1 d3 ...
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-fp32-check --no-extra-legs"
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-fp32-check --no-extra-legs $BENCH_EXTRA"
 for V in base "$@"; do
   if [ "$V" = base ]; then L=""; else L=build_var/libnrt_hip_$V.so; fi
   NRT_LIB=$L timeout -k 10 300 python bench.py $ARGS > gpurun_out/exp_$V.log 2>&1 || { echo "$V failed"; tail -3 gpurun_out/exp_$V.log; exit 1; }

@@ -19,7 +19,7 @@ from neural_raytracing_amd import build as B  # noqa: E402
 B.build(verbose=False)
 out = os.path.join(ROOT, "build_var")
 os.makedirs(out, exist_ok=True)
-VARIED = ["nrt_api_sdf.hip", "nrt_ring_march.hip", "nrt_ring_normal.hip"]
+VARIED = os.environ.get("VARIED", "nrt_api_sdf.hip,nrt_ring_march.hip,nrt_ring_normal.hip").split(",")
 others = [os.path.join(B.OBJDIR, os.path.splitext(s)[0] + ".o") for s in B.SOURCES
           if s not in VARIED]
 
