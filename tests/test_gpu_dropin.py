@@ -249,13 +249,13 @@ def test_model_files_render_like_the_oracle(tmp_path, ref_paths):
 def test_train_sample_colocated_lights_per_camera(tmp_path, monkeypatch):
     """colocate.py's training call (colocate.py:109-137): train_sample with N = 2 cameras per step,
     a point light moved onto each camera (light.location = cameras.get_camera_center() * 1.05,
-    one light per camera), NeRFIntegrator(Direct) and a learned occlusion MLP (w_isect=occ_mlp)
+    one light per camera), Direct() (colocate.py:78) and a learned occlusion MLP (w_isect=occ_mlp)
     -- every step shades each camera with its own light on the training path.  Two steps and a
     validation render run; the losses are finite and the weights move."""
     import neural_raytracing_amd.pathtracer as pt
     from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, Diffuse, NeuralBSDF
     from neural_raytracing_amd.pathtracer.cameras import look_at_view_transform
-    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.integrators import Direct
     from neural_raytracing_amd.pathtracer.lights import PointLights
     from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
     from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
@@ -285,7 +285,7 @@ def test_train_sample_colocated_lights_per_camera(tmp_path, monkeypatch):
         light.location = cam.get_camera_center().to(dev) * 1.05
         seen.append(light.per_camera())
 
-    losses = train_sample(shape, bsdf=bsdf, integrator=NeRFIntegrator(Direct()), lights=lights,
+    losses = train_sample(shape, bsdf=bsdf, integrator=Direct(), lights=lights,
                           Rs=Rs, Ts=Ts, exp_imgs=exp_imgs, exp_masks=exp_masks, opt=opt,
                           size=size, crop_size=16, N=2, iters=2, save_freq=10_000, valid_freq=1,
                           max_valid_size=16, uv_select=lambda _, cs: (8, 8),
