@@ -374,7 +374,15 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     const float x1 = __fadd_rn(r[1], __fmul_rn(t, dy));
     const float x2 = __fadd_rn(r[2], __fmul_rn(t, dz));
     f16v o[3];
-    nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
+#ifndef NRT_NERF_SKIP
+#define NRT_NERF_SKIP 0  // timing-only experiment bits (tools/exp_variants.py); 0 in every shipped build
+#endif
+    if (NRT_NERF_SKIP & 2) {
+#pragma unroll
+      for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(m1, kNerfL1 + 1, ob, h) + x0;
+    } else {
+      nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
+    }
     // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
     h8 e[9], ea[9], lo[7];
 #pragma unroll
@@ -429,6 +437,13 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     constexpr int NB = 2;
     f16v acc[NB];
     h8 hv[2 * NB];
+    if (NRT_NERF_SKIP & 1) {
+      if (valid && h == 0) {
+        alpha_raw[g] = o[0][0];
+        rgb_raw[g * 3] = (float)e[0][0]; rgb_raw[g * 3 + 1] = (float)ea[1][1]; rgb_raw[g * 3 + 2] = 0.f;
+      }
+      continue;
+    }
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
     nerf_layer<NB, 9, 0, kNerfKC2>(E, acc, e, e);

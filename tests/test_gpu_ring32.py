@@ -205,3 +205,22 @@ def test_ring32_after_device_refresh_matches_fresh_pack():
             _lib.load().nrt_sdf_destroy(sh)
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 511, 3001])
+def test_ring32_ragged_ray_counts_match_slab_kernel(n):
+    """Ray counts that are not a multiple of the 16-ray tile, fewer rays than one wave / block,
+    and more rays than waves: every ray's t / hit / p / throughput equal the FP32 slab kernel's
+    up to the summation-order tolerance, and no ray is dropped or written twice."""
+    _, mine = _blob(64, 128, 32, "softplus", seed=23)
+    g = torch.Generator().manual_seed(n)
+    o = torch.tensor([0.0, 0.2, 1.1]) + 0.05 * torch.randn(1, n, 1, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, n, 1, 1, 2, generator=g) * 0.8 - 0.4,
+                               -torch.ones(1, n, 1, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    it, hit, n32 = _march(mine, rays)
+    assert n32 >= 1
+    os.environ["NRT_NO_RING32"] = "1"
+    sit, shit, _ = _march(mine, rays)
+    assert torch.isfinite(it.t).all() and torch.isfinite(it.throughput).all()
+    _compare(f"ring32_ragged[{n}]", it, hit, sit, shit, flip_frac=max(0.005, 1.0 / n))
