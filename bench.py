@@ -258,7 +258,7 @@ def main():
         march_kernel = "k_march16" if args.precision == "fp16" else "k_march32"
         k_ms, k_n = _lib.profile_read(march_kernel)
         i_ms, i_n = _lib.profile_read("k_intersect")
-        evals = _lib.profile_evals()
+        evals = count_evals(step)
         elapsed = max_over_ranks(elapsed, world, device)
 
     ms_step = 1000 * elapsed / args.steps
@@ -274,7 +274,7 @@ def main():
     peak = PEAK_TFLOPS[args.precision]
     # executed work of the march launch: evaluations the job lists actually ran (counted on the
     # device while profiling), less the sdf(best) pass's one per ray
-    exec_flop = (evals / max(args.steps, 1) - rays_per_rank) * FLOP_SDF_8x256
+    exec_flop = (evals - rays_per_rank) * FLOP_SDF_8x256
     exec_achieved = exec_flop / (avg_kernel_ms * 1e-3) / 1e12
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
@@ -382,8 +382,22 @@ def max_over_ranks(elapsed, world, device):
     return t.item()
 
 
+def count_evals(render):
+    """SDF evaluations the ring marches execute in one more, untimed render (the device counter
+    is one atomic per wave-evaluation, so it stays out of the timed steps)."""
+    from neural_raytracing_amd import _lib
+    _lib.profile_reset()
+    _lib.profile_enable(False, evals=True)
+    render()
+    torch.cuda.synchronize()
+    evals = _lib.profile_evals()
+    _lib.profile_enable(False)
+    return evals
+
+
 def _time_frames(render, steps, warmup, kernels):
-    """Wall time of `steps` renders after `warmup`, and the HIP-event time of each kernel."""
+    """Wall time of `steps` renders after `warmup`, the HIP-event time of each kernel, and the
+    SDF evaluations of one render."""
     from neural_raytracing_amd import _lib
     for _ in range(warmup):
         render()
@@ -396,7 +410,8 @@ def _time_frames(render, steps, warmup, kernels):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     _lib.profile_enable(False)
-    return elapsed, {k: _lib.profile_read(k) for k in kernels}
+    times = {k: _lib.profile_read(k) for k in kernels}
+    return elapsed, times, count_evals(render)
 
 
 def extra_legs(scene, cameras, size, args, rows):
@@ -415,12 +430,11 @@ def extra_legs(scene, cameras, size, args, rows):
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
                      size, rows, background=0.0, with_noise=1e-3, device=cameras.cam_to_world.device)
     steps = 2
-    el, ks = _time_frames(rr.render, steps, 1, ["k_march32", "k_intersect"])
-    evals = _lib.profile_evals()
+    el, ks, evals = _time_frames(rr.render, steps, 1, ["k_march32", "k_intersect"])
     k_ms = ks["k_march32"][0] / max(ks["k_march32"][1], 1)
     flop = frame_rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256  # march + scan launch
     ach = flop / (k_ms * 1e-3) / 1e12
-    exe = (evals / steps - frame_rays) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
+    exe = (evals - frame_rays) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
     out["fp32"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                    "ms_per_step": 1000 * el / steps, "steps": steps,
                    "roofline": {"bound": "mfma", "kernel": "k_march32", "achieved": ach,
@@ -436,14 +450,13 @@ def extra_legs(scene, cameras, size, args, rows):
                      scene["bsdf"], size, rows, background=0.0, with_noise=1e-3,
                      device=cameras.cam_to_world.device)
     steps = 3
-    el, ks = _time_frames(rr.render, steps, 1, ["k_march16"])
-    evals = _lib.profile_evals()
+    el, ks, evals = _time_frames(rr.render, steps, 1, ["k_march16"])
     k_ms = ks["k_march16"][0] / max(ks["k_march16"][1], 1)
     flop = frame_rays * S * FLOP_SDF_8x256
     ach = flop / (k_ms * 1e-3) / 1e12
     # without the scan a ray stops at its hit (or at max_t): the algorithmic count (every ray at
     # every step, as the reference evaluates) is far above what the job lists execute
-    exe = (evals / steps) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
+    exe = evals * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
     out["scan_free"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                         "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": args.precision,
                         "roofline": {"bound": "mfma", "kernel": "k_march16", "achieved": ach,
@@ -451,7 +464,7 @@ def extra_legs(scene, cameras, size, args, rows):
                                      "frac": ach / PEAK_TFLOPS[args.precision],
                                      "avg_kernel_ms": k_ms, "flop_per_launch": flop,
                                      "executed_frac": exe / PEAK_TFLOPS[args.precision],
-                                     "executed_evals_per_ray": evals / steps / frame_rays}}
+                                     "executed_evals_per_ray": evals / frame_rays}}
     return out
 
 

@@ -335,11 +335,14 @@ int nrt_light_envmap(const nrt_light* light, int32_t bins, float* out, void* str
  * are bracketed by hipEvents on the stream they run on.  nrt_profile_read synchronises those
  * events and returns the summed duration and launch count of kernel `name`.
  * ------------------------------------------------------------------------------------- */
-void nrt_profile_enable(int on);
+#define NRT_PROF_TIMING 1 /* hipEvents around the profiled launches */
+#define NRT_PROF_EVALS 2  /* count the ring marches' SDF evaluations (one device atomic per
+                             wave-evaluation: enable it in an untimed pass only) */
+void nrt_profile_enable(int flags);
 void nrt_profile_reset(void);
 int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
 /* SDF evaluations (ray x point) the ring marches (k_march16 / k_scan_best16 / k_march32 /
- * k_scan_best32) executed while profiling was enabled, since the last nrt_profile_reset: the
+ * k_scan_best32) executed while NRT_PROF_EVALS was enabled, since the last nrt_profile_reset: the
  * executed work behind the algorithmic count (every ray at every march step and scan point,
  * sdfs.py:119-131, 232-249), which the lane-level job lists lower.  Synchronises. */
 int nrt_profile_evals(uint64_t* evals);

@@ -176,8 +176,10 @@ def precision_code():
     return _precision["value"]
 
 
-def profile_enable(on=True):
-    load().nrt_profile_enable(1 if on else 0)
+def profile_enable(on=True, evals=False):
+    """HIP-event timing of the profiled launches (on); evals=True also counts the ring marches'
+    SDF evaluations (a device atomic per wave-evaluation: keep it out of timed regions)."""
+    load().nrt_profile_enable((1 if on else 0) | (2 if evals else 0))
 
 
 def profile_reset():

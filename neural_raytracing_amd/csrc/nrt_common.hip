@@ -20,7 +20,8 @@ struct ProfRec {
   std::string name;
   hipEvent_t a, b;
 };
-static bool g_prof = false;
+static bool g_prof = false;        // NRT_PROF_TIMING: hipEvents around the profiled launches
+static bool g_prof_evals = false;  // NRT_PROF_EVALS: the ring marches' evaluation counter
 static std::vector<ProfRec> g_recs;
 
 ProfScope::ProfScope(const char* n, hipStream_t s) : name(n), stream(s) {
@@ -40,7 +41,7 @@ ProfScope::~ProfScope() {
 static unsigned long long* g_evals[64] = {};
 
 unsigned long long* profile_eval_counter() {
-  if (!g_prof) return nullptr;
+  if (!g_prof_evals) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!g_evals[dev]) {
@@ -56,9 +57,10 @@ using namespace nrt;
 
 extern "C" {
 
-void nrt_profile_enable(int on) {
-  nrt::g_prof = on != 0;
-  if (nrt::g_prof) (void)nrt::profile_eval_counter();  // allocate outside any timed region
+void nrt_profile_enable(int flags) {
+  nrt::g_prof = (flags & NRT_PROF_TIMING) != 0;
+  nrt::g_prof_evals = (flags & NRT_PROF_EVALS) != 0;
+  if (nrt::g_prof_evals) (void)nrt::profile_eval_counter();  // allocate outside any timed region
 }
 
 void nrt_profile_reset(void) {

@@ -356,8 +356,9 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
 // points (sdfs.py:119-131, 232-249); only the march is data-dependent (hit / t >= max_t end it
 // early), the scan is a fixed walk that does not depend on the march.  A wave therefore works
 // through a private job list instead of a fixed 32-ray tile: the grid is persistent (one block
-// per resident slot), wave w owns rays w, w + nw, w + 2 nw, ... (a strided sample of the image,
-// so every wave gets a similar mix of short hit marches and long miss marches), and its list is
+// per resident slot), wave w owns a strided sample of the image in chunks of consecutive rays
+// (OwnedRays: every wave gets a similar mix of short hit marches and long miss marches), and its
+// list is
 //     [march of each owned ray] [scan segment 0 of each ray] ... [scan segment NSEG-1 ...]
 // A lane whose job has ended takes the next list entry (ballot + prefix count on a wave-uniform
 // cursor, no atomics), so lanes never idle on a finished ray; the list ends with short
@@ -371,12 +372,40 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
 #define NRT_KEY_SCOPE 0
 #endif
 constexpr int kScanSegs = 8;  // sample j in [0, 128]: segment 0 = [0, 16], segment q = [16q+1, 16q+16]
+#ifndef NRT_SCAN_SPLIT
+#define NRT_SCAN_SPLIT 64
+#endif
+constexpr int kScanSplit = NRT_SCAN_SPLIT;  // rays per wave scanned in segments (-1: all)
 
 __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
   uint32_t b = __float_as_uint(v + 0.f);  // -0 -> +0: equal values tie, as under the reference's <
   b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
   return ((uint64_t)b << 32) | (uint32_t)idx;
 }
+
+// Rays owned by wave w of nw: whole rounds of kRayChunk consecutive rays (chunk c of round f is
+// chunk f*nw + w of the image), then the remainder dealt one ray at a time (w, w + nw, ...), so
+// every wave owns the same number of rays to within one.  A chunk's rays, their ray records,
+// outputs and scan keys are contiguous and touched by one wave only (one XCD's L2 assembles
+// whole lines); a wave's ~10 chunks are spread over the image, so its mix of short (hit) and
+// long (miss) marches stays near the frame's.  kRayChunk = 1 is the plain strided deal.
+#ifndef NRT_RAY_CHUNK
+#define NRT_RAY_CHUNK 1  // 32 measured 7 % slower (chunk-correlated march lengths unbalance the waves)
+#endif
+constexpr int64_t kRayChunk = NRT_RAY_CHUNK;
+struct OwnedRays {
+  int64_t nw, w, full, R;  // full = rays of this wave in whole chunk rounds
+  __device__ __forceinline__ OwnedRays(int64_t P, int64_t nw_, int64_t w_) : nw(nw_), w(w_) {
+    const int64_t rounds = P / (nw * kRayChunk);
+    full = rounds * kRayChunk;
+    const int64_t rem = P - rounds * nw * kRayChunk;
+    R = full + (w < rem ? (rem - 1 - w) / nw + 1 : 0);
+  }
+  __device__ __forceinline__ int64_t ray(int64_t k) const {
+    if (k < full) return ((k / kRayChunk) * nw + w) * kRayChunk + (k % kRayChunk);
+    return (full * nw) + w + (k - full) * nw;
+  }
+};
 
 // The SDF evaluator of a ring march: FP16 (32-ray tiles, ring::eval, fast sphere exp) or FP32
 // (16-ray tiles, ring32::eval, torch-exact transcendentals).  RPW rays per wave; lane l serves
@@ -419,9 +448,13 @@ __device__ __forceinline__ void march_body(
   const int lane = lane_id(), r = lane & (RPW - 1);
   const int64_t nw = (int64_t)gridDim.x * WV;
   const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t R = w < P ? (P - 1 - w) / nw + 1 : 0;  // rays owned by this wave
+  const OwnedRays own(P, nw, w);
+  const int64_t R = own.R;  // rays owned by this wave
   const bool scan = mode == 0 && a.primary;
-  const int64_t J = mode == 0 ? R * (scan ? 1 + kScanSegs : 1) : R;
+  // scan jobs: the whole 129-point scan of each of the first R - T rays (one plain key store),
+  // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail
+  const int64_t T = kScanSplit < 0 ? R : (R < kScanSplit ? R : (int64_t)kScanSplit);
+  const int64_t J = mode == 0 ? (scan ? R + (R - T) + T * kScanSegs : R) : R;
   const uint32_t lt = (1u << r) - 1u;
   typename Pol::Eng E;
   Pol::init(E, s, m, smem_c);
@@ -431,7 +464,7 @@ __device__ __forceinline__ void march_body(
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
   float t = 0.f, best = 0.f;
   int i = 0, j = 0, jend = 0, idx = 0;
-  bool ended = false, hit = false;
+  bool ended = false, hit = false, whole = false;
   int64_t cursor = 0;  // wave-uniform
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
@@ -455,7 +488,9 @@ __device__ __forceinline__ void march_body(
           // all segments of a ray are in this wave's list: the merge never crosses a workgroup
           // (NRT_KEY_SCOPE 1 keeps it in the XCD's L2 instead of the memory-side atomic unit)
           if (lane < RPW) {
-            if (NRT_KEY_SCOPE == 1)
+            if (whole)
+              keys[ray] = (unsigned long long)scan_key(best, idx);
+            else if (NRT_KEY_SCOPE == 1)
               __hip_atomic_fetch_min(keys + ray, (unsigned long long)scan_key(best, idx),
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else
@@ -476,9 +511,18 @@ __device__ __forceinline__ void march_body(
         const int64_t q = cursor + __popc(want & lt);
         if (q < J) {
           int64_t k = q;
-          int seg = -1;
-          if (mode == 0 && q >= R) { seg = (int)((q - R) / R); k = (q - R) - (int64_t)seg * R; }
-          ray = w + k * nw;
+          int seg = -1;  // -1 march, kScanSegs whole scan, else a segment
+          if (mode == 0 && q >= R) {
+            k = q - R;
+            if (k < R - T) {
+              seg = kScanSegs;
+            } else {
+              k -= R - T;
+              seg = (int)(k / T);
+              k = R - T + (k - (int64_t)seg * T);
+            }
+          }
+          ray = own.ray(k);
           const float* rp = rays + ray * 6;
           ox = rp[0]; oy = rp[1]; oz = rp[2]; dx = rp[3]; dy = rp[4]; dz = rp[5];
           ended = false;
@@ -489,8 +533,9 @@ __device__ __forceinline__ void march_body(
             kind = 0; t = 0.f; i = 0; hit = false;
           } else {
             kind = 1;
-            j = seg == 0 ? 0 : 16 * seg + 1;
-            jend = 16 * seg + 16;
+            whole = seg == kScanSegs;
+            j = (seg == 0 || whole) ? 0 : 16 * seg + 1;
+            jend = whole ? 16 * kScanSegs : 16 * seg + 16;
             idx = -1;
           }
         } else {

@@ -6,7 +6,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/pmc
 KRX=$1; shift
-ARGS="${BENCH_ARGS:---size ${SIZE:-400} --steps 1 --warmup 0 --no-cpu-baseline --no-fp32-check}"
+ARGS="${BENCH_ARGS:---size ${SIZE:-400} --steps 1 --warmup 0 --no-cpu-baseline --no-fp32-check --no-extra-legs}"
 i=0
 for SET in "$@"; do
   i=$((i+1))

@@ -22,7 +22,10 @@ def counter(run_dir, name, kernel="k_march16"):
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"{name} for {kernel} not found in {path}")
-    return sum(vals.values()) / len(vals), len(vals)
+    # the first dispatch is the timed frame (--steps 1 --warmup 0); bench.py's later untimed
+    # evaluation-counting frame adds one device atomic per wave-evaluation and is not counted
+    first = min(vals, key=int)
+    return vals[first], len(vals)
 
 
 def main():
@@ -39,7 +42,8 @@ def main():
         "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
         "note": "FETCH_SIZE x2 (gfx950 16-B/lane read correction), WRITE_SIZE as reported; "
-                "separate rocprofv3 --pmc passes of bench.py --size %d --steps 1 --warmup 0" % size,
+                "separate rocprofv3 --pmc passes of bench.py --size %d --steps 1 --warmup 0 "
+                "--no-extra-legs; the timed frame's launch (first dispatch)" % size,
     }
     path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
     json.dump(out, open(path, "w"), indent=1)
