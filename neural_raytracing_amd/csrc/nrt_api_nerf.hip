@@ -259,12 +259,16 @@ __global__ void k_plain_composite(const float* __restrict__ first_out, int astri
 // row 0 and rows > 64 have zero weight); e8 = (r_d, light) in half 0.
 // ------------------------------------------------------------------------------------------
 #ifndef NRT_NERF_WAVES
-#define NRT_NERF_WAVES 8
+#define NRT_NERF_WAVES 12  // 3 waves per SIMD (162 VGPRs with the DMA engine)
 #endif
 #ifndef NRT_NERF_MAXF
 #define NRT_NERF_MAXF 32
 #endif
+#ifndef NRT_NERF_DMA
+#define NRT_NERF_DMA 1
+#endif
 constexpr int kNerfWaves = NRT_NERF_WAVES;
+constexpr bool kNerfDma = NRT_NERF_DMA != 0;  // weight chunks by LDS-DMA (KEngine DMA mode)
 constexpr int kNerfMaxF = NRT_NERF_MAXF;  // fragments per ring slot (3 slots: 96 KiB of LDS at 32)
 constexpr int kNerfKC1 = kNerfMaxF / 4;   // k-steps per chunk of the first MLP (4 row blocks)
 constexpr int kNerfKC2 = kNerfMaxF / 2;   // ... of the second MLP (2 row blocks)
@@ -280,9 +284,6 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
   constexpr int NCH = (KS + KC - 1) / KC;
 #ifndef NRT_NERF_W
 #define NRT_NERF_W 4
-#endif
-#ifndef NRT_NERF_SB
-#define NRT_NERF_SB 1
 #endif
   constexpr int W = NRT_NERF_W;  // A fragments in flight (LDS latency cover)
 #pragma unroll
@@ -300,7 +301,7 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
         const h8 b = s < KS1 ? b1[s < KS1 ? s : 0] : b2[s >= KS1 ? s - KS1 : 0];
         acc[ib] = mfma16(a[m % W], b, acc[ib]);
         if (m + W < nf) a[m % W] = A[(m + W) * 64];
-        if (NRT_NERF_SB) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     E.end();
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
   const int64_t n = (int64_t)S * P;
   const int64_t per_block = 32 * WV;
   if ((int64_t)blockIdx.x * per_block >= n) return;
-  ring::KEngine<WV, kNerfMaxF> E;
+  ring::KEngine<WV, kNerfMaxF, kNerfDma> E;
   E.init(prog, smem_c);
   const int lane = lane_id(), h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -374,15 +375,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     const float x1 = __fadd_rn(r[1], __fmul_rn(t, dy));
     const float x2 = __fadd_rn(r[2], __fmul_rn(t, dz));
     f16v o[3];
-#ifndef NRT_NERF_SKIP
-#define NRT_NERF_SKIP 0  // timing-only experiment bits (tools/exp_variants.py); 0 in every shipped build
-#endif
-    if (NRT_NERF_SKIP & 2) {
-#pragma unroll
-      for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(m1, kNerfL1 + 1, ob, h) + x0;
-    } else {
-      nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
-    }
+    nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
     // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
     h8 e[9], ea[9], lo[7];
 #pragma unroll
@@ -437,13 +430,6 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     constexpr int NB = 2;
     f16v acc[NB];
     h8 hv[2 * NB];
-    if (NRT_NERF_SKIP & 1) {
-      if (valid && h == 0) {
-        alpha_raw[g] = o[0][0];
-        rgb_raw[g * 3] = (float)e[0][0]; rgb_raw[g * 3 + 1] = (float)ea[1][1]; rgb_raw[g * 3 + 2] = 0.f;
-      }
-      continue;
-    }
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
     nerf_layer<NB, 9, 0, kNerfKC2>(E, acc, e, e);
@@ -463,6 +449,7 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
       rgb_raw[g * 3] = out[0][0]; rgb_raw[g * 3 + 1] = out[0][1]; rgb_raw[g * 3 + 2] = out[0][2];
     }
   }
+  E.drain();
 }
 
 // first: 3 -> 65, hidden 128, F 16; second: 70 -> 3, hidden 64, F 16; both leaky_relu, no latent
@@ -663,7 +650,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     float* alpha = (float*)ws;
     float* rgb_raw = (float*)(ws + a256(n * 4));
     auto kern = k_nerfle16<kNerfWaves>;
-    const size_t lds = ring::KEngine<kNerfWaves, kNerfMaxF>::lds_bytes(pd);
+    const size_t lds = ring::KEngine<kNerfWaves, kNerfMaxF, kNerfDma>::lds_bytes(pd);
     if (int rc = set_lds(kern, lds)) return rc;
     int dev = 0, cus = 0, per_cu = 0;
     NRT_HIP(hipGetDevice(&dev));

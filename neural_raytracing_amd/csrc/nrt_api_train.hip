@@ -479,14 +479,18 @@ __global__ void __launch_bounds__(256) k_colsum_partial(const float* __restrict_
     part[(int64_t)blockIdx.x * R + c] = ((red[0][c & 63] + red[1][c & 63]) + red[2][c & 63]) + red[3][c & 63];
 }
 
+// one wave per column: lane l sums chunks l, l + 64, ... in order, then a fixed xor-butterfly
+// (deterministic; a thread per column walking all chunks was latency-bound at ~55 us a call)
 template <int = 0>
-__global__ void k_colsum_final(const float* __restrict__ part, int R, int chunks,
-                               float* __restrict__ db) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= R) return;
+__global__ void __launch_bounds__(256) k_colsum_final(const float* __restrict__ part, int R,
+                                                      int chunks, float* __restrict__ db) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= R) return;  // whole wave
   float acc = 0.f;
-  for (int k = 0; k < chunks; ++k) acc += part[(int64_t)k * R + c];
-  db[c] = acc;
+  for (int k = lane; k < chunks; k += 64) acc += part[(int64_t)k * R + c];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
+  if (lane == 0) db[c] = acc;
 }
 
 int grad_bias(const float* dZ, int R, int64_t M, float* part, float* db, hipStream_t st) {
@@ -494,7 +498,7 @@ int grad_bias(const float* dZ, int R, int64_t M, float* part, float* db, hipStre
   const int64_t rpc = std::max<int64_t>(64, (M + kBiasChunks - 1) / kBiasChunks);
   const int chunks = (int)((M + rpc - 1) / rpc);
   k_colsum_partial<><<<dim3(chunks, (R + 63) / 64), dim3(256), 0, st>>>(dZ, R, M, rpc, part);
-  k_colsum_final<><<<dim3((R + 255) / 256), dim3(256), 0, st>>>(part, R, chunks, db);
+  k_colsum_final<><<<dim3((R + 3) / 4), dim3(256), 0, st>>>(part, R, chunks, db);
   return check_launch("k_colsum");
 }
 }  // namespace

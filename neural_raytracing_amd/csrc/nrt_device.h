@@ -565,9 +565,6 @@ __device__ __forceinline__ void mlp32_backward_out0(const MlpDev& m, const EncIn
 // LDS, issues its global loads for chunk c+2 into registers, then runs chunk c's MFMAs with A
 // read by ds_read_b128 from LDS; one barrier per chunk.  Loads and stores are unconditional
 // (fixed count per wave; slots are padded) so hipcc never drains vmcnt inside the loop.
-#ifndef NRT_EXP
-#define NRT_EXP 0  // timing-only experiment bits (tools/exp_variants.sh); 0 in every shipped build
-#endif
 namespace nrt {
 namespace ring {
 
@@ -577,11 +574,6 @@ __device__ __forceinline__ float sp2(float x) {
   // the only loss is below the f16 the result is rounded to: 1 + 2^x rounds to 1 for x < -24
   // (true value < 9e-8) and 2^x overflows for x >= 128 (a natural pre-activation above 88),
   // which the FP16 path does not support; the FP32 path keeps torch's exact form.
-  if (NRT_EXP & 2) return x;
-  if (NRT_EXP & 32) {
-    const float pos = __int_as_float(max(__float_as_int(x), 0));
-    return pos + __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(-fabsf(x)));
-  }
   return __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(x));
 }
 
@@ -653,17 +645,8 @@ __device__ __forceinline__ void static_for(F&& f) {
 // Written as asm so hipcc neither drains it with vmcnt(0) before every ring read (it cannot
 // tell the DMA target from the slot being read) nor counts it: the engine waits for it itself.
 // M0 is compiler-reserved, so it is saved and restored inside the statement.
-#ifndef NRT_M0
-#define NRT_M0 0  // 1: pass the LDS address through an "{m0}" operand (no save / restore)
-#endif
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t srd, int voff, int soff,
                                           uint32_t lds_addr) {
-  if (NRT_M0) {
-    asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
-                 :
-                 : "v"(voff), "s"(srd), "{m0}"(lds_addr), "s"(soff));
-    return;
-  }
   unsigned keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -716,7 +699,6 @@ struct Engine {
   // once, stalling their MFMA issue.
   template <int CH>
   __device__ __forceinline__ void dma_at(int k, int nm) {
-    if (NRT_EXP & 4) return;
     constexpr int c = CH + D - 1;
     const int pieces = C::loads(c);
 #pragma unroll
@@ -784,7 +766,7 @@ struct Engine {
     // hipcc may leave the last A reads of chunk c-1 in flight past the barrier otherwise
     asm volatile("" ::: "memory");
     __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(after(c)));
-    if (!(NRT_EXP & 1)) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * C::SLOTF * 64 + lane;
@@ -816,50 +798,12 @@ __device__ __forceinline__ void chain_schedule() {
   __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
 }
 
-#ifndef NRT_SP2
-#define NRT_SP2 0  // softplus of the folded FP16 ring: 0 exp+log, 1 f32 polynomial, 2 packed f16
-#endif
-// log2(1 + y) on [0, 1] = y Q(y), Q a degree-4 least-squares fit on Chebyshev nodes (max abs error
-// 5.9e-5 in f32, below the f16 the activation is rounded to)
-__device__ __forceinline__ float sp2_poly(float x) {
-  const float y = __builtin_amdgcn_exp2f(-fabsf(x));
-  float q = fmaf(0.05994559f, y, -0.22771265f);
-  q = fmaf(q, y, 0.44227418f);
-  q = fmaf(q, y, -0.7170639f);
-  q = fmaf(q, y, 1.4426156f);
-  return fmaf(q, y, __int_as_float(max(__float_as_int(x), 0)));
-}
-typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ h2v sp2_pk(float a, float b) {
-  const h2v x = {(_Float16)a, (_Float16)b};
-  const h2v na = -__builtin_elementwise_abs(x);
-  const h2v y = __builtin_elementwise_exp2(na);
-  h2v q = __builtin_elementwise_fma(h2v{(_Float16)0.05994559f, (_Float16)0.05994559f}, y,
-                                    h2v{(_Float16)-0.22771265f, (_Float16)-0.22771265f});
-  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)0.44227418f, (_Float16)0.44227418f});
-  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)-0.7170639f, (_Float16)-0.7170639f});
-  q = __builtin_elementwise_fma(q, y, h2v{(_Float16)1.4426156f, (_Float16)1.4426156f});
-  return __builtin_elementwise_fma(q, y, __builtin_elementwise_max(x, h2v{(_Float16)0.f, (_Float16)0.f}));
-}
-
 template <bool FOLD>
 __device__ __forceinline__ void act_pack1(const f16v& acc, h8& lo, h8& hi, int act) {
-  if (FOLD && NRT_SP2 == 2) {
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      const h2v l = sp2_pk(acc[j], acc[j + 1]), h = sp2_pk(acc[8 + j], acc[9 + j]);
-      lo[j] = l[0]; lo[j + 1] = l[1];
-      hi[j] = h[0]; hi[j + 1] = h[1];
-    }
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     float a = acc[j], b = acc[8 + j];
-    if (FOLD) {
-      if (NRT_SP2 == 1) { a = sp2_poly(a); b = sp2_poly(b); }
-      else { a = sp2(a); b = sp2(b); }
-    }
+    if (FOLD) { a = sp2(a); b = sp2(b); }
     else { a = act_fwd<true>(a, act); b = act_fwd<true>(b, act); }
     lo[j] = (_Float16)a;
     hi[j] = (_Float16)b;
@@ -1022,7 +966,7 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
       for (int s = 0; s < 2 * NB; ++s)
 #pragma unroll
         for (int b = 0; b < RB; ++b) {
-          acc[b] = mfma16((NRT_EXP & 16) ? hv[src][(s + 1) % (2 * NB)] : A[(s * RB + b) * 64], hv[src][s], acc[b]);
+          acc[b] = mfma16(A[(s * RB + b) * 64], hv[src][s], acc[b]);
           E.template dma_at<1 + i * G + j>(s * RB + b, nm);
         }
       if (skip) {
@@ -1076,19 +1020,24 @@ __device__ __forceinline__ float eval(Engine<NB, NE, WV>& E, const MlpDev& m, fl
 // per layer), which keeps wide encodings (F = 64 / 128) out of the register file.  The layer
 // count and skip period are runtime values.
 // ------------------------------------------------------------------------------------------
-template <int WV, int MAXF_ = 16>
+// DMA = true: the chunks go global -> LDS by LDS-DMA (buffer_load ... lds, as ring::Engine):
+// no staging registers and no ds_write per piece; a wave waits for its own pieces of the next
+// chunk with a counted vmcnt before the chunk barrier.
+template <int WV, int MAXF_ = 16, bool DMA = false>
 struct KEngine {
   static constexpr int MAXF = MAXF_;  // fragments per chunk: KC * NB <= MAXF (out layer: KC)
   static constexpr int MAXL = (MAXF + WV - 1) / WV;
   static constexpr int SLOTF = MAXL * WV;
   static constexpr int RING_BYTES = 3 * SLOTF * 1024;
+  static constexpr int NSTG = DMA ? 1 : MAXL;
   h8* ring;
+  uint32_t ring_lds;
   const float* lbias;
   const float4* lbasis;
   __amdgpu_buffer_rsrc_t srd;
   const NRT_CONST int* coff;
   int nch, c, slot, lane, wv;
-  h8 stg[MAXL];
+  h8 stg[NSTG];
 
   __host__ __device__ static size_t lds_bytes(const ProgDev& p) {
     return RING_BYTES + (size_t)p.basis_q * 16 + (size_t)p.bias_floats * 4;
@@ -1106,10 +1055,21 @@ struct KEngine {
 #pragma unroll
     for (int q = 0; q < MAXL; ++q) D[(wv + WV * q) * 64] = stg[q];
   }
+  // DMA: this wave's MAXL pieces of `chunk` into slot sl (pieces past the chunk's end read the
+  // stream's zero padding / next chunk: harmless, and the count stays compile-time)
+  __device__ __forceinline__ void dma(int chunk, int sl) {
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    const int off = __builtin_amdgcn_readfirstlane((coff[chunk] + w) * 1024);
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)((sl * SLOTF + w) * 1024));
+#pragma unroll
+    for (int q = 0; q < MAXL; ++q) lds_dma16(srd, lane * 16, off + WV * q * 1024, dst + WV * q * 1024);
+  }
   __device__ __forceinline__ int nxt(int x) const { return x + 1 == nch ? 0 : x + 1; }
-  // block-wide: LDS = ring | basis | bias; afterwards slot 0 = chunk 0, stg = chunk 1
+  // block-wide: LDS = ring | basis | bias; afterwards slot 0 = chunk 0 and chunk 1 is on its way
+  // (DMA: in flight into slot 1; otherwise staged in stg)
   __device__ __forceinline__ void init(const ProgDev& p, char* lds) {
     ring = reinterpret_cast<h8*>(lds);
+    ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
     float4* lq = reinterpret_cast<float4*>(lds + RING_BYTES);
     for (int q = threadIdx.x; q < p.basis_q; q += blockDim.x) lq[q] = p.basis[q];
     lbasis = lq;
@@ -1123,22 +1083,44 @@ struct KEngine {
     wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     c = 0;
     slot = 0;
-    load(0);
-    store(0);
-    load(nxt(0));
+    if (DMA) {
+      dma(0, 0);
+      dma(nxt(0), 1);
+      __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(MAXL));  // chunk 0 landed
+    } else {
+      load(0);
+      store(0);
+      load(nxt(0));
+    }
     __syncthreads();
   }
   __device__ __forceinline__ const h8* begin() {
     const int s1 = slot == 2 ? 0 : slot + 1;
-    store(s1);
-    load(nxt(nxt(c)));
+    if (DMA) {
+      dma(nxt(nxt(c)), s1 == 2 ? 0 : s1 + 1);  // into the slot chunk c-1 was read from
+    } else {
+      store(s1);
+      load(nxt(nxt(c)));
+    }
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * SLOTF * 64 + lane;
   }
   __device__ __forceinline__ void end() {
-    __syncthreads();
+    if (DMA) {
+      // own pieces of chunk c+1 landed (those of c+2 may fly on); own reads of this slot retired
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(MAXL));
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
     c = nxt(c);
     slot = slot == 2 ? 0 : slot + 1;
+  }
+  // DMA: no LDS write may still be in flight when the block's waves exit
+  __device__ __forceinline__ void drain() {
+    if (DMA) __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0));
   }
   // acc[reg] = bias[layer][32 ib + (reg&3) + 8 (reg>>2) + 4h]
   __device__ __forceinline__ f16v bias_at(const ProgMlp& pm, int layer, int ib, int h) const {

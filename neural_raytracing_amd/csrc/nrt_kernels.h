@@ -368,9 +368,6 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
 // smallest value and, among equal values, the first sample -- the reference's strict-< update.
 // A second launch (mode 1) evaluates sdf(best) for the throughput.  Lanes l and l + 32 carry the
 // same ray (the MFMA K halves) and run identical state machines.
-#ifndef NRT_KEY_SCOPE
-#define NRT_KEY_SCOPE 0
-#endif
 constexpr int kScanSegs = 8;  // sample j in [0, 128]: segment 0 = [0, 16], segment q = [16q+1, 16q+16]
 #ifndef NRT_SCAN_SPLIT
 #define NRT_SCAN_SPLIT 64
@@ -485,14 +482,11 @@ __device__ __forceinline__ void march_body(
         }
       } else if (kind == 1) {
         if (j > jend) {
-          // all segments of a ray are in this wave's list: the merge never crosses a workgroup
-          // (NRT_KEY_SCOPE 1 keeps it in the XCD's L2 instead of the memory-side atomic unit)
+          // a whole scan stores its key; a segment merges into it (all segments of a ray are
+          // in this wave's list; the key buffer starts at all-ones)
           if (lane < RPW) {
             if (whole)
               keys[ray] = (unsigned long long)scan_key(best, idx);
-            else if (NRT_KEY_SCOPE == 1)
-              __hip_atomic_fetch_min(keys + ray, (unsigned long long)scan_key(best, idx),
-                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             else
               atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
           }

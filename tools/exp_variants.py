@@ -1,10 +1,9 @@
 """Build timing variants of libnrt_hip.so into build_var/ (one box session then times them all).
 
-A variant is NAME=FLAGS, e.g.  e1=-DNRT_EXP=1  d3=-DNRT_RING_DEPTH=3.  Only the SDF translation
-units are recompiled; the others come from the normal build.  NRT_EXP variants compute wrong
-results on purpose (no barrier, no activation, ...) and exist to price one component of the
-march kernel: never ship or test them.  Usage:
-    python tools/exp_variants.py e1=-DNRT_EXP=1 d3=-DNRT_RING_DEPTH=3
+A variant is NAME=FLAGS, e.g.  d3=-DNRT_RING_DEPTH=3  c32=-DNRT_RAY_CHUNK=32.  Only the SDF
+translation units are recompiled (VARIED=a.hip,b.hip to choose others); the others come from the
+normal build.  Usage:
+    python tools/exp_variants.py d3=-DNRT_RING_DEPTH=3 c32=-DNRT_RAY_CHUNK=32
 then on the box:  bash tools/exp_run.sh e1 d3
 """
 import os

@@ -5,6 +5,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "nerfle or plain_nerf" -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/nerf_tests.log 2>&1 || { tail -20 gpurun_out/nerf_tests.log; exit 1; }
 tail -1 gpurun_out/nerf_tests.log
+for V in "$@"; do
+  NRT_LIB=build_var/libnrt_hip_$V.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "nerfle" -x -q --timeout 120 --timeout-method thread -m gpu > gpurun_out/nerf_tests_$V.log 2>&1 || { echo "$V parity failed"; tail -20 gpurun_out/nerf_tests_$V.log; exit 1; }
+  echo "$V $(tail -1 gpurun_out/nerf_tests_$V.log)"
+done
 BENCH_EXTRA="--scene nerfle" bash tools/exp_run.sh "$@" || exit 1
 rm -rf gpurun_out/pmc_nerf
 mkdir -p gpurun_out/pmc_nerf
