@@ -496,7 +496,9 @@ def test_ring_march_zero_shift_matches_oracle(P):
 def test_ring_march_schedule_invariant(monkeypatch):
     """Results of the persistent load-balanced march do not depend on the grid: 1, 5 and the
     default number of blocks give bit-identical t, hit, p, n and throughput (each ray's
-    arithmetic is its own; only which lane runs it changes)."""
+    arithmetic is its own; only which lane runs it changes).  At 1 and 5 blocks a wave owns 375 /
+    75 rays, so most scans run as whole 129-point jobs with a plain key store; at the default grid
+    every ray is in the segmented tail (atomicMin merge): the two scan paths agree bit for bit."""
     from neural_raytracing_amd import set_precision
     from neural_raytracing_amd.pathtracer.shapes import SDF
     _, mine = _ring_blob(256, 16, 8)

@@ -17,7 +17,7 @@ if [ "$STEP" = all ] || [ "$STEP" = bench ]; then
   rc=$?; echo "BENCH EXIT $rc"; tail -1 gpurun_out/bench.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-fp32-check > gpurun_out/prof.log 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-fp32-check --no-extra-legs > gpurun_out/prof.log 2>&1
   rc=$?; echo "PROF EXIT $rc"; tail -1 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$STEP" = all ] || [ "$STEP" = pmc ]; then
