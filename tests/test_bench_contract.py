@@ -6,8 +6,8 @@ import json
 import pathlib
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-BENCH = ROOT / "profiles" / "r02_v6_bench.json"
-STATS = ROOT / "profiles" / "r02_v6_kernel_stats.csv"
+BENCH = ROOT / "profiles" / "r02_final/bench.json"
+STATS = ROOT / "profiles" / "r02_final/kernel_stats.csv"
 
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
