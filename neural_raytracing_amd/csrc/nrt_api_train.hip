@@ -90,7 +90,14 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
     wave_lds_fence();
   }
   // ---- backward seed: dZ_L = (dY W_out) * act'(Z_L)
-  float* egrad = rowp + H + ke;
+  // The encoding gradient accumulates in the slab's encoding slots (the backward GEMMs read only
+  // columns [0, H)); the skip layers' act'(enc) reads the raw encoding back from Eraw, which this
+  // wave wrote above (row rr is always one of this wave's own rows).  One slab row is H + ke
+  // floats instead of H + 2 ke: twice the waves per CU for the 16x256 F=128 spatial-weights MLP.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  float* egrad = rowp + H;
+  const float* eraw_row = Eraw + rr * dp;
   for (int s = h; s < ke; s += 2) egrad[s] = 0.f;
   const float* Ao = m.w32[L + 1];
   const int out = m.out;
@@ -124,7 +131,10 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
             const int slot = pos - enc_pos0;
             if (slot >= 0 && slot < ke) {
               float v = acc[ib][reg];
-              if (l != 0) v *= act_bwd(rowp[H + slot], m.act);  // skip inputs are act(enc)
+              if (l != 0) {  // skip inputs are act(enc)
+                const int c = enc_col(m, slot);
+                v = c < 0 ? 0.f : v * act_bwd(eraw_row[c], m.act);
+              }
               egrad[slot] += v;
             }
           }
@@ -541,7 +551,8 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     return NRT_OK;
   }
   TrainWs w = carve(m, M, workspace);
-  LdsPlan lp = plan_lds(H, d.ke, 1, false, true);
+  // slab row [a | encoding, then its gradient]: H + ke floats (see k_mlp_backward32)
+  LdsPlan lp = plan_lds(H, d.ke, 1, false, false);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
