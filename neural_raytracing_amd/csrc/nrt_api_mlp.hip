@@ -12,6 +12,7 @@ int nrt_mlp_forward(const nrt_mlp* m, const float* x, const float* latent, int64
   if (m->desc.latent > 0 && !latent) { set_error("nrt_mlp_forward: latent required"); return NRT_EINVAL; }
   const bool f16 = precision == NRT_FP16;
   LdsPlan p = plan_lds(m->desc.hidden, m->host_dev.ke, m->desc.out, f16, false);
+  if (!f16) spread_waves(p);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, p.waves)), block(64 * p.waves);
   hipStream_t st = (hipStream_t)stream;

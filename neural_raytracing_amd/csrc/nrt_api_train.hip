@@ -553,6 +553,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   TrainWs w = carve(m, M, workspace);
   // slab row [a | encoding, then its gradient]: H + ke floats (see k_mlp_backward32)
   LdsPlan lp = plan_lds(H, d.ke, 1, false, false);
+  spread_waves(lp);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;

@@ -55,6 +55,17 @@ static inline LdsPlan plan_lds(int hidden, int ke, int ys, bool f16, bool with_g
   return p;
 }
 
+// Re-cut an LDS-bound plan into the block size that fits the most waves per CU (at most 2 per
+// SIMD): waves are independent, so a 29 KB-a-wave FP32 slab (the 6x96 NeuralBSDF) runs as five
+// one-wave blocks per CU instead of one four-wave block.
+static inline void spread_waves(LdsPlan& p) {
+  const int per_cu = std::min(8, kLdsBytes / std::max(p.per_wave * 4, 1));
+  int b = std::min(p.waves, per_cu);
+  while (b > 1 && (per_cu / b) * b < per_cu) --b;
+  p.waves = std::max(1, b);
+  p.bytes = (size_t)p.waves * p.per_wave * 4;
+}
+
 template <typename K>
 static inline int set_lds(K kernel, size_t bytes) {
   if (bytes > 64 * 1024) {
