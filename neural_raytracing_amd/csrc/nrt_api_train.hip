@@ -25,17 +25,23 @@ __device__ __forceinline__ int enc_col(const MlpDev& m, int s) {
   return -1;
 }
 
-template <int NB>
+// TILE: the encoding and its gradient live in per-wave global tiles [ke][32 rows] (L2-resident)
+// and the LDS slab row is the H hidden columns only -- for MLPs whose H + ke slab row caps the CU
+// at two waves (the 16x256 F=128 spatial-weights MLP: 68 KB a wave -> 33 KB).  Otherwise the slab
+// row is [hidden | encoding], and the encoding slots take the encoding gradient in the backward.
+template <int NB, bool TILE>
 __global__ void __launch_bounds__(256) k_mlp_backward32(
     const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
     int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
     float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
-    float* __restrict__ Eact, float* __restrict__ dZg, int RS, int per_wave) {
+    float* __restrict__ Eact, float* __restrict__ dZg, float* __restrict__ Et,
+    float* __restrict__ Gt, int RS, int per_wave) {
   extern __shared__ float smem[];
   const MlpDev& m = *mp;
   float* X = smem + (size_t)(threadIdx.x >> 6) * per_wave;
   const int lane = lane_id(), r = lane & 31, h = lane >> 5;
-  const int64_t row0 = wave_global() * 32;
+  const int64_t wg = wave_global();
+  const int64_t row0 = wg * 32;
   if (row0 >= M) return;  // whole wave exits together
   const int64_t row = row0 + r;
   const bool valid = row < M;
@@ -51,14 +57,27 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
   }
   e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
   float* rowp = X + r * RS;
+  // slot s of this lane's row: encoding in the forward, its gradient in the backward
+  float* const et = TILE ? Et + wg * ke * 32 + r : rowp + H;
+  float* const gt = TILE ? Gt + wg * ke * 32 + r : rowp + H;
+  constexpr int es = TILE ? 32 : 1;
   // ---- forward (mlp32_forward's order of operations), saving Z_l, A_l and the encoding
-  write_enc_slab<false>(m, e, X, RS);
+  for (int slot = 2 * h; slot < ke; slot += 4) {
+    float a, b;
+    enc_pair<false>(m, e, slot, a, b);
+    et[slot * es] = a;
+    et[(slot + 1) * es] = b;
+  }
   wave_lds_fence();
+  if (TILE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   if (valid)
     for (int s = h; s < ke; s += 2) {
       const int c = enc_col(m, s);
       if (c < 0) continue;
-      const float v = rowp[H + s];
+      const float v = et[s * es];
       Eraw[row * dp + c] = v;
       Eact[row * dp + c] = act_fwd<false>(v, m.act);
     }
@@ -66,12 +85,16 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
   for (int l = 0; l <= L; ++l) {
     bias32<NB>(acc, m.bias[l], 0, NB, h);
     if (l == 0) {
-      gemm32<NB>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, H, -1);
+      if (TILE) gemm32_tile<NB>(acc, m.w32[0], NB, 0, ke >> 1, et - r, -1);
+      else gemm32<NB>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, H, -1);
     } else {
       const int i = l - 1;
       gemm32<NB>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
-      if (i != L - 1 && (i % m.skip) == 0)
-        gemm32<NB>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, H, m.act);
+      if (i != L - 1 && (i % m.skip) == 0) {
+        const float* Ws = m.w32[l] + (H >> 1) * NB * 64;
+        if (TILE) gemm32_tile<NB>(acc, Ws, NB, 0, ke >> 1, et - r, m.act);
+        else gemm32<NB>(acc, Ws, NB, 0, ke >> 1, X, RS, H, m.act);
+      }
     }
     wave_lds_fence();
 #pragma unroll
@@ -90,15 +113,18 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
     wave_lds_fence();
   }
   // ---- backward seed: dZ_L = (dY W_out) * act'(Z_L)
-  // The encoding gradient accumulates in the slab's encoding slots (the backward GEMMs read only
-  // columns [0, H)); the skip layers' act'(enc) reads the raw encoding back from Eraw, which this
-  // wave wrote above (row rr is always one of this wave's own rows).  One slab row is H + ke
-  // floats instead of H + 2 ke: twice the waves per CU for the 16x256 F=128 spatial-weights MLP.
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  float* egrad = rowp + H;
+  // The encoding gradient accumulates in gt: slot s of row r belongs to lane (r, (s >> 2) & 1)
+  // in every accumulation pass (the MFMA output layout), so a lane only re-reads its own stores
+  // until the fence before dL/dx.  The skip layers' act'(enc) reads the raw encoding back from
+  // Eraw, which this wave wrote above (row rr is always one of this wave's own rows).
+  if (!TILE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
   const float* eraw_row = Eraw + rr * dp;
-  for (int s = h; s < ke; s += 2) egrad[s] = 0.f;
+  for (int s = 4 * h; s < ke; s += 8)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gt[(s + j) * es] = 0.f;
   const float* Ao = m.w32[L + 1];
   const int out = m.out;
   for (int k = h; k < H; k += 2) {
@@ -135,7 +161,7 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
                 const int c = enc_col(m, slot);
                 v = c < 0 ? 0.f : v * act_bwd(eraw_row[c], m.act);
               }
-              egrad[slot] += v;
+              gt[slot * es] += v;
             }
           }
         }
@@ -158,20 +184,26 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
     }
   }
   // ---- encoding -> inputs: d sin(p_q) = cos(p_q) B_iq, d cos(p_q) = -sin(p_q) B_iq, x_i direct
+  wave_lds_fence();
+  if (TILE) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  }
+  const float* egrad = gt;  // egrad[es * s] = slot s of this lane's row
   const int F = m.freqs;
   for (int i = 0; i < in; ++i) {
     float g = 0.f;
     for (int q = h; q < F; q += 2) {
       float s, c;
       sincosf(proj<false>(m, e, q), &s, &c);
-      g = fmaf(egrad[2 * q] * c - egrad[2 * q + 1] * s, m.basis[i * F + q], g);
+      g = fmaf(egrad[es * (2 * q)] * c - egrad[es * (2 * q + 1)] * s, m.basis[i * F + q], g);
     }
-    if (h == 0) g += egrad[2 * F + i];
+    if (h == 0) g += egrad[es * (2 * F + i)];
     g += __shfl_xor(g, 32);
     if (dX && valid && h == 0) dX[row * in + i] = g;
   }
   if (dLat && valid)
-    for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[2 * F + in + j];
+    for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[es * (2 * F + in + j)];
 }
 
 // second derivative of act at pre-activation x (torch double-backward formulas:
@@ -366,8 +398,13 @@ constexpr int kBiasChunks = 256;  // bias-gradient partial sums (k_colsum_*)
 constexpr int kBiasMaxR = 256;
 
 struct TrainWs {
-  float *Z, *A, *dZ, *Eraw, *Eact, *part, *kpart;
+  float *Z, *A, *dZ, *Eraw, *Eact, *Et, *Gt, *part, *kpart;
 };
+
+// per-wave encoding / encoding-gradient tiles of k_mlp_backward32: [waves][ke][32] floats
+static inline size_t enc_tile_bytes(const MlpDev& d, int64_t M) {
+  return (size_t)((M + 31) / 32) * 32 * (size_t)d.ke * 4;
+}
 
 TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   const MlpDev& d = m->host_dev;
@@ -380,6 +417,8 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   w.dZ = (float*)p; p += a256(lay);
   w.Eraw = (float*)p; p += a256(enc);
   w.Eact = (float*)p; p += a256(enc);
+  w.Et = (float*)p; p += a256(enc_tile_bytes(d, M));
+  w.Gt = (float*)p; p += a256(enc_tile_bytes(d, M));
   w.part = (float*)p; p += a256((size_t)kBiasChunks * kBiasMaxR * 4);
   w.kpart = (float*)p;
   return w;
@@ -525,8 +564,8 @@ size_t nrt_mlp_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
   const MlpDev& d = m->host_dev;
   const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
   const size_t enc = (size_t)M * d.dp * 4;
-  return 3 * a256(lay) + 2 * a256(enc) + a256((size_t)kBiasChunks * kBiasMaxR * 4) +
-         a256(split_part_floats(d) * 4);
+  return 3 * a256(lay) + 2 * a256(enc) + 2 * a256(enc_tile_bytes(d, M)) +
+         a256((size_t)kBiasChunks * kBiasMaxR * 4) + a256(split_part_floats(d) * 4);
 }
 
 int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int64_t M,
@@ -551,19 +590,38 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     return NRT_OK;
   }
   TrainWs w = carve(m, M, workspace);
-  // slab row [a | encoding, then its gradient]: H + ke floats (see k_mlp_backward32)
-  LdsPlan lp = plan_lds(H, d.ke, 1, false, false);
-  spread_waves(lp);
+  // LDS slab row [hidden | encoding] (H + ke floats), or [hidden] with the encoding in global
+  // tiles when that at least doubles the waves per CU (k_mlp_backward32's TILE)
+  auto plan = [&](bool tile) {
+    LdsPlan p;
+    p.RS = (std::max(H, 32) + (tile ? 0 : d.ke)) | 1;
+    p.per_wave = wave_lds_floats(p.RS, 1, false);
+    p.waves = std::max(1, std::min(4, kLdsBytes / (p.per_wave * 4)));
+    p.bytes = (size_t)p.waves * p.per_wave * 4;
+    spread_waves(p);
+    return p;
+  };
+  const LdsPlan slab = plan(false), tiled = plan(true);
+  const auto per_cu = [](const LdsPlan& p) { return std::min(8, kLdsBytes / (p.per_wave * 4)); };
+  const bool tile = per_cu(tiled) >= 2 * per_cu(slab);
+  const LdsPlan lp = tile ? tiled : slab;
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
   {
     ProfScope prof("k_mlp_backward32", st);
     NRT_NB_SWITCH(d.nb, {
-      if (!(rc = set_lds(k_mlp_backward32<NB>, lp.bytes)))
-        k_mlp_backward32<NB><<<grid, block, lp.bytes, st>>>(m->dev, x, latent, M, dy, dx, dlatent,
-                                                            w.Z, w.A, w.Eraw, w.Eact, w.dZ, lp.RS,
-                                                            lp.per_wave);
+      if (tile) {
+        if (!(rc = set_lds(k_mlp_backward32<NB, true>, lp.bytes)))
+          k_mlp_backward32<NB, true><<<grid, block, lp.bytes, st>>>(
+              m->dev, x, latent, M, dy, dx, dlatent, w.Z, w.A, w.Eraw, w.Eact, w.dZ, w.Et, w.Gt,
+              lp.RS, lp.per_wave);
+      } else {
+        if (!(rc = set_lds(k_mlp_backward32<NB, false>, lp.bytes)))
+          k_mlp_backward32<NB, false><<<grid, block, lp.bytes, st>>>(
+              m->dev, x, latent, M, dy, dx, dlatent, w.Z, w.A, w.Eraw, w.Eact, w.dZ, w.Et, w.Gt,
+              lp.RS, lp.per_wave);
+      }
     });
     if (rc) return rc;
     if ((rc = check_launch("k_mlp_backward32"))) return rc;

@@ -411,6 +411,47 @@ __device__ __forceinline__ void gemm32(f16v (&acc)[NB], const float* __restrict_
   if (s < nks) step(a0, s);
 }
 
+// gemm32 with B from a per-wave global tile T[slot][32 rows] (coalesced: a k-step reads two
+// 128-byte rows) instead of the LDS slab; B is prefetched one k-step ahead like the A fragments.
+// Used by k_mlp_backward32 to keep the encoding out of LDS.
+template <int NB>
+__device__ __forceinline__ void gemm32_tile(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
+                                            int rb0, int nks, const float* T, int act_in) {
+  using gptr = const __attribute__((address_space(1))) float*;
+  if (nks <= 0) return;
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const gptr Bg = (gptr)(T + h * 32 + r);
+  const gptr Ag = (gptr)(A + (size_t)rb0 * 64 + lane);
+  const int stride = nrb * 64;
+  int off[NB];
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) off[ib] = (rb0 + ib < nrb ? ib : nrb - 1 - rb0) * 64;
+  float a0[NB], a1[NB], b0, b1;
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[off[ib]];
+  b0 = Bg[0];
+  auto step = [&](const float (&a)[NB], float b) {
+    if (act_in >= 0) b = act_fwd<false>(b, act_in);
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+      if (rb0 + ib < nrb) acc[ib] = mfma32(a[ib], b, acc[ib]);
+  };
+  int s = 0;
+  for (; s + 1 < nks; s += 2) {
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a1[ib] = Ag[(size_t)(s + 1) * stride + off[ib]];
+    b1 = Bg[(s + 1) * 64];
+    step(a0, b0);
+    const int s2 = s + 2 < nks ? s + 2 : nks - 1;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[(size_t)s2 * stride + off[ib]];
+    b0 = Bg[s2 * 64];
+    step(a1, b1);
+  }
+  if (s < nks) step(a0, b0);
+}
+
 template <int NB>
 __device__ __forceinline__ void bias32(f16v (&acc)[NB], const float* bias, int rb0, int nrb, int h) {
 #pragma unroll
