@@ -5,7 +5,8 @@
 //                     forward with saved pre-activations Z_l and activations A_l = act(Z_l),
 //                     the encoding (raw and activated) in the reference's column order, then the
 //                     row-local backward chain dZ_l = (dZ_{l+1} W_{l+1}) * act'(Z_l) with the W^T
-//                     fragments, the encoding gradient, and dL/dx, dL/dlatent.
+//                     fragments, the encoding gradient, and dL/dx, dL/dlatent.  TILE moves the
+//                     encoding and its gradient out of the slab into per-wave global tiles.
 //   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M): rocBLAS sgemm on the saved
 //                     activations; bias gradients = column sums of dZ_l (k_colsum_*).
 #include <rocblas/rocblas.h>
