@@ -46,7 +46,7 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
                               const float* const* weights, const float* const* biases,
                               nrt_mlp** out) {
   using namespace nrt;
-  if (!d || !basis || !weights || !biases || !out) {
+  if (!d || (!basis && d->freqs > 0) || !weights || !biases || !out) {
     set_error("nrt_mlp_create: null argument");
     return NRT_EINVAL;
   }
@@ -101,7 +101,11 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   md.skip = d->skip; md.latent = lat; md.act = d->activation;
   md.dp = dp; md.ke = ke; md.nb = NB; md.ob = OB;
 
-  size_t off_basis = blob.add(basis, sizeof(float) * (size_t)in * (F > 0 ? F : 1));
+  // [in, F] basis; at F = 0 the caller's basis is empty (it may be null) and a zero row stands in
+  // (found by the host ASan run, tools/asan: the copy read `in` floats past an empty basis)
+  std::vector<float> basis_h((size_t)in * (F > 0 ? F : 1), 0.f);
+  if (F > 0) std::memcpy(basis_h.data(), basis, sizeof(float) * (size_t)in * F);
+  size_t off_basis = blob.add(basis_h.data(), sizeof(float) * basis_h.size());
   std::vector<size_t> off16(layers.size()), off32(layers.size()), offt(layers.size()),
       offb(layers.size());
 
