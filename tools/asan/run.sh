@@ -20,6 +20,6 @@ done
 wait
 "$HIPCC" --offload-host-only -O1 -g -std=c++20 "${SAN[@]}" -Iinclude -c tools/asan/pack_driver.cpp \
   -o "$OUT/pack_driver.o"
-"$HIPCC" -fsanitize=address -o "$OUT/pack_driver" "$OUT/pack_driver.o" "${objs[@]}" \
+"$HIPCC" -fsanitize=address -fno-gpu-sanitize -o "$OUT/pack_driver" "$OUT/pack_driver.o" "${objs[@]}" \
   -L/opt/rocm/lib -lrocblas -Wl,-rpath,/opt/rocm/lib
 ASAN_OPTIONS=detect_leaks=0 "$OUT/pack_driver"
