@@ -44,11 +44,13 @@ def parse():
     ap.add_argument("--samples", type=int, default=None,
                     help="march steps per ray (max_steps) or NeRF depths per ray "
                          "(default 64; 256 for --scene nerfle, BASELINE cfg5)")
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32"],
+                    help="arithmetic of the headline frame (default fp32, the reference's; the "
+                         "fp16 frame is reported as the `fp16` leg)")
     ap.add_argument("--tile-rows", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-crop", type=int, default=128, help="side of the CPU-baseline crop")
-    ap.add_argument("--no-fp32-check", action="store_true")
+    ap.add_argument("--no-fp32-check", action="store_true", help="no-op (kept for tools/)")
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the FP32 (reference precision) and scan-free timing legs")
     ap.add_argument("--scene", default="nerf_synthetic",
@@ -89,8 +91,11 @@ def view_c2w(i, n):
     return look_at((math.sin(a) * math.cos(0.4), math.sin(0.4), math.cos(a) * math.cos(0.4)))
 
 
-def build_scene(device, samples, seed=0):
-    """Product objects of the bench scene (identical on every rank)."""
+def build_scene(device, samples, seed=0, light_gain=1.0):
+    """Product objects of the bench scene (identical on every rank).  light_gain scales the
+    LightField MLP's output layer, i.e. the light magnitude |v| (lights.py:191-194): the bench
+    frame uses 10 so its RGB spans most of [0, 1] (at 1 it peaks near 0.09) and accuracy
+    numbers are not flattered by a dark image; the work is unchanged."""
     import neural_raytracing_amd.pathtracer as pt
     from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, NeuralBSDF
     from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
@@ -115,6 +120,10 @@ def build_scene(device, samples, seed=0):
         b.mlp.to(device)
     bsdf.sp_var_fn.to(device)
     lights = LightField(device="cpu").to(device)
+    if light_gain != 1.0:
+        with torch.no_grad():
+            lights.light_field_approx.out.weight.mul_(light_gain)
+            lights.light_field_approx.out.bias.mul_(light_gain)
     return dict(shape=shape, bsdf=bsdf, lights=lights, integrator=NeRFIntegrator(Direct()),
                 pt=pt)
 
@@ -199,6 +208,9 @@ def _copy_to_oracle(dst, src):
             a.bias.copy_(b.bias.cpu())
 
 
+LIGHT_GAIN = 10.0  # bench frame light magnitude x10: RGB spans most of [0, 1] (build_scene)
+
+
 def main():
     args = parse()
     if args.scene == "train":
@@ -222,7 +234,7 @@ def main():
     nra.set_precision(args.precision)
 
     size = args.size
-    scene = build_scene(device, args.samples)
+    scene = build_scene(device, args.samples, light_gain=LIGHT_GAIN)
     if world > 1:
         # every rank built the scene from the same seed; broadcasting rank 0's tensors makes the
         # replication explicit (a model loaded from file on rank 0 is replicated the same way)
@@ -265,36 +277,20 @@ def main():
     rays_per_rank = len(rows) * size * world  # this rank's rows of every view
     rays_total = world * size * size * args.steps
     value = rays_total * args.samples / elapsed
-    # algorithmic FLOP of one k_march16 launch: every ray at every march step and every scan
-    # point, the reference's own count (sdfs.py:119-131, 232-249); the lane-level job lists
-    # lower the executed work, not this count
-    flop_launch = rays_per_rank * (args.samples + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
-    avg_kernel_ms = k_ms / max(k_n, 1)
-    achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.precision]
-    # executed work of the march launch: evaluations the job lists actually ran (counted on the
-    # device while profiling), less the sdf(best) pass's one per ray
-    exec_flop = (evals - rays_per_rank) * FLOP_SDF_8x256
-    exec_achieved = exec_flop / (avg_kernel_ms * 1e-3) / 1e12
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
-    if os.path.exists(pmc_path):
-        try:
-            pm = json.load(open(pmc_path))
-            if pm.get("size") == size and pm.get("precision") == args.precision:
-                traffic = pm.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    roof = march_roofline(march_kernel, args.precision, rays_per_rank, args.samples, k_ms, k_n,
+                          evals, size)
+    roof["intersect_ms"] = i_ms / max(i_n, 1)
 
     extra = {}
     if rank == 0 and world == 1:
         with torch.no_grad():
             hit_frac = float(rr_hit_fraction(rr))
         extra["hit_fraction"] = round(hit_frac, 4)
-        if not args.no_fp32_check and args.precision == "fp16":
-            extra["psnr_fp16_vs_fp32"] = round(psnr_vs_fp32(scene, cameras, size), 2)
         if not args.no_extra_legs:
+            if args.precision == "fp32":
+                extra["fp16"] = fp16_leg(rr, args, rows, size)
             extra.update(extra_legs(scene, cameras, size, args, rows))
+            extra["api_paths"] = api_path_legs(scene, args)
         if not args.no_cpu_baseline:
             extra.update(cpu_baseline(scene, size, args))
 
@@ -315,34 +311,14 @@ def main():
             "config": {
                 "workload": f"{size}x{size} NeRFCamera frame per GPU, {args.samples} march steps + "
                             f"{SCAN_EVALS}-eval coarse scan per ray, SDF MLP 8x256 F16, "
-                            "8x NeuralBSDF(6x96) + 16x256 spatial MLP + LightField(10x256), "
-                            "NeRFIntegrator(Direct)",
+                            "8x NeuralBSDF(6x96) + 16x256 spatial MLP + LightField(10x256, "
+                            f"output x{LIGHT_GAIN:g}), NeRFIntegrator(Direct)",
                 "image": [size, size],
                 "samples_per_ray": args.samples,
                 "views_per_step": world,
                 "parallelism": f"row-tile shard x{world} ({args.tile_rows}-row tiles) + RCCL all-gather",
             },
-            "roofline": {
-                "bound": "mfma",
-                "kernel": march_kernel,
-                "achieved": achieved,
-                "peak": peak,
-                "unit": "TFLOP/s",
-                "frac": achieved / peak,
-                "traffic": traffic,
-                "traffic_source": (f"committed PMC pass, profiles/pmc_k_march16.json "
-                                   f"(FETCH_SIZE + WRITE_SIZE, {size}^2 {args.precision}); not "
-                                   "measured in this run") if traffic is not None else None,
-                "flop_per_launch": flop_launch,
-                "flop_basis": "algorithmic: every ray at every march step and scan point "
-                              "(sdfs.py:119-131, 232-249)",
-                "executed_flop_per_launch": exec_flop,
-                "executed_achieved": exec_achieved,
-                "executed_frac": exec_achieved / peak,
-                "avg_kernel_ms": avg_kernel_ms,
-                "launches": k_n,
-                "intersect_ms": i_ms / max(i_n, 1),
-            },
+            "roofline": roof,
             "sdf_evals_per_s": rays_total * (args.samples + SCAN_EVALS) / elapsed,
         }
         if "cpu_baseline" in extra:
@@ -351,6 +327,103 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def march_roofline(kernel, precision, rays, samples, k_ms, k_n, evals, size):
+    """Roofline object of one march + scan launch: algorithmic FLOP = every ray at every march
+    step and scan point (the reference's count, sdfs.py:119-131, 232-249) x the 8x256 MLP's FLOP
+    per evaluation, over the launch's HIP-event duration; `executed_*` counts the evaluations the
+    job lists actually ran (device counter, one untimed frame) less the sdf(best) pass's."""
+    flop_launch = rays * (samples + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
+    avg_kernel_ms = k_ms / max(k_n, 1)
+    achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[precision]
+    exec_flop = (evals - rays) * FLOP_SDF_8x256
+    exec_achieved = exec_flop / (avg_kernel_ms * 1e-3) / 1e12
+    traffic, source = None, None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("size") == size and pm.get("precision") == precision:
+                traffic = pm.get("hbm_bytes_per_launch")
+                source = (f"committed PMC pass, profiles/pmc_{kernel}.json (FETCH_SIZE + "
+                          f"WRITE_SIZE, {size}^2 {precision}); not measured in this run")
+        except Exception:
+            traffic = None
+    return {
+        "bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+        "frac": achieved / peak, "traffic": traffic, "traffic_source": source,
+        "flop_per_launch": flop_launch,
+        "flop_basis": "algorithmic: every ray at every march step and scan point "
+                      "(sdfs.py:119-131, 232-249)",
+        "executed_flop_per_launch": exec_flop, "executed_achieved": exec_achieved,
+        "executed_frac": exec_achieved / peak, "avg_kernel_ms": avg_kernel_ms, "launches": k_n,
+    }
+
+
+def _frame_state(rr, seed):
+    """One render with fixed camera jitter / scan jitter draws; returns (image, hit, t) copies."""
+    from neural_raytracing_amd.pathtracer import render as R
+    torch.manual_seed(seed)
+    random.seed(seed)
+    img = rr.render().clone()
+    b = next(iter(R._BUFS.values()))
+    return img, b.hit.clone().bool(), b.t.clone()
+
+
+def frame_accuracy(got, want, hit, rhit, t, rt):
+    """Full-frame comparison of two renders of the same rays (RGBA [..., 4]): max |diff|, pixels
+    with any channel off by more than 1e-4, hit flips, step flips (both hit, depth differs by
+    more than 1e-4: one march stopped a step earlier on an SDF value within rounding of eps),
+    RGB PSNR against the reference frame's own peak (mse2psnr with data range = the peak),
+    and the alpha error."""
+    err = (got - want).abs()
+    px = err.amax(-1).reshape(-1)
+    hit, rhit, t, rt = hit.reshape(-1), rhit.reshape(-1), t.reshape(-1), rt.reshape(-1)
+    step = (hit & rhit) & ((t - rt).abs() > 1e-4)
+    agree = (hit == rhit) & ~step
+    peak = float(want[..., :3].max())
+    mse = float(((got[..., :3] - want[..., :3]) ** 2).mean())
+    return {
+        "pixels": int(px.numel()), "hits": int(rhit.sum()),
+        "maxabs": float(err.max()), "maxabs_rgb": float(err[..., :3].max()),
+        "maxabs_alpha": float(err[..., 3].max()) if got.shape[-1] > 3 else None,
+        "pixels_over_1e-4": int((px > 1e-4).sum()),
+        "pixels_over_1e-3": int((px > 1e-3).sum()),
+        "pixels_over_1e-2": int((px > 1e-2).sum()),
+        "hit_flips": int((hit != rhit).sum()), "step_flips": int(step.sum()),
+        "maxabs_agreeing": float(px[agree].max()) if bool(agree.any()) else 0.0,
+        "rgb_peak": peak, "rgb_min": float(want[..., :3].min()),
+        "psnr_peak": (10 * math.log10(peak * peak / mse)) if mse > 0 else float("inf"),
+    }
+
+
+def fp16_leg(rr, args, rows, size, steps=5, warmup=2):
+    """The same frame on the FP16 MFMA path (march k_march16 on the 2.5 PF FP16 peak; sdf(best)
+    FP32, option scan_best32), timed, and compared over the whole frame with the FP32 frame of
+    the same rays and weights."""
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd import _lib
+    with torch.no_grad():
+        want, rhit, rt = _frame_state(rr, 1234)
+        nra.set_precision("fp16")
+        try:
+            el, ks, evals = _time_frames(rr.render, steps, warmup,
+                                         ["k_march16", "k_intersect", "k_scan_best32"])
+            got, hit, t = _frame_state(rr, 1234)
+        finally:
+            nra.set_precision(args.precision)
+    frame_rays = len(rows) * size
+    roof = march_roofline("k_march16", "fp16", frame_rays, args.samples, *ks["k_march16"],
+                          evals, size)
+    roof["intersect_ms"] = ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)
+    roof["scan_best32_ms"] = ks["k_scan_best32"][0] / max(ks["k_scan_best32"][1], 1)
+    return {"value": frame_rays * args.samples * steps / el, "unit": "ray-samples/s",
+            "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": "fp16",
+            "roofline": roof,
+            "vs_fp32_full_frame": frame_accuracy(got.cpu(), want.cpu(), hit.cpu(), rhit.cpu(),
+                                                 t.cpu(), rt.cpu())}
 
 
 def make_step(render, rows, size, rank, world, tile_rows, device, channels=4):
@@ -415,56 +488,104 @@ def _time_frames(render, steps, warmup, kernels):
 
 
 def extra_legs(scene, cameras, size, args, rows):
-    """The same frame at the reference's precision (FP32: every MLP on exact-f32 MFMA, the
-    1e-4 parity path) and without the 130-eval coarse scan (SURVEY §8d cfg2 asks for both)."""
+    """The same frame at the reference's precision when the headline ran FP16 (FP32: every MLP
+    on exact-f32 MFMA, the 1e-4 parity path), and without the 130-eval coarse scan (SURVEY §8d
+    cfg2 asks for both)."""
     import neural_raytracing_amd as nra
     from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
     from neural_raytracing_amd.pathtracer.render import RowRenderer
     out = {}
     S = args.samples
     frame_rays = len(rows) * size * len(cameras)
-    # FP32 leg: k_march32 (exact-f32 MFMA march + scan on the LDS ring) on the 157.3 TF FP32
-    # matrix peak
-    from neural_raytracing_amd import _lib
-    nra.set_precision("fp32")
-    rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
-                     size, rows, background=0.0, with_noise=1e-3, device=cameras.cam_to_world.device)
-    steps = 2
-    el, ks, evals = _time_frames(rr.render, steps, 1, ["k_march32", "k_intersect"])
-    k_ms = ks["k_march32"][0] / max(ks["k_march32"][1], 1)
-    flop = frame_rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256  # march + scan launch
-    ach = flop / (k_ms * 1e-3) / 1e12
-    exe = (evals - frame_rays) * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
-    out["fp32"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
-                   "ms_per_step": 1000 * el / steps, "steps": steps,
-                   "roofline": {"bound": "mfma", "kernel": "k_march32", "achieved": ach,
-                                "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
-                                "frac": ach / PEAK_TFLOPS["fp32"], "avg_kernel_ms": k_ms,
-                                "flop_per_launch": flop, "executed_frac": exe / PEAK_TFLOPS["fp32"],
-                                "intersect_ms": ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)}}
-    nra.set_precision(args.precision)
+    dev = cameras.cam_to_world.device
+    if args.precision != "fp32":
+        nra.set_precision("fp32")
+        rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"],
+                         scene["bsdf"], size, rows, background=0.0, with_noise=1e-3, device=dev)
+        steps = 2
+        el, ks, evals = _time_frames(rr.render, steps, 1, ["k_march32", "k_intersect"])
+        out["fp32"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
+                       "ms_per_step": 1000 * el / steps, "steps": steps,
+                       "roofline": march_roofline("k_march32", "fp32", frame_rays, S,
+                                                  *ks["k_march32"], evals, size)}
+        nra.set_precision(args.precision)
     # scan-free leg: Direct with training = False (the reference's Path / primary=False march)
+    kernel = "k_march16" if args.precision == "fp16" else "k_march32"
     direct = Direct()
     direct.training = False
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, NeRFIntegrator(direct),
-                     scene["bsdf"], size, rows, background=0.0, with_noise=1e-3,
-                     device=cameras.cam_to_world.device)
+                     scene["bsdf"], size, rows, background=0.0, with_noise=1e-3, device=dev)
     steps = 3
-    el, ks, evals = _time_frames(rr.render, steps, 1, ["k_march16"])
-    k_ms = ks["k_march16"][0] / max(ks["k_march16"][1], 1)
+    el, ks, evals = _time_frames(rr.render, steps, 1, [kernel])
+    k_ms = ks[kernel][0] / max(ks[kernel][1], 1)
     flop = frame_rays * S * FLOP_SDF_8x256
     ach = flop / (k_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[args.precision]
     # without the scan a ray stops at its hit (or at max_t): the algorithmic count (every ray at
-    # every step, as the reference evaluates) is far above what the job lists execute
+    # every step, as the reference evaluates) is far above what the job lists execute, so the
+    # executed fraction is the utilisation figure here
     exe = evals * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
     out["scan_free"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                         "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": args.precision,
-                        "roofline": {"bound": "mfma", "kernel": "k_march16", "achieved": ach,
-                                     "peak": PEAK_TFLOPS[args.precision], "unit": "TFLOP/s",
-                                     "frac": ach / PEAK_TFLOPS[args.precision],
+                        "roofline": {"bound": "mfma", "kernel": kernel, "achieved": ach,
+                                     "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
                                      "avg_kernel_ms": k_ms, "flop_per_launch": flop,
-                                     "executed_frac": exe / PEAK_TFLOPS[args.precision],
-                                     "executed_evals_per_ray": evals / frame_rays}}
+                                     "executed_frac": exe / peak,
+                                     "executed_evals_per_ray": evals / frame_rays,
+                                     "note": "frac is algorithmic (every ray x 64 steps); "
+                                             "executed_frac is the utilisation"}}
+    return out
+
+
+def api_path_legs(scene, args, reps=3):
+    """The render calls the drivers make, timed through the public API:
+    test_nerf's pathtrace(size=256, chunk_size=256) (training_utils.py:323-329), test_dtu's
+    pathtrace(size=256, chunk_size=128) (training_utils.py:458-464) and the training step's
+    forward, pathtrace_sample of a 6-view 80x80 crop of 256^2 (training_utils.py:256-266,
+    nerf_synthetic.py), under torch.no_grad (the render path; training's autograd path is
+    --scene train).  Each: ray-samples/s over the wall time and the march kernel's time / frac."""
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd import _lib
+    pt = scene["pt"]
+    S = args.samples
+    prec = args.precision
+    kernel = "k_march16" if prec == "fp16" else "k_march32"
+    size = 256
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    dev = scene["shape"].device
+
+    def cam(n):
+        c2w = torch.stack([view_c2w(i, n) for i in range(n)]).to(dev)
+        return pt.cameras.NeRFCamera(cam_to_world=c2w, focal=focal, device=dev)
+
+    cases = [
+        ("test_nerf pathtrace(size=256, chunk_size=256)", cam(1), 256 * 256,
+         lambda c: pt.pathtrace(scene["shape"], scene["lights"], c, scene["integrator"],
+                                bsdf=scene["bsdf"], size=size, chunk_size=256, bundle_size=1,
+                                background=0, silent=True, device=dev)),
+        ("test_dtu pathtrace(size=256, chunk_size=128)", cam(1), 256 * 256,
+         lambda c: pt.pathtrace(scene["shape"], scene["lights"], c, scene["integrator"],
+                                bsdf=scene["bsdf"], size=size, chunk_size=128, bundle_size=1,
+                                background=0, silent=True, device=dev)),
+        ("train_nerf pathtrace_sample(6 views, crop 80 of 256, chunk_size=256) forward", cam(6),
+         6 * 80 * 80,
+         lambda c: pt.pathtrace_sample(scene["shape"], scene["lights"], c, scene["integrator"],
+                                       bsdf=scene["bsdf"], size=size, chunk_size=256,
+                                       bundle_size=1, crop_size=80, uv=(88, 88), background=0,
+                                       device=dev)),
+    ]
+    out = {}
+    with torch.no_grad():
+        for name, c, rays, fn in cases:
+            el, ks, evals = _time_frames(lambda: fn(c), reps, 1, [kernel])
+            k_ms, k_n = ks[kernel]
+            flop = rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
+            out[name] = {"value": rays * S * reps / el, "unit": "ray-samples/s",
+                         "ms_per_call": 1000 * el / reps, "rays": rays,
+                         "kernel": kernel, "kernel_launches_per_call": k_n / reps,
+                         "kernel_ms_per_call": k_ms / reps,
+                         "frac": flop / (k_ms / reps * 1e-3) / 1e12 / PEAK_TFLOPS[prec],
+                         "dtype": prec}
     return out
 
 
@@ -781,25 +902,6 @@ def rr_hit_fraction(rr):
     for b in R._BUFS.values():
         return b.hit.float().mean().item()
     return 0.0
-
-
-def psnr_vs_fp32(scene, cameras, size, crop=200):
-    """PSNR of the fp16 render against the fp32 render of a central crop (no camera jitter)."""
-    import neural_raytracing_amd as nra
-    pt = scene["pt"]
-    c0 = (size - crop) // 2
-    imgs = {}
-    for prec in ("fp32", "fp16"):
-        nra.set_precision(prec)
-        random.seed(123)
-        img, _ = pt.pathtrace_sample(scene["shape"], scene["lights"], single_camera(cameras),
-                                     scene["integrator"], bsdf=scene["bsdf"], size=size,
-                                     chunk_size=size, bundle_size=1, crop_size=crop, uv=(c0, c0),
-                                     background=0, with_noise=0.0)
-        imgs[prec] = img.clamp(0, 1)
-    nra.set_precision("fp16")
-    mse = ((imgs["fp16"] - imgs["fp32"]) ** 2).mean().item()
-    return -10 * math.log10(max(mse, 1e-12))
 
 
 def single_camera(cameras):

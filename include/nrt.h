@@ -348,17 +348,29 @@ int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
 int nrt_profile_evals(uint64_t* evals);
 
 /* ---------------------------------------------------------------------------------------
- * Diagnostic environment variables (A/B and schedule tests; none is set in normal use, and
- * each one only selects between two implementations that the parity tests hold to the same
- * oracle bar, or changes the grid size of a schedule-independent kernel):
- *   NRT_NO_RING       FP16 SDF march / normals on the per-wave kernels instead of the LDS ring
- *   NRT_NO_RING32     FP32 SDF march on the per-wave slab kernel k_intersect instead of k_march32
- *   NRT_F32_NORMALS   FP32 backward normals after an FP16 ring march (instead of k_normal16)
- *   NRT_MARCH_BLOCKS  persistent-grid size of the ring marches (results are bit-identical)
- *   NRT_NO_PROGRAM    FP16 shading MLPs per component instead of the fused program kernel
- *   NRT_NERF_UNFUSED  FP16 NeRFLE on separate MLP launches instead of k_nerfle16
- *   NRT_MAX_WAVES     waves per block (1..4) of the per-wave kernels
+ * Runtime options (no reference counterpart: the reference has one eager implementation).
+ * Process-wide, read when a call launches its kernels; the library reads no environment
+ * variables.  Each option selects between implementations that the parity tests hold to the
+ * same oracle bar, or sets a schedule that does not change results:
+ *   "ring16"        1  FP16 SDF march / normals on the LDS-ring engine (0: per-wave kernels)
+ *   "ring32"        1  FP32 SDF march on the FP32 ring engine k_march32 (0: per-wave k_intersect)
+ *   "normals16"     1  after an FP16 ring march, normals by FP16 forward mode (k_normal16);
+ *                      0: the FP32 backward (k_sdf_grad) -- FP32-accurate normals
+ *   "scan_best32"   1  FP16 primary march: the throughput -1000 sdf(best) (sdfs.py:137, 249) is
+ *                      evaluated by the FP32 engine (k_scan_best32) at the FP16 scan's argmin;
+ *                      0: by the FP16 engine (k_scan_best16) -- the x1000 logit amplifies FP16
+ *                      SDF error into alpha
+ *   "march_blocks"  0  persistent-grid size of the ring marches (0: every resident slot);
+ *                      results are bit-identical for every value
+ *   "shade_program" 1  FP16 shading MLPs in one fused program kernel (0: per component)
+ *   "nerf_fused"    1  FP16 NeRFLE in the fused k_nerfle16 (0: separate MLP launches)
+ *   "max_waves"     0  waves per block (1..4) of the per-wave kernels (0: 4)
+ * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
+int nrt_set_option(const char* name, int64_t value);
+int nrt_get_option(const char* name, int64_t* value);
+/* every option back to its default */
+int nrt_reset_options(void);
 
 #ifdef __cplusplus
 }

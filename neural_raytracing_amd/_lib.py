@@ -102,6 +102,9 @@ _SIGNATURES = {
     "nrt_profile_read": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_I64)]),
     "nrt_profile_evals": (_I32, [ctypes.POINTER(ctypes.c_uint64)]),
+    "nrt_set_option": (_I32, [ctypes.c_char_p, _I64]),
+    "nrt_get_option": (_I32, [ctypes.c_char_p, ctypes.POINTER(_I64)]),
+    "nrt_reset_options": (_I32, []),
     "nrt_composite": (_I32, [_P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F, _P, _I32, _I32, _I32,
                              _I32, _I32, _P]),
 }
@@ -174,6 +177,36 @@ def get_precision():
 
 def precision_code():
     return _precision["value"]
+
+
+def set_option(name, value):
+    """nrt_set_option (include/nrt.h "Runtime options"): select an implementation or schedule."""
+    check(load().nrt_set_option(name.encode(), int(value)), f"nrt_set_option({name})")
+
+
+def get_option(name):
+    v = ctypes.c_int64()
+    check(load().nrt_get_option(name.encode(), ctypes.byref(v)), f"nrt_get_option({name})")
+    return v.value
+
+
+class options:
+    """Context manager: ``with _lib.options(ring32=0): ...`` sets options and restores them."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
 
 
 def profile_enable(on=True, evals=False):

@@ -638,7 +638,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   hipStream_t st = (hipStream_t)stream;
   const size_t n = (size_t)P * S;
   char* ws = (char*)workspace;
-  if (precision == NRT_FP16 && std::getenv("NRT_NERF_UNFUSED") == nullptr &&
+  if (precision == NRT_FP16 && option(OPT_NERF_FUSED) != 0 &&
       nerf_fusable(first, second)) {
     if (!second->nerf_prog || second->nerf_first_serial != first->serial) {
       std::unique_ptr<nrt_prog> pr(new nrt_prog());

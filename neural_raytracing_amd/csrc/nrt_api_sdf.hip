@@ -195,9 +195,9 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   dim3 grid(ceil_div64(ceil_div64(P, 32), lp.waves)), block(64 * lp.waves);
   int rc0 = NRT_OK;
   // FP16 SDF MLPs of width 128/256 with F = 16/32 run the block-cooperative ring kernel
-  const bool ring16 = f16 && ring_supported(s) && std::getenv("NRT_NO_RING") == nullptr;
+  const bool ring16 = f16 && ring_supported(s) && option(OPT_RING16) != 0;
   // ... and FP32 SDF MLPs of those widths the FP32 ring kernel (refreshed training handles too)
-  const bool ring32 = !f16 && ring32_supported(s) && std::getenv("NRT_NO_RING32") == nullptr;
+  const bool ring32 = !f16 && ring32_supported(s) && option(OPT_RING32) != 0;
   if (ring16 || ring32) {
     ProfScope prof("k_intersect", st);
     auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
@@ -225,7 +225,7 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   if (int rc = check_launch("k_intersect")) return rc;
   // normals on hit rays: raw gradient, unit normal, p += 5 eps n.  FP16 ring SDFs use the
   // forward-mode kernel (8 rays per wave-evaluation), everything else the f32 backward.
-  if (ring16 && std::getenv("NRT_F32_NORMALS") == nullptr) {
+  if (ring16 && option(OPT_NORMALS16) != 0) {
     ProfScope prof("k_normal16", st);
     if (int rc = ring_normals(s, idx, cnt, P, raw_n, n, p, a->epsilon, st)) return rc;
   } else if (int rc = launch_grad(s, p, idx, cnt, P, raw_n, n, p, a->epsilon, ws, st)) {

@@ -109,7 +109,7 @@ int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, con
   for (auto* m : b->mlps) upd(m);
   // FP16: light field, spatial weights and NeuralBSDFs on the program engine when compiled for
   // their shapes (NRT_NO_PROGRAM keeps the per-wave register path)
-  if (f16 && std::getenv("NRT_NO_PROGRAM") == nullptr) {
+  if (f16 && option(OPT_SHADE_PROGRAM) != 0) {
     const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out, st);
     if (rc != NRT_EUNSUPPORTED) return rc;
   }

@@ -117,11 +117,11 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
   // The encoding gradient accumulates in gt: slot s of row r belongs to lane (r, (s >> 2) & 1)
   // in every accumulation pass (the MFMA output layout), so a lane only re-reads its own stores
   // until the fence before dL/dx.  The skip layers' act'(enc) reads the raw encoding back from
-  // Eraw, which this wave wrote above (row rr is always one of this wave's own rows).
-  if (!TILE) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  }
+  // Eraw, which this wave wrote above (row rr is always one of this wave's own rows) -- other
+  // lanes' stores, so the fence orders them in both variants (the TILE variant's earlier fence
+  // precedes the Eraw stores and does not cover them).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   const float* eraw_row = Eraw + rr * dp;
   for (int s = 4 * h; s < ke; s += 8)
 #pragma unroll

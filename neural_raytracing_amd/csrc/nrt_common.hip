@@ -1,6 +1,7 @@
 // nrt_common.hip -- error state and library identity
 #include "nrt_launch.h"
 
+#include <atomic>
 #include <vector>
 
 namespace nrt {
@@ -15,6 +16,26 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 int max_hidden(const nrt_mlp* m) { return m ? m->desc.hidden : 0; }
+
+// nrt_set_option table: name, default
+struct OptionDef {
+  const char* name;
+  int64_t def;
+};
+static const OptionDef kOptions[OPT_COUNT] = {
+    {"ring16", 1}, {"ring32", 1}, {"normals16", 1}, {"scan_best32", 1},
+    {"march_blocks", 0}, {"shade_program", 1}, {"nerf_fused", 1}, {"max_waves", 0},
+};
+static std::atomic<int64_t> g_opts[OPT_COUNT] = {1, 1, 1, 1, 0, 1, 1, 0};
+
+int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
+
+static int option_index(const char* name) {
+  if (!name) return -1;
+  for (int i = 0; i < OPT_COUNT; ++i)
+    if (std::strcmp(kOptions[i].name, name) == 0) return i;
+  return -1;
+}
 
 struct ProfRec {
   std::string name;
@@ -96,6 +117,26 @@ int nrt_profile_read(const char* name, double* total_ms, int64_t* launches) {
   }
   if (total_ms) *total_ms = tot;
   if (launches) *launches = n;
+  return NRT_OK;
+}
+
+int nrt_set_option(const char* name, int64_t value) {
+  const int i = nrt::option_index(name);
+  if (i < 0) { set_error(std::string("nrt_set_option: unknown option ") + (name ? name : "(null)")); return NRT_EINVAL; }
+  if (value < 0) { set_error("nrt_set_option: negative value"); return NRT_EINVAL; }
+  nrt::g_opts[i].store(value, std::memory_order_relaxed);
+  return NRT_OK;
+}
+
+int nrt_get_option(const char* name, int64_t* value) {
+  const int i = nrt::option_index(name);
+  if (i < 0 || !value) { set_error("nrt_get_option: unknown option or null value"); return NRT_EINVAL; }
+  *value = nrt::g_opts[i].load(std::memory_order_relaxed);
+  return NRT_OK;
+}
+
+int nrt_reset_options(void) {
+  for (int i = 0; i < OPT_COUNT; ++i) nrt::g_opts[i].store(nrt::kOptions[i].def, std::memory_order_relaxed);
   return NRT_OK;
 }
 

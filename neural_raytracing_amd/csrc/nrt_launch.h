@@ -14,7 +14,19 @@
 
 namespace nrt {
 
-
+// Named runtime options (nrt_set_option, include/nrt.h): process-wide, read at launch time.
+enum Option {
+  OPT_RING16 = 0,      // "ring16"
+  OPT_RING32,          // "ring32"
+  OPT_NORMALS16,       // "normals16"
+  OPT_SCAN_BEST32,     // "scan_best32"
+  OPT_MARCH_BLOCKS,    // "march_blocks"
+  OPT_SHADE_PROGRAM,   // "shade_program"
+  OPT_NERF_FUSED,      // "nerf_fused"
+  OPT_MAX_WAVES,       // "max_waves"
+  OPT_COUNT
+};
+int64_t option(Option o);
 
 // compile-time hidden-block count for a runtime MLP width (32, 64, 96, 128, 256)
 #define NRT_NB_SWITCH(nbv, ...)                               \
@@ -37,15 +49,14 @@ struct LdsPlan {
   size_t bytes = 0;
 };
 
-static inline int env_max_waves() {
-  const char* s = std::getenv("NRT_MAX_WAVES");
-  int v = s ? std::atoi(s) : 4;
-  return v >= 1 && v <= 4 ? v : 4;
+static inline int opt_max_waves() {
+  const int64_t v = option(OPT_MAX_WAVES);
+  return v >= 1 && v <= 4 ? (int)v : 4;
 }
 
 static inline LdsPlan plan_lds(int hidden, int ke, int ys, bool f16, bool with_grad, int max_waves = 4) {
   LdsPlan p;
-  max_waves = std::min(max_waves, env_max_waves());
+  max_waves = std::min(max_waves, opt_max_waves());
   p.ys = std::max(ys, 1);
   p.RS = f16 ? 1 : slab_stride(std::max(hidden, 32), std::max(ke, 16), with_grad);
   p.per_wave = wave_lds_floats(p.RS, p.ys, f16);
@@ -155,6 +166,9 @@ inline bool ring32_supported(const nrt_sdf* s) {
 int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                  uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                  int32_t* cnt, unsigned long long* keys, hipStream_t st);
+// k_scan_best32 alone: thr = -1000 sdf(best) on the FP32 engine at the argmins in keys
+int ring_scan_best32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                     float* thr, unsigned long long* keys, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
 inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,

@@ -12,6 +12,9 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
   NRT_HIP(hipGetDevice(&dev));
   NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const bool scan = ma.primary != 0;
+  // option "scan_best32": sdf(best) on the FP32 engine -- the throughput -1000 sdf(best)
+  // (sdfs.py:137) multiplies the FP16 SDF error by 1000 in the alpha logit
+  const bool best32 = scan && option(OPT_SCAN_BEST32) != 0 && ring32_supported(s);
   if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   int rc = ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
     auto launch = [&](auto kern, const char* name) -> int {
@@ -22,18 +25,20 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
       // persistent grid: every resident block slot, but no more waves than 32-ray tiles
       const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 32 * kRingWaves)));
-      // NRT_MARCH_BLOCKS: force the grid (tests check that results do not depend on the schedule)
-      if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
+      // option "march_blocks": force the grid (tests check that results do not depend on the schedule)
+      if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
           s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, thr, keys);
       return check_launch(name);
     };
     if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
-    if (scan) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
+    if (scan && !best32) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
     return NRT_OK;
   });
   if (rc) return rc;
+  if (best32)
+    if (int rc2 = ring_scan_best32(s, rays, P, ma, thr, keys, st)) return rc2;
   if (idx) {
     k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
     if (int rc2 = check_launch("k_hit_list")) return rc2;

@@ -5,16 +5,18 @@
 
 namespace nrt {
 
-int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
-                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
-                 int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+// which = 0: march + scan (k_march32, then k_scan_best32 when primary); 1: k_scan_best32 alone
+// at the argmins already in `keys` (an FP16 march's scan, option "scan_best32")
+static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                         float* t, uint8_t* hit, float* p, float* n, float* raw_n, float* thr,
+                         unsigned long long* keys, hipStream_t st, int which) {
   const MlpDev& md = s->mlp->host_dev;
   const size_t extra = (size_t)md.freqs * 16 + ring32_bias_bytes(s) + ring32_sphere_bytes(s);
   int dev = 0, cus = 0;
   NRT_HIP(hipGetDevice(&dev));
   NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const bool scan = ma.primary != 0;
-  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
+  if (scan && which == 0) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   auto run = [&]<int KH, int KE, int ACT>() -> int {
     constexpr int WV = kRing32Waves;
     auto launch = [&](auto kern, const char* name) -> int {
@@ -24,13 +26,14 @@ int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
       NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WV, lds));
       const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * WV)));
-      if (const char* e = std::getenv("NRT_MARCH_BLOCKS")) blocks = std::max(1, std::atoi(e));
+      if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, p, n,
                                                      raw_n, thr, keys);
       return check_launch(name);
     };
-    if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32")) return rc;
+    if (which == 0)
+      if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32")) return rc;
     if (scan) return launch(k_scan_best32<KH, KE, WV, ACT>, "k_scan_best32");
     return NRT_OK;
   };
@@ -46,7 +49,18 @@ int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
     return NRT_EINVAL;
   }
 #undef NRT_R32
-  if (rc) return rc;
+  return rc;
+}
+
+int ring_scan_best32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                     float* thr, unsigned long long* keys, hipStream_t st) {
+  return ring32_launch(s, rays, P, ma, nullptr, nullptr, nullptr, nullptr, nullptr, thr, keys, st, 1);
+}
+
+int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                 int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+  if (int rc = ring32_launch(s, rays, P, ma, t, hit, p, n, raw_n, thr, keys, st, 0)) return rc;
   if (idx) {
     k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
     if (int rc2 = check_launch("k_hit_list")) return rc2;

@@ -21,8 +21,9 @@ def rand_uv(w, h, size):
     return random.randint(0, w - size), random.randint(0, h - size)
 
 
-def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, with_noise, device):
-    if hasattr(cameras, "rays_tile"):
+def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, with_noise, device,
+               positions=False):
+    if hasattr(cameras, "rays_tile") and not positions:
         return cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise)
     gx, gy = torch.meshgrid(torch.arange(x0, x0 + chunk, device=device, dtype=torch.float),
                             torch.arange(y0, y0 + chunk, device=device, dtype=torch.float),
@@ -32,10 +33,16 @@ def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, w
                                     with_noise=with_noise)
 
 
-def _composite(out, values, mask, background, xs, ys, chunk):
+def _composite(out, values, mask, background, xs, ys, chunk, trim=0):
     valid = mask.any(dim=-1)
     v = torch.mean(values, dim=-2)
     v[~valid] = background
+    if trim:
+        # the tile was rendered with a `trim`-pixel border; keep its interior.  The reference
+        # writes this as v[trim:-trim, trim:-trim] (main.py:52), which slices v's camera and row
+        # axes ([N, W, H, C]) -- a shape error at the assignment for every trim > 0 -- so the
+        # intended crop of the two pixel axes is what runs here.
+        v = v[:, trim:-trim, trim:-trim]
     out[:, xs:xs + chunk, ys:ys + chunk, :] = v
 
 
@@ -51,9 +58,10 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
               chunk_size=32, bundle_size=4, background=1, addition=nothing, sampler=Sampler(),
               silent=False, trim=0, device="cuda", squeeze_first=True, w_isect=False,
               with_noise=1e-3):
-    """main.py:13-93."""
-    if trim != 0:
-        raise NotImplementedError("pathtrace(trim != 0) is not supported on the HIP path")
+    """main.py:13-93.  trim > 0 renders each tile with a trim-pixel border of extra rays
+    (main.py:67-68) and keeps the tile's interior (see _composite)."""
+    if trim < 0:
+        raise ValueError("trim must be >= 0")
     batch_dims = len(cameras)
     if width is None:
         width = size
@@ -66,7 +74,7 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     xs = list(range(0, width, chunk_size))
     ys = list(range(0, height, chunk_size))
     it = None
-    fused = _fused(integrator, cameras, w_isect, addition)
+    fused = _fused(integrator, cameras, w_isect, addition) if trim == 0 else None
     if needs_grad(shapes, bsdf, lights):
         fused = None  # training: integrator.sample carries the gradients
     if getattr(lights, "per_camera", lambda: None)() is not None:
@@ -78,11 +86,11 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
             render_tile(fused, shapes, lights, cameras, bsdf, out, x0, y0, chunk_size, size,
                         with_noise, background)
             continue
-        rays = _tile_rays(cameras, x0, y0, chunk_size, size, sampler, bundle_size, batch_dims,
-                          with_noise, device)
+        rays = _tile_rays(cameras, x0 - trim, y0 - trim, chunk_size + 2 * trim, size, sampler,
+                          bundle_size, batch_dims, with_noise, device, positions=bool(trim))
         values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
                                              sampler=sampler, w_isect=w_isect)
-        _composite(out, values, mask, background, x0, y0, chunk_size)
+        _composite(out, values, mask, background, x0, y0, chunk_size, trim)
     if squeeze_first and batch_dims == 1:
         out = out.squeeze(0)
     return out, addition(it)

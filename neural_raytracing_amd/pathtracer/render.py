@@ -181,17 +181,26 @@ class RowGather:
 
 
 _GATHERS = {}
+_GATHERS_MAX = 4  # RowGathers (each holds world x slab staging buffers) kept, least recent out
+
+
+def clear_gathers():
+    """Drop the cached RowGathers (call after destroy_process_group)."""
+    _GATHERS.clear()
 
 
 def gather_rows(local, size, rank, world, tile_rows, out=None, group=None):
     """All-gather every rank's row slab ([N, R_rank, W, C]) and assemble [N, size, W, C]
-    (a cached RowGather per frame shape / device / group)."""
+    (a RowGather per frame shape / device / group from a small LRU; a caller that renders many
+    shapes should own its RowGather, as bench.make_step does)."""
     N, _, W, C = local.shape
     key = (size, rank, world, tile_rows, N, W, C, local.device, local.dtype, group)
-    g = _GATHERS.get(key)
+    g = _GATHERS.pop(key, None)
     if g is None:
-        g = _GATHERS[key] = RowGather(size, rank, world, tile_rows, (N, W, C), local.device,
-                                      local.dtype, group)
+        g = RowGather(size, rank, world, tile_rows, (N, W, C), local.device, local.dtype, group)
+    _GATHERS[key] = g  # most recent last
+    while len(_GATHERS) > _GATHERS_MAX:
+        _GATHERS.pop(next(iter(_GATHERS)))
     if out is None:
         out = local.new_empty(N, size, W, C)
     return g(local, out)
@@ -203,23 +212,18 @@ def broadcast_module(module, src=0, group=None):
     replicated before the row-sharded render, so every shard is rendered by the same weights.
     Tensors are coalesced by dtype into one flat broadcast each (no per-parameter collective)."""
     import torch.distributed as dist
-    tensors = [t for t in list(module.parameters()) + list(module.buffers())]
-    # basis_p and other plain tensor attributes of the package's MLPs are not buffers
-    for m in module.modules():
-        for v in vars(m).values():
-            if isinstance(v, torch.Tensor) and not isinstance(v, torch.nn.Parameter):
-                tensors.append(v)
-    seen, uniq = set(), []
-    for t in tensors:
-        if id(t) not in seen:
-            seen.add(id(t))
-            uniq.append(t)
+    uniq = _module_tensors(module)
+    # an NCCL (RCCL) group moves device tensors only: CPU tensors (e.g. PointLights' falloff
+    # coefficients) are staged through the current device and copied back
+    stage = dist.get_backend(group) == "nccl"
     by_dtype = {}
     for t in uniq:
         by_dtype.setdefault((t.dtype, t.device), []).append(t)
     with torch.no_grad():
         for (dtype, device), ts in by_dtype.items():
             flat = torch.cat([t.reshape(-1) for t in ts])
+            if stage and flat.device.type != "cuda":
+                flat = flat.to(torch.device("cuda", torch.cuda.current_device()))
             dist.broadcast(flat, src=src, group=group)
             off = 0
             for t in ts:
@@ -227,3 +231,31 @@ def broadcast_module(module, src=0, group=None):
                 t.copy_(flat[off:off + n].view_as(t))
                 off += n
     return module
+
+
+def _module_tensors(obj):
+    """Every tensor that defines `obj`'s render: parameters, buffers and plain tensor attributes
+    (basis_p of the MLPs) of an nn.Module tree; for an SDF shape (shapes.SDF, a plain class
+    with parameters() only, sdfs.py:89-109) those of its ``sdf`` module (SPHERE_SDF has none);
+    for any other object its parameters()."""
+    if not isinstance(obj, torch.nn.Module):
+        inner = getattr(obj, "sdf", None)
+        if isinstance(inner, torch.nn.Module):
+            return _module_tensors(inner)
+        params = getattr(obj, "parameters", None)
+        return _uniq(list(params()) if params is not None else [])
+    tensors = list(obj.parameters()) + list(obj.buffers())
+    for m in obj.modules():
+        for v in vars(m).values():
+            if isinstance(v, torch.Tensor) and not isinstance(v, torch.nn.Parameter):
+                tensors.append(v)
+    return _uniq(tensors)
+
+
+def _uniq(tensors):
+    seen, uniq = set(), []
+    for t in tensors:
+        if id(t) not in seen:
+            seen.add(id(t))
+            uniq.append(t)
+    return uniq

@@ -41,12 +41,17 @@ def _alias_pathtracer():
 pathtracer = _alias_pathtracer()
 
 
-def _register_safe_globals():
-    """Let the drivers' ``torch.load("models/*_bsdf.pt")`` / ``*_lights.pt`` (dtu.py:100, :108)
-    rebuild pickled modules under torch's default ``weights_only=True`` loader, which constructs
-    only allow-listed classes and executes nothing else from the file: this package's modules,
-    under their own and the reference's module paths, plus the torch modules and activation
-    functions those pickles reference."""
+def safe_global_entries():
+    """The allow-list for torch's ``weights_only=True`` unpickler: exactly the module classes a
+    driver pickle of a BSDF / light / SDF holds (dtu.py:100, :108 ``torch.load`` them), under
+    this package's and the reference's module paths, plus the torch layers and the pure
+    activation functions those modules keep as attributes (neural_blocks.py:26, sdfs.py:29).
+
+    Only ``nn.Module`` subclasses are listed (the unpickler rebuilds them with ``__new__`` +
+    ``__setstate__``, running none of their code) plus three pure element-wise activation
+    functions, never another free function of the package: the
+    weights_only unpickler calls any allow-listed callable with arguments the file chooses, so a
+    function such as ``utils.save_image`` on the list would let a crafted ``.pt`` write files."""
     import inspect
 
     import torch
@@ -59,14 +64,28 @@ def _register_safe_globals():
         for attr, obj in vars(mod).items():
             if getattr(obj, "__module__", None) != mod.__name__:
                 continue
-            if inspect.isclass(obj) or inspect.isfunction(obj):
+            if inspect.isclass(obj) and issubclass(obj, nn.Module):
                 alias = _DST + name[len(_SRC):] + "." + attr
                 entries += [obj, (obj, alias)]
+    # the package's pure element-wise functions that modules keep as attributes: SkipConnMLP's
+    # default activation (neural_blocks.py:26) and the BSDF preprocessors (bsdfs.py:80-96)
+    from neural_raytracing_amd.pathtracer import neural_blocks
+    from neural_raytracing_amd.pathtracer.bsdf import bsdfs
+    for fn, mod in ((neural_blocks._leaky, "neural_blocks"), (bsdfs.identity, "bsdf.bsdfs"),
+                    (bsdfs.identity_div_pi, "bsdf.bsdfs")):
+        entries += [fn, (fn, f"{_DST}.{mod}.{fn.__name__}")]
     entries += [nn.Linear, nn.ModuleList, nn.Sequential, nn.Softplus, nn.Sigmoid, nn.LeakyReLU,
                 nn.ReLU, nn.Tanh, nn.Identity, nn.Parameter, F.softplus, F.leaky_relu, F.relu,
                 torch.sigmoid, torch.relu, torch.tanh]
+    return entries
+
+
+def _register_safe_globals():
+    """Registered process-wide at import (not only inside ``model_io.load``, which has its own
+    restricted unpickler) because the drivers call ``torch.load`` themselves."""
+    import torch
     try:
-        torch.serialization.add_safe_globals(entries)
+        torch.serialization.add_safe_globals(safe_global_entries())
     except Exception:  # noqa: BLE001 -- an older torch without the allow-list: nothing to do
         pass
 

@@ -27,3 +27,12 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _reset_nrt_options(request):
+    """GPU tests switch implementations through nrt_set_option; put every option back after."""
+    yield
+    if "gpu" in request.keywords and gpu_available():
+        from neural_raytracing_amd import _lib
+        _lib.load().nrt_reset_options()

@@ -30,3 +30,10 @@ def product_mlp_like(src, activation):
 def seeded(seed=0):
     torch.manual_seed(seed)
     random.seed(seed)
+
+
+def lib_opt(name, value):
+    """nrt_set_option (include/nrt.h): the GPU tests' implementation / schedule switches; the
+    conftest fixture resets every option after each GPU test."""
+    from neural_raytracing_amd import _lib
+    _lib.set_option(name, value)

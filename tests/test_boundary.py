@@ -224,3 +224,61 @@ def test_broadcast_module_gloo_world2():
     rank, in place (version counters move, so packed handles are rebuilt)."""
     res = _spawn(_broadcast_worker, 2)
     assert res == {0: (True, True), 1: (True, True)}
+
+
+def _bench_scene_broadcast_worker(rank, world, port, q):
+    """bench.py's multi-GPU branch broadcasts its real scene objects -- the SDF shape
+    (a plain class with parameters() only), the BSDF and the lights, including a PointLights
+    whose falloff tensors stay on the host."""
+    import torch.distributed as dist
+    import bench
+    from neural_raytracing_amd.pathtracer.render import _module_tensors, broadcast_module
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    dev = torch.device("cpu")
+    scene = bench.build_scene(dev, 64, seed=10 + rank)  # every rank a different scene
+    other = bench.build_other_scene("colocate", dev, 64)
+    with torch.no_grad():
+        for t in _module_tensors(other["lights"]):
+            t.add_(rank)
+    objs = [scene["shape"], scene["bsdf"], scene["lights"], other["lights"], other["shape"]]
+    for o in objs:
+        broadcast_module(o)
+    flat = torch.cat([t.reshape(-1).float() for o in objs for t in _module_tensors(o)])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    q.put((rank, (flat.numel() > 1_000_000, all(torch.equal(g, gathered[0]) for g in gathered))))
+    dist.destroy_process_group()
+
+
+def test_broadcast_bench_scene_gloo_world2():
+    res = _spawn(_bench_scene_broadcast_worker, 2)
+    assert res == {0: (True, True), 1: (True, True)}
+
+
+def test_runtime_options_roundtrip():
+    """nrt_set_option / nrt_get_option / nrt_reset_options (include/nrt.h "Runtime options"):
+    named, validated, restored -- the library reads no environment variables."""
+    import os
+    from neural_raytracing_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libnrt_hip.so not built")
+    lib = _lib.load()
+    names = ["ring16", "ring32", "normals16", "scan_best32", "march_blocks", "shade_program",
+             "nerf_fused", "max_waves"]
+    defaults = {n: _lib.get_option(n) for n in names}
+    assert defaults == {"ring16": 1, "ring32": 1, "normals16": 1, "scan_best32": 1,
+                        "march_blocks": 0, "shade_program": 1, "nerf_fused": 1, "max_waves": 0}
+    with _lib.options(march_blocks=5, ring32=0):
+        assert _lib.get_option("march_blocks") == 5 and _lib.get_option("ring32") == 0
+    assert _lib.get_option("march_blocks") == 0 and _lib.get_option("ring32") == 1
+    with pytest.raises(_lib.NrtError):
+        _lib.set_option("no_such_option", 1)
+    with pytest.raises(_lib.NrtError):
+        _lib.set_option("ring16", -1)
+    _lib.set_option("normals16", 0)
+    assert lib.nrt_reset_options() == 0
+    assert _lib.get_option("normals16") == 1
+    src = open(os.path.join(os.path.dirname(_lib.HERE), "include", "nrt.h")).read()
+    for n in names:
+        assert f'"{n}"' in src

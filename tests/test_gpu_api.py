@@ -1,0 +1,98 @@
+"""Round-3 API items on the GPU, against the oracle or against the API's own untrimmed /
+un-optioned result:
+
+* ``pathtrace(trim > 0)`` (main.py:52, 67-68): every tile rendered with a trim-pixel border and
+  cropped back gives the untrimmed image (rays are per pixel, so the interior is unchanged);
+* option ``scan_best32`` (include/nrt.h "Runtime options"): on the FP16 march, the throughput
+  -1000 sdf(best) (sdfs.py:137, 249) evaluated by the FP32 engine -- the FP16 SDF error the x1000
+  logit amplifies into alpha drops, and the flip / depth statistics do not change.
+"""
+import math
+import random
+
+import pytest
+import torch
+
+import bench
+from oracle import pathtracer_ref as R
+from tests.helpers import lib_opt as _lib_opt
+from tests.report import report
+from tests.test_gpu_configs import _camera_rays, _mlp_sdf_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _fp32():
+    from neural_raytracing_amd import set_precision
+    set_precision("fp32")
+    yield
+    set_precision("fp32")
+
+
+@pytest.mark.parametrize("trim", [1, 3])
+def test_pathtrace_trim_matches_untrimmed(trim):
+    scene = bench.build_scene("cuda", samples=32, seed=3)
+    pt = scene["pt"]
+    size = 64
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    cam = pt.cameras.NeRFCamera(cam_to_world=bench.view_c2w(0, 1).unsqueeze(0).cuda(), focal=focal)
+    imgs = []
+    for tr in (0, trim):
+        random.seed(11)
+        with torch.no_grad():
+            img, _ = pt.pathtrace(scene["shape"], scene["lights"], cam, scene["integrator"],
+                                  bsdf=scene["bsdf"], size=size, chunk_size=32, bundle_size=1,
+                                  background=0, with_noise=0.0, trim=tr, silent=True)
+        imgs.append(img.cpu())
+    assert imgs[0].shape == imgs[1].shape == (size, size, 4)
+    assert (imgs[0][..., 3] > 0.5).any() and (imgs[0][..., 3] < 0.5).any()
+    assert (imgs[0] - imgs[1]).abs().max().item() <= 1e-6
+
+
+def test_pathtrace_trim_negative_raises():
+    scene = bench.build_scene("cuda", samples=8, seed=3)
+    pt = scene["pt"]
+    cam = pt.cameras.NeRFCamera(cam_to_world=bench.view_c2w(0, 1).unsqueeze(0).cuda(), focal=50.0)
+    with pytest.raises(ValueError):
+        pt.pathtrace(scene["shape"], scene["lights"], cam, scene["integrator"], bsdf=scene["bsdf"],
+                     size=32, chunk_size=32, trim=-1)
+
+
+def test_fp16_scan_best32_cuts_throughput_error():
+    """The bare 8x256 MLP SDF (cfg2 / cfg4 kind) marched in FP16 with and without the FP32
+    sdf(best) pass, against the oracle's throughput."""
+    from neural_raytracing_amd import _lib, set_precision
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    ref, mine = _mlp_sdf_pair()
+    rays = _camera_rays(40, 3)
+    random.seed(12)
+    jit = random.random()
+    with torch.no_grad():
+        rit, rhit = R.MarchedSDF(sdf=lambda p: ref(p)[..., 0], max_steps=64).intersect(
+            rays, primary=True, jitter=jit)
+    want = rit.throughput.reshape(-1)
+    set_precision("fp16")
+    res = {}
+    for best32 in (0, 1):
+        _lib_opt("scan_best32", best32)
+        _lib.profile_enable(True)
+        _lib.profile_reset()
+        random.seed(12)
+        with torch.no_grad():
+            it, hit = SDF(sdf=mine, max_steps=64).intersect(rays.cuda(), primary=True)
+        n32 = _lib.profile_read("k_scan_best32")[1]
+        n16 = _lib.profile_read("k_scan_best16")[1]
+        _lib.profile_enable(False)
+        assert (n32, n16) == ((1, 0) if best32 else (0, 1))
+        err = (it.throughput.cpu().reshape(-1) - want).abs()
+        alpha_err = (torch.sigmoid(it.throughput.cpu().reshape(-1)) - torch.sigmoid(want)).abs()
+        res[best32] = (hit.cpu().reshape(-1), it.t.cpu().reshape(-1), err, alpha_err)
+        report(f"fp16_scan_best32[{best32}]", rays=err.numel(), thr_maxabs=err.max().item(),
+               thr_over_0p1=int((err > 0.1).sum()), alpha_maxabs=alpha_err.max().item(),
+               alpha_over_1e4=int((alpha_err > 1e-4).sum()))
+    # the march itself is the same FP16 march either way
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    e16, e32 = res[0][2], res[1][2]
+    assert int((e32 > 0.1).sum()) < int((e16 > 0.1).sum())
+    assert e32.median().item() < 0.25 * e16.median().item()

@@ -25,6 +25,7 @@ import bench
 from oracle import pathtracer_ref as R
 from tests.helpers import copy_mlp, product_mlp_like, seeded
 from tests.report import report
+from tests.helpers import lib_opt as _lib_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -277,7 +278,7 @@ def test_nerfle_256_depths_matches_oracle(prec, monkeypatch):
     from neural_raytracing_amd import set_precision
     from neural_raytracing_amd.pathtracer.lights import PointLights
     from neural_raytracing_amd.pathtracer.shapes import NeRFLE
-    monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
+    _lib_opt("nerf_fused", 1)
     seeded(37)
     ref = R.NeRFLERef(steps=256)
     mine = NeRFLE(device="cpu", steps=256)

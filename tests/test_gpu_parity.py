@@ -9,6 +9,7 @@ import torch.nn.functional as F
 from oracle import pathtracer_ref as R
 from oracle import recipes
 from tests.helpers import copy_mlp, product_mlp_like, seeded
+from tests.helpers import lib_opt as _lib_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -362,12 +363,12 @@ def test_fp16_normals_match_f32_backward(monkeypatch):
     out = {}
     for mode in ("f16", "f32"):
         if mode == "f32":
-            monkeypatch.setenv("NRT_F32_NORMALS", "1")
+            _lib_opt("normals16", 0)
         random.seed(5)
         with torch.no_grad():
             it, hit = SDF(sdf=mine, max_steps=48).intersect(rays, primary=True)
             out[mode] = (hit.clone(), it.raw_normals.clone(), it.n.clone(), it.p.clone())
-    monkeypatch.delenv("NRT_F32_NORMALS")
+    _lib_opt("normals16", 1)
     set_precision("fp32")
     h16, g16, n16, p16 = out["f16"]
     h32, g32, n32, p32 = out["f32"]
@@ -415,9 +416,9 @@ def test_program_shading_nerf_synthetic_scene(monkeypatch):
     _, n_light = _lib.profile_read("k_light16")
     _lib.profile_enable(False)
     assert n_bsdf >= 1 and n_light >= 1, "program shading path did not run"
-    monkeypatch.setenv("NRT_NO_PROGRAM", "1")
+    _lib_opt("shade_program", 0)
     regs = render()
-    monkeypatch.delenv("NRT_NO_PROGRAM")
+    _lib_opt("shade_program", 1)
     nra.set_precision("fp32")
     assert (prog - regs).abs().max() < 2e-3, (prog - regs).abs().max()
     # oracle (fp32 restatement) on the same crop
@@ -507,9 +508,9 @@ def test_ring_march_schedule_invariant(monkeypatch):
     outs = []
     for blocks in (None, "1", "5"):
         if blocks is None:
-            monkeypatch.delenv("NRT_MARCH_BLOCKS", raising=False)
+            _lib_opt("march_blocks", 0)
         else:
-            monkeypatch.setenv("NRT_MARCH_BLOCKS", blocks)
+            _lib_opt("march_blocks", int(blocks))
         random.seed(2)
         with torch.no_grad():
             it, hit = SDF(sdf=mine, max_steps=64).intersect(rays, primary=True)
@@ -772,10 +773,10 @@ def test_nerfle_matches_oracle(prec, monkeypatch):
     "fp16" runs the fused k_nerfle16 program kernel, "fp16-unfused" the per-MLP kernels."""
     from neural_raytracing_amd import set_precision
     if prec == "fp16-unfused":
-        monkeypatch.setenv("NRT_NERF_UNFUSED", "1")
+        _lib_opt("nerf_fused", 0)
         prec = "fp16"
     else:
-        monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
+        _lib_opt("nerf_fused", 1)
     from neural_raytracing_amd.pathtracer.lights import PointLights
     ref, mine = _nerfle_pair()
     g = torch.Generator().manual_seed(4)
@@ -805,7 +806,7 @@ def test_nerfle_depth_counts(prec, steps, monkeypatch):
     from neural_raytracing_amd import set_precision
     from neural_raytracing_amd.pathtracer.shapes import NeRFLE
     from neural_raytracing_amd.pathtracer.lights import PointLights
-    monkeypatch.delenv("NRT_NERF_UNFUSED", raising=False)
+    _lib_opt("nerf_fused", 1)
     seeded(31)
     ref = R.NeRFLERef(steps=steps)
     mine = NeRFLE(device="cpu", steps=steps)

@@ -4,8 +4,8 @@ the block's LDS ring.
 
 * against the oracle (sdfs.py:111-160, 232-249) on the configurations it serves: SphereSDF(n=128)
   + 8x128 F=32 shift (the training SDF), the bare 8x256 F=16 MLP SDF, leaky_relu shifts;
-* against the FP32 slab kernel k_intersect (NRT_NO_RING32=1) on the same inputs;
-* independent of the persistent grid's size (NRT_MARCH_BLOCKS);
+* against the FP32 slab kernel k_intersect (option ring32=0) on the same inputs;
+* independent of the persistent grid's size (option march_blocks);
 * after nrt_mlp_refresh (the training handle re-gathers stream32 on the device) the march equals a
   freshly packed handle's.
 FP32 bar: 1e-4 abs on rays whose hit flag and step count agree; flips reported and bounded.
@@ -21,6 +21,7 @@ import bench
 from oracle import pathtracer_ref as R
 from tests.helpers import copy_mlp, product_mlp_like, seeded
 from tests.report import report
+from tests.helpers import lib_opt as _lib_opt
 
 pytestmark = pytest.mark.gpu
 
@@ -31,8 +32,6 @@ def _fp32():
     set_precision("fp32")
     yield
     set_precision("fp32")
-    os.environ.pop("NRT_NO_RING32", None)
-    os.environ.pop("NRT_MARCH_BLOCKS", None)
 
 
 def _rays(n, seed, eye=(0.0, 0.1, 1.0), spread=0.9):
@@ -151,7 +150,7 @@ def test_ring32_bare_mlp_matches_slab_kernel():
     rays = _rays(40, 3)
     it, hit, n32 = _march(mine, rays)
     assert n32 >= 1
-    os.environ["NRT_NO_RING32"] = "1"
+    _lib_opt("ring32", 0)
     sit, shit, n32b = _march(mine, rays)
     assert n32b == 0
     _compare("ring32_vs_slab[bare 8x256]", it, hit, sit, shit)
@@ -167,7 +166,7 @@ def test_ring32_independent_of_grid_size():
     rays = _rays(24, 11, eye=(0.0, 0.2, 1.1))
     base, bh, _ = _march(mine, rays)
     for blocks in ("1", "5"):
-        os.environ["NRT_MARCH_BLOCKS"] = blocks
+        _lib_opt("march_blocks", int(blocks))
         it, h, _ = _march(mine, rays)
         assert torch.equal(h, bh)
         assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)
@@ -221,7 +220,7 @@ def test_ring32_ragged_ray_counts_match_slab_kernel(n):
     rays = torch.cat([o, d], -1)
     it, hit, n32 = _march(mine, rays)
     assert n32 >= 1
-    os.environ["NRT_NO_RING32"] = "1"
+    _lib_opt("ring32", 0)
     sit, shit, _ = _march(mine, rays)
     assert torch.isfinite(it.t).all() and torch.isfinite(it.throughput).all()
     _compare(f"ring32_ragged[{n}]", it, hit, sit, shit, flip_frac=max(0.005, 1.0 / n))

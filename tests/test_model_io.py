@@ -220,3 +220,33 @@ def test_loader_runs_nothing_from_the_file(tmp_path, ref_paths):
     assert not (tmp_path / "ran").exists()
     with pytest.raises(ValueError):
         model_io.to_module(obj["x"])
+
+
+class _WritesAFile:
+    """A crafted pickle whose reduce calls the package's save_image (a side-effecting function)."""
+
+    def __init__(self, path):
+        self.path = path
+
+    def __reduce__(self):
+        from neural_raytracing_amd.pathtracer.utils import save_image
+        return save_image, (self.path, torch.zeros(2, 2, 3))
+
+
+def test_weights_only_load_rejects_package_functions(tmp_path):
+    """the weights_only allow-list holds the package's module classes only -- a
+    pickle that calls utils.save_image must be refused, and no file written."""
+    import pytorch3d  # noqa: F401  -- registers the allow-list
+    from pytorch3d import safe_global_entries
+    from neural_raytracing_amd.pathtracer import utils
+    listed = [e[0] if isinstance(e, tuple) else e for e in safe_global_entries()]
+    assert utils.save_image not in listed
+    pure = {"_leaky", "identity", "identity_div_pi"}
+    assert all(isinstance(e, type) or getattr(e, "__module__", "").startswith("torch")
+               or e.__name__ in pure for e in listed)
+    target = tmp_path / "pwned.png"
+    f = tmp_path / "evil.pt"
+    torch.save(_WritesAFile(str(target)), f)
+    with pytest.raises(Exception):
+        torch.load(f, weights_only=True)
+    assert not target.exists()
