@@ -32,6 +32,7 @@ SCAN_EVALS = 130             # sdf(o) + 128 samples + sdf(best)
 # k_march16 evaluates the march and the 129 scan points; sdf(best) is k_scan_best16's
 MARCH_KERNEL_SCAN_EVALS = 129
 PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_TFLOPS["fp32-split"] = PEAK_TFLOPS["fp16"]  # its MFMA work runs on the FP16 matrix cores
 
 
 def parse():
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--samples", type=int, default=None,
                     help="march steps per ray (max_steps) or NeRF depths per ray "
                          "(default 64; 256 for --scene nerfle, BASELINE cfg5)")
-    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32"],
+    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32", "fp32-split"],
                     help="arithmetic of the headline frame (default fp32, the reference's; the "
                          "fp16 frame is reported as the `fp16` leg)")
     ap.add_argument("--tile-rows", type=int, default=10)
@@ -267,7 +268,7 @@ def main():
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
-        march_kernel = "k_march16" if args.precision == "fp16" else "k_march32"
+        march_kernel = MARCH_KERNEL[args.precision]
         k_ms, k_n = _lib.profile_read(march_kernel)
         i_ms, i_n = _lib.profile_read("k_intersect")
         evals = count_evals(step)
@@ -288,6 +289,7 @@ def main():
         extra["hit_fraction"] = round(hit_frac, 4)
         if not args.no_extra_legs:
             if args.precision == "fp32":
+                extra["fp32_split"] = split_leg(rr, args, rows, size)
                 extra["fp16"] = fp16_leg(rr, args, rows, size)
             extra.update(extra_legs(scene, cameras, size, args, rows))
             extra["api_paths"] = api_path_legs(scene, args)
@@ -329,16 +331,24 @@ def main():
         torch.distributed.destroy_process_group()
 
 
+MARCH_KERNEL = {"fp16": "k_march16", "fp32": "k_march32", "fp32-split": "k_march3"}
+
+
 def march_roofline(kernel, precision, rays, samples, k_ms, k_n, evals, size):
     """Roofline object of one march + scan launch: algorithmic FLOP = every ray at every march
     step and scan point (the reference's count, sdfs.py:119-131, 232-249) x the 8x256 MLP's FLOP
     per evaluation, over the launch's HIP-event duration; `executed_*` counts the evaluations the
-    job lists actually ran (device counter, one untimed frame) less the sdf(best) pass's."""
-    flop_launch = rays * (samples + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
+    job lists actually ran (device counter, one untimed frame) less the sdf(best) pass's.
+    fp32-split: the kernel issues 3 f16 MFMA products per f32 product, so the MFMA work is 3x
+    the algorithmic count, on the FP16 peak; fp32_equivalent_* is the algorithmic rate beside the
+    FP32 peak."""
+    split = precision == "fp32-split"
+    products = 3 if split else 1
+    flop_launch = rays * (samples + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256 * products
     avg_kernel_ms = k_ms / max(k_n, 1)
     achieved = flop_launch / (avg_kernel_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[precision]
-    exec_flop = (evals - rays) * FLOP_SDF_8x256
+    exec_flop = (evals - rays) * FLOP_SDF_8x256 * products
     exec_achieved = exec_flop / (avg_kernel_ms * 1e-3) / 1e12
     traffic, source = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
@@ -351,7 +361,7 @@ def march_roofline(kernel, precision, rays, samples, k_ms, k_n, evals, size):
                           f"WRITE_SIZE, {size}^2 {precision}); not measured in this run")
         except Exception:
             traffic = None
-    return {
+    out = {
         "bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
         "frac": achieved / peak, "traffic": traffic, "traffic_source": source,
         "flop_per_launch": flop_launch,
@@ -360,6 +370,13 @@ def march_roofline(kernel, precision, rays, samples, k_ms, k_n, evals, size):
         "executed_flop_per_launch": exec_flop, "executed_achieved": exec_achieved,
         "executed_frac": exec_achieved / peak, "avg_kernel_ms": avg_kernel_ms, "launches": k_n,
     }
+    if split:
+        out["flop_basis"] = ("MFMA work issued: 3 f16 products per f32 product (hi*hi, hi*lo, "
+                             "lo*hi) x the algorithmic count (every ray at every march step and "
+                             "scan point, sdfs.py:119-131, 232-249)")
+        out["fp32_equivalent_achieved"] = achieved / 3
+        out["fp32_equivalent_vs_fp32_peak"] = achieved / 3 / PEAK_TFLOPS["fp32"]
+    return out
 
 
 def _frame_state(rr, seed):
@@ -487,6 +504,36 @@ def _time_frames(render, steps, warmup, kernels):
     return elapsed, times, count_evals(render)
 
 
+def split_leg(rr, args, rows, size, steps=5, warmup=2):
+    """The same frame in the fp32-split precision (include/nrt.h NRT_FP32_SPLIT): the march +
+    coarse scan on k_march3 -- every SDF layer on v_mfma_f32_16x16x32_f16 with f32 operands
+    split into two f16 halves, three products per block, f32 accumulation -- everything else as
+    FP32.  Roofline: the MFMA work the kernel issues (3 x the algorithmic FLOP) on the 2.5 PF
+    FP16 peak; `fp32_equivalent_*` puts the algorithmic FLOP beside the 157.3 TF FP32 peak.
+    Compared over the whole frame with the FP32 frame of the same rays and weights."""
+    import neural_raytracing_amd as nra
+    with torch.no_grad():
+        want, rhit, rt = _frame_state(rr, 1234)
+        nra.set_precision("fp32-split")
+        try:
+            el, ks, evals = _time_frames(rr.render, steps, warmup,
+                                         ["k_march3", "k_intersect", "k_scan_best3"])
+            got, hit, t = _frame_state(rr, 1234)
+        finally:
+            nra.set_precision(args.precision)
+    frame_rays = len(rows) * size
+    roof = march_roofline("k_march3", "fp32-split", frame_rays, args.samples, *ks["k_march3"],
+                          evals, size)
+    roof["intersect_ms"] = ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)
+    roof["scan_best_ms"] = ks["k_scan_best3"][0] / max(ks["k_scan_best3"][1], 1)
+    return {"value": frame_rays * args.samples * steps / el, "unit": "ray-samples/s",
+            "ms_per_step": 1000 * el / steps, "steps": steps,
+            "dtype": "fp32-split (f32 operands as f16 hi + lo, 3 f16 MFMA products, f32 accumulate)",
+            "roofline": roof,
+            "vs_fp32_full_frame": frame_accuracy(got.cpu(), want.cpu(), hit.cpu(), rhit.cpu(),
+                                                 t.cpu(), rt.cpu())}
+
+
 def extra_legs(scene, cameras, size, args, rows):
     """The same frame at the reference's precision when the headline ran FP16 (FP32: every MLP
     on exact-f32 MFMA, the 1e-4 parity path), and without the 130-eval coarse scan (SURVEY §8d
@@ -510,7 +557,7 @@ def extra_legs(scene, cameras, size, args, rows):
                                                   *ks["k_march32"], evals, size)}
         nra.set_precision(args.precision)
     # scan-free leg: Direct with training = False (the reference's Path / primary=False march)
-    kernel = "k_march16" if args.precision == "fp16" else "k_march32"
+    kernel = MARCH_KERNEL[args.precision]
     direct = Direct()
     direct.training = False
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, NeRFIntegrator(direct),
@@ -518,13 +565,14 @@ def extra_legs(scene, cameras, size, args, rows):
     steps = 3
     el, ks, evals = _time_frames(rr.render, steps, 1, [kernel])
     k_ms = ks[kernel][0] / max(ks[kernel][1], 1)
-    flop = frame_rays * S * FLOP_SDF_8x256
+    products = 3 if args.precision == "fp32-split" else 1  # f16 MFMA products per f32 product
+    flop = frame_rays * S * FLOP_SDF_8x256 * products
     ach = flop / (k_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
     # without the scan a ray stops at its hit (or at max_t): the algorithmic count (every ray at
     # every step, as the reference evaluates) is far above what the job lists execute, so the
     # executed fraction is the utilisation figure here
-    exe = evals * FLOP_SDF_8x256 / (k_ms * 1e-3) / 1e12
+    exe = evals * FLOP_SDF_8x256 * products / (k_ms * 1e-3) / 1e12
     out["scan_free"] = {"value": frame_rays * S * steps / el, "unit": "ray-samples/s",
                         "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": args.precision,
                         "roofline": {"bound": "mfma", "kernel": kernel, "achieved": ach,
@@ -549,7 +597,7 @@ def api_path_legs(scene, args, reps=3):
     pt = scene["pt"]
     S = args.samples
     prec = args.precision
-    kernel = "k_march16" if prec == "fp16" else "k_march32"
+    kernel = MARCH_KERNEL[prec]
     size = 256
     focal = float(0.5 * size / math.tan(0.5 * 0.6911))
     dev = scene["shape"].device
@@ -579,7 +627,8 @@ def api_path_legs(scene, args, reps=3):
         for name, c, rays, fn in cases:
             el, ks, evals = _time_frames(lambda: fn(c), reps, 1, [kernel])
             k_ms, k_n = ks[kernel]
-            flop = rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256
+            flop = rays * (S + MARCH_KERNEL_SCAN_EVALS) * FLOP_SDF_8x256 * \
+                (3 if prec == "fp32-split" else 1)
             out[name] = {"value": rays * S * reps / el, "unit": "ray-samples/s",
                          "ms_per_call": 1000 * el / reps, "rays": rays,
                          "kernel": kernel, "kernel_launches_per_call": k_n / reps,

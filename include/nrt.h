@@ -15,9 +15,13 @@
  *     reference's [N, W, H, B] order.
  *   - Return value: 0 on success, negative NRT_E* on error; nrt_last_error() returns a
  *     thread-local message for the last failure on the calling thread.
- *   - precision: NRT_FP32 computes every MLP layer with exact-f32 MFMA (v_mfma_f32_32x32x2_f32)
- *     and matches the CPU restatement to ~1e-6; NRT_FP16 uses v_mfma_f32_32x32x16_f16 with f32
- *     accumulation (the throughput path, judged by PSNR against FP32).
+ *   - precision: NRT_FP32 computes every MLP layer with exact-f32 MFMA (v_mfma_f32_32x32x2_f32 /
+ *     16x16x4_f32) and matches the CPU restatement to ~1e-6; NRT_FP16 uses v_mfma_f32_32x32x16_f16
+ *     with f32 accumulation (the throughput path, judged by PSNR against FP32); NRT_FP32_SPLIT is
+ *     NRT_FP32 except that the SDF march + coarse scan of the ring-engine SDFs runs every layer on
+ *     v_mfma_f32_16x16x32_f16 with each f32 operand split into two f16 halves and three products
+ *     (hi*hi + hi*lo + lo*hi, f32 accumulation): FP32 accuracy (22-bit operands, fewer
+ *     accumulation roundings than an fma chain) at FP16 matrix-core throughput.
  */
 #ifndef NRT_H_
 #define NRT_H_
@@ -37,6 +41,7 @@ extern "C" {
 
 #define NRT_FP32 0
 #define NRT_FP16 1
+#define NRT_FP32_SPLIT 2
 
 /* activations (neural_blocks.py:26 leaky_relu default; sdfs.py:29 softplus) */
 #define NRT_ACT_LEAKY_RELU 0
@@ -138,7 +143,7 @@ typedef struct {
   float max_t;         /* intersect(max_t=10)                                              */
   int32_t primary;     /* 1: run the 128-step coarse scan (SDF.throughput, sdfs.py:232)     */
   double scan_max_t;   /* dist + random.random()*(2/128), computed by the caller           */
-  int32_t precision;   /* NRT_FP32 / NRT_FP16                                               */
+  int32_t precision;   /* NRT_FP32 / NRT_FP16 / NRT_FP32_SPLIT                              */
   int32_t* scan_index; /* optional [P] output: the coarse-scan argmin idxs (sdfs.py:243-246), so a
                           training caller can rebuild best_pos = o + idx*step*d; NULL = unused  */
 } nrt_march_params;

@@ -15,6 +15,8 @@ LIB_PATH = os.environ.get("NRT_LIB") or os.path.join(HERE, "libnrt_hip.so")
 
 NRT_FP32 = 0
 NRT_FP16 = 1
+NRT_FP32_SPLIT = 2
+_PRECISIONS = {"fp32": NRT_FP32, "fp16": NRT_FP16, "fp32-split": NRT_FP32_SPLIT}
 
 ACT = {"leaky_relu": 0, "softplus": 1, "none": 2, "sigmoid": 3, "relu": 4}
 
@@ -165,14 +167,16 @@ _precision = {"value": NRT_FP16 if os.environ.get("NRT_PRECISION", "fp32") == "f
 
 
 def set_precision(p):
-    """'fp32' (exact-f32 MFMA, parity with the reference) or 'fp16' (f16 MFMA, f32 accumulate)."""
-    if p not in ("fp32", "fp16"):
-        raise ValueError("precision must be 'fp32' or 'fp16'")
-    _precision["value"] = NRT_FP16 if p == "fp16" else NRT_FP32
+    """'fp32' (exact-f32 MFMA, parity with the reference), 'fp16' (f16 MFMA, f32 accumulate) or
+    'fp32-split' ('fp32', with the SDF march + scan at FP32 accuracy on FP16 MFMA: every operand
+    split into two f16 halves, three products; include/nrt.h NRT_FP32_SPLIT)."""
+    if p not in _PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}")
+    _precision["value"] = _PRECISIONS[p]
 
 
 def get_precision():
-    return "fp16" if _precision["value"] == NRT_FP16 else "fp32"
+    return {v: k for k, v in _PRECISIONS.items()}[_precision["value"]]
 
 
 def precision_code():

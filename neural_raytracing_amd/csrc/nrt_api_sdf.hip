@@ -76,6 +76,8 @@ int nrt_sdf_eval(const nrt_sdf* s, const float* p, int64_t M, float* out, int pr
   if (!s || M < 0) { set_error("nrt_sdf_eval: bad argument"); return NRT_EINVAL; }
   if (M == 0) return NRT_OK;
   if (!p || !out) { set_error("nrt_sdf_eval: null p / out"); return NRT_EINVAL; }
+  if (precision == NRT_FP32_SPLIT && ring3_supported(s) && option(OPT_RING32) != 0)
+    return ring_eval3(s, p, M, out, (hipStream_t)stream);
   const bool f16 = precision == NRT_FP16;
   int hidden, ke;
   sdf_dims(s, hidden, ke);
@@ -198,10 +200,13 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   const bool ring16 = f16 && ring_supported(s) && option(OPT_RING16) != 0;
   // ... and FP32 SDF MLPs of those widths the FP32 ring kernel (refreshed training handles too)
   const bool ring32 = !f16 && ring32_supported(s) && option(OPT_RING32) != 0;
+  // ... and the fp32-split precision the FP32-accurate FP16-MFMA engine (nrt_ring3.h)
+  const bool ring3 = ring32 && a->precision == NRT_FP32_SPLIT && ring3_supported(s);
   if (ring16 || ring32) {
     ProfScope prof("k_intersect", st);
     auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
     rc0 = ring16 ? ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
+        : ring3  ? ring_march3(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
                  : ring_march32(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
     if (!rc0 && ma.scan_idx) {
       k_keys_index<><<<dim3(ceil_div64(P, 256)), dim3(256), 0, st>>>(keys, P, ma.scan_idx);

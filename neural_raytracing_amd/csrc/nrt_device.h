@@ -85,6 +85,16 @@ struct MlpDev {
   const float4* stream32;
   int stream32_bytes;
   const float* bias32;             // [layer][bias16_stride], unfolded
+  // FP32-accurate split stream of the ring3 engine (nrt_ring3.h): every weight of layer l as
+  // W 2^s_l = hi + lo, two f16 (hi = RNE(W 2^s_l), lo = RNE(W 2^s_l - hi)), fragments of
+  // v_mfma_f32_16x16x32_f16 on 16-ray tiles in consumption order (nrt_internal.h ring3_walk);
+  // s_l puts the layer's largest |W| in [1, 2) so lo stays a normal f16 for all but the smallest
+  // weights.  bias3 = bias 2^s_l (the accumulator's initial value), scale3[l] = 2^-s_l.
+  const float4* stream3;
+  int stream3_bytes;
+  const float* bias3;              // [layer][bias16_stride]
+  float scale3[kMaxLin];
+  int ke3;                         // encoding slots padded to 32 (one f16 k-step)
 };
 
 // A shading "program": the MLPs one kernel evaluates per ray batch, concatenated into one

@@ -146,6 +146,37 @@ inline void ring32_walk(const std::vector<Ring32Layer>& ls, int H, int ke, F&& f
             }
   }
 }
+
+// Element order of the split stream (MlpDev::stream3, consumed by nrt_ring3.h with
+// v_mfma_f32_16x16x32_f16 on 16-ray tiles).  f(layer, row, pos, part) is called once per stream
+// half, in order (part 0 = hi, 1 = lo); pos as in ring32_walk (hidden feature k < H, or H +
+// encoding slot; rows past the layer's R are padding).
+//   chunk = 32 output rows (sub-blocks b = 0, 1 of 16) of one layer; the out layer is one chunk of
+//   one sub-block.  A chunk is k-steps u = 0 .. kh + kq - 1 (kh = H / 32 hidden, kq = ke3 / 32
+//   encoding k-steps), each [sub-block b][part][lane][e] = 1 KiB per (b, part): lane (g = lane >> 4,
+//   i = lane & 15) holds A[row 16 b + i][k = 8 g + e] of k-step u.  Hidden k-step u takes feature
+//   16 (2u + (e >> 2)) + 4 g + (e & 3) -- register e & 3 of sub-block 2u + (e >> 2) of the previous
+//   layer's 16x16 accumulators, which is chunk u of that layer -- and encoding k-step v takes slot
+//   32 v + 8 g + e.
+template <class F>
+inline void ring3_walk(const std::vector<Ring32Layer>& ls, int H, int ke3, F&& f) {
+  for (size_t l = 0; l < ls.size(); ++l) {
+    const bool out = l + 1 == ls.size();
+    const int nsub = out ? 1 : 2, nch = out ? 1 : (ls[l].R + 31) / 32;
+    const int kh = ls[l].hid ? H / 32 : 0, kq = ls[l].enc ? ke3 / 32 : 0;
+    for (int c = 0; c < nch; ++c)
+      for (int u = 0; u < kh + kq; ++u)
+        for (int b = 0; b < nsub; ++b)
+          for (int part = 0; part < 2; ++part)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e = 0; e < 8; ++e) {
+                const int g = lane >> 4;
+                const int pos = u < kh ? 16 * (2 * u + (e >> 2)) + 4 * g + (e & 3)
+                                       : H + 32 * (u - kh) + 8 * g + e;
+                f((int)l, 32 * c + 16 * b + (lane & 15), pos, part);
+              }
+  }
+}
 }  // namespace nrt
 
 #define NRT_HIP(call)                                         \

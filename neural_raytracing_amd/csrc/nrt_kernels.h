@@ -17,6 +17,7 @@
 #include <cmath>
 
 #include "nrt_internal.h"
+#include "nrt_ring3.h"
 
 namespace nrt {
 
@@ -432,6 +433,22 @@ struct RingPol32 {
   __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
 };
 
+// FP32-accurate evaluation on FP16 matrix cores (nrt_ring3.h, the "fp32-split" precision):
+// 16-ray tiles like RingPol32, torch-exact transcendentals, sphere blobs as in ring32
+template <int KH, int KQ, int WV, int ACT>
+struct RingPol3 {
+  static constexpr int RPW = 16, WAVES = WV;
+  using Eng = ring3::Engine<KH, KQ, WV>;
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds) {
+    E.init(m, s, lds, 4 * KQ);
+  }
+  __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
+    const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
+    return d + ring3::eval<KH, KQ, WV, ACT>(E, m, x, y, z);
+  }
+  __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
+};
+
 template <class Pol, int MODE>
 __device__ __forceinline__ void march_body(
     const SdfDev s, const MlpDev m, const float* __restrict__ rays, int64_t P, MarchArgs a,
@@ -517,10 +534,18 @@ __device__ __forceinline__ void march_body(
             }
           }
           ray = own.ray(k);
-          const float* rp = rays + ray * 6;
-          ox = rp[0]; oy = rp[1]; oz = rp[2]; dx = rp[3]; dy = rp[4]; dz = rp[5];
+          if (mode == 2) {  // point evaluation: `rays` holds [P, 3] points, sdf(p) -> thr_out
+            const float* pp = rays + ray * 3;
+            ox = pp[0]; oy = pp[1]; oz = pp[2];
+          } else {
+            const float* rp = rays + ray * 6;
+            ox = rp[0]; oy = rp[1]; oz = rp[2]; dx = rp[3]; dy = rp[4]; dz = rp[5];
+          }
           ended = false;
-          if (mode == 1) {
+          if (mode == 2) {
+            kind = 2;
+            idx = 0;
+          } else if (mode == 1) {
             kind = 2;
             idx = (int)(uint32_t)keys[ray];
           } else if (seg < 0) {
@@ -548,6 +573,8 @@ __device__ __forceinline__ void march_body(
       // scan point j: o + (step * j) dir (sdfs.py:241-245); sdf(best): o + (idx * step) dir
       if (kind == 1 && j == 0) {
         px = ox; py = oy; pz = oz;
+      } else if (mode == 2) {
+        px = ox; py = oy; pz = oz;
       } else {
         const float ts = kind == 1 ? (float)(a.step * (double)j) : __fmul_rn((float)idx, (float)a.step);
         px = __fadd_rn(ox, __fmul_rn(ts, dx));
@@ -573,7 +600,7 @@ __device__ __forceinline__ void march_body(
       }
       ++j;
     } else if (kind == 2) {
-      if (lane < RPW) thr_out[ray] = -1000.f * d;
+      if (lane < RPW) thr_out[ray] = mode == 2 ? d : -1000.f * d;
       ended = true;
     }
   }
@@ -604,6 +631,24 @@ __global__ void __launch_bounds__(64 * WV, 1) k_march32(NRT_MARCH_ARGS) {
 template <int KH, int KE, int WV, int ACT>
 __global__ void __launch_bounds__(64 * WV, 1) k_scan_best32(NRT_MARCH_ARGS) {
   march_body<RingPol32<KH, KE, WV, ACT>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+// fp32-split (FP32-accurate on FP16 MFMA): one block of WV waves per CU, two waves per SIMD
+template <int KH, int KQ, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_march3(NRT_MARCH_ARGS) {
+  march_body<RingPol3<KH, KQ, WV, ACT>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+template <int KH, int KQ, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_scan_best3(NRT_MARCH_ARGS) {
+  march_body<RingPol3<KH, KQ, WV, ACT>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+// sdf(p) of P points on the ring engines (nrt_sdf_eval: fp32-split and FP32 precision)
+template <int KH, int KQ, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_sdf_eval3(NRT_MARCH_ARGS) {
+  march_body<RingPol3<KH, KQ, WV, ACT>, 2>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+template <int KH, int KE, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_sdf_eval32r(NRT_MARCH_ARGS) {
+  march_body<RingPol32<KH, KE, WV, ACT>, 2>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 #undef NRT_MARCH_PASS
 #undef NRT_MARCH_ARGS

@@ -169,6 +169,18 @@ int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
 // k_scan_best32 alone: thr = -1000 sdf(best) on the FP32 engine at the argmins in keys
 int ring_scan_best32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
                      float* thr, unsigned long long* keys, hipStream_t st);
+// ---- fp32-split ring engine (nrt_ring_march3.hip, nrt_ring3.h): the ring32 configurations,
+// from a handle packed by nrt_mlp_create (a refreshed handle's split stream is not re-packed)
+constexpr int kRing3Waves = 8;
+inline bool ring3_supported(const nrt_sdf* s) {
+  if (!s->mlp || s->mlp->refreshed) return false;
+  const MlpDev& m = s->mlp->host_dev;
+  return ring32_supported(s) && (m.ke3 == 64 || m.ke3 == 96);
+}
+int ring_eval3(const nrt_sdf* s, const float* pts, int64_t M, float* out, hipStream_t st);
+int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                int32_t* cnt, unsigned long long* keys, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
 inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstring>
 #include <memory>
@@ -271,6 +272,37 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   std::vector<float> bias32(layers.size() * (size_t)bstride, 0.f);
   for (size_t l = 0; l < layers.size(); ++l)
     for (int r = 0; r < layers[l].R; ++r) bias32[l * bstride + r] = layers[l].b[r];
+  // ---- split stream (nrt_ring3.h): per layer a power-of-two scale 2^s with max|W| 2^s in
+  // [1, 2), then W 2^s = hi + lo in two RNE f16 halves
+  const int ke3 = (dp + 31) / 32 * 32;
+  std::vector<float> lscale(layers.size(), 1.f);
+  for (size_t l = 0; l < layers.size(); ++l) {
+    float mx = 0.f;
+    const Layer& ly = layers[l];
+    for (size_t i = 0; i < (size_t)ly.R * ly.C; ++i) mx = std::max(mx, std::fabs(ly.W[i]));
+    int e = 0;
+    if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &e);  // mx = f 2^e, f in [0.5, 1)
+    lscale[l] = std::ldexp(1.f, std::max(-64, std::min(64, 1 - e)));  // mx * scale in [1, 2)
+  }
+  std::vector<_Float16> stream3;
+  {
+    std::vector<Ring32Layer> rl;
+    for (const Layer& ly : layers) rl.push_back({ly.R, ly.hidden_in, ly.enc_in});
+    ring3_walk(rl, H, ke3, [&](int l, int row, int pos, int part) {
+      const Layer& ly = layers[l];
+      int col = -1;
+      if (pos < H) col = col_of_hidden(pos);
+      else if (pos - H < ke) col = col_of_slot(ly, pos - H);
+      const float w = wval(ly, row, col) * lscale[l];
+      const _Float16 hi = (_Float16)w;
+      stream3.push_back(part == 0 ? hi : (_Float16)(w - (float)hi));
+    });
+  }
+  std::vector<float> bias3(layers.size() * (size_t)bstride, 0.f);
+  for (size_t l = 0; l < layers.size(); ++l)
+    for (int r = 0; r < layers[l].R; ++r) bias3[l * bstride + r] = layers[l].b[r] * lscale[l];
+  size_t off_stream3 = blob.add(stream3.data(), stream3.size() * sizeof(_Float16));
+  size_t off_b3 = blob.add(bias3.data(), bias3.size() * sizeof(float));
   size_t off_stream32 = blob.add(stream32.data(), stream32.size() * sizeof(float));
   size_t off_b32 = blob.add(bias32.data(), bias32.size() * sizeof(float));
   size_t off_streamk = blob.add(streamk.data(), streamk.size() * sizeof(_Float16));
@@ -316,6 +348,11 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   md.stream32 = reinterpret_cast<const float4*>(base + off_stream32);
   md.stream32_bytes = (int)(stream32.size() * sizeof(float));
   md.bias32 = reinterpret_cast<const float*>(base + off_b32);
+  md.stream3 = reinterpret_cast<const float4*>(base + off_stream3);
+  md.stream3_bytes = (int)(stream3.size() * sizeof(_Float16));
+  md.bias3 = reinterpret_cast<const float*>(base + off_b3);
+  for (size_t l = 0; l < layers.size(); ++l) md.scale3[l] = 1.f / lscale[l];
+  md.ke3 = ke3;
   m->host_dev = md;
   NRT_HIP(hipMalloc(&m->dev, sizeof(MlpDev)));
   NRT_HIP(hipMemcpy(m->dev, &md, sizeof(MlpDev), hipMemcpyHostToDevice));

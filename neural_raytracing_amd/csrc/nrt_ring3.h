@@ -1,0 +1,300 @@
+// nrt_ring3.h -- the SDF MLP at FP32 accuracy on the FP16 matrix cores ("fp32-split" precision).
+//
+// gfx950 has no TF32/xf32 MFMA; its exact-f32 MFMA (v_mfma_f32_16x16x4_f32) runs at 1/16 of the
+// FP16 rate.  This engine evaluates the same GEMMs as the FP32 ring (nrt_device.h ring32) with
+// every operand split into two FP16 halves and three FP16 MFMAs per product block:
+//     W 2^s = Wh + Wl,  a = ah + al   (Wh = RNE_f16(W 2^s), Wl = RNE_f16(W 2^s - Wh); likewise a)
+//     acc  += Wh ah + Wh al + Wl ah     (v_mfma_f32_16x16x32_f16, f32 accumulation)
+//     z     = acc 2^-s                 (s per layer: max|W| 2^s in [1, 2), so Wl is a normal f16)
+// The halves carry 22 significant bits of each operand; the dropped Wl al term is 2^-22 of a
+// product and the split residuals 2^-23, while the accumulation rounds once per MFMA (24 times
+// per 256-input row instead of 256 fma roundings): the result is as close to the float64 value
+// as the FP32 fma chain's (tests/test_gpu_split.py measures both against float64).  Throughput:
+// 3 x 16 cycles per 16x16x32 block against 8 x 32 cycles for the same block on f32 MFMA.
+//
+// Layout is ring32's with K steps of 32: a wave owns 16 rays (lane (g = lane >> 4, j = lane & 15)
+// serves ray j, lane group g holds k = 8 g .. 8 g + 7 of each k-step); the 16x16 accumulator of
+// output sub-block b holds rows 16 b + 4 g + r of ray j in register r, so sub-blocks 2u, 2u + 1 of
+// a layer are k-step u of the next layer's B operand (the packer permutes W's columns to match,
+// nrt_internal.h ring3_walk) and activations never leave registers: per lane H / 16 f16 words for
+// the hi halves and as many for the lo halves (32 + 32 VGPRs at H = 256).  The weight stream
+// moves through a 2-slot LDS ring by LDS-DMA exactly as in ring32 (chunk = 32 output rows =
+// one k-step of the next layer: 2 sub-blocks x 2 halves x 1 KiB per k-step).
+#pragma once
+#include "nrt_device.h"
+
+namespace nrt {
+namespace ring3 {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+typedef _Float16 hv2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f4v mfma(const u4v& a, const u4v& b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b),
+                                                c, 0, 0, 0);
+}
+
+// (a, b) -> packed hi = RNE_f16(a, b) and lo = RNE_f16(a - hi.x, b - hi.y).  The remainders are
+// exact in f32 (hi holds a's top 11 bits); v_fma_mix_f32 reads hi's f16 half directly (one
+// instruction instead of a convert and a subtract).
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const hv2 h = {(_Float16)a, (_Float16)b};
+  const uint32_t hw = __builtin_bit_cast(uint32_t, h);
+  float ra, rb;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(ra) : "v"(hw), "v"(a));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(rb) : "v"(hw), "v"(b));
+  const hv2 l = {(_Float16)ra, (_Float16)rb};
+  hi = hw;
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// KH = H / 32 hidden k-steps, KQ = ke3 / 32 encoding k-steps
+template <int KH, int KQ, int WV>
+struct Engine {
+  static constexpr int MAXQ = 4 * (KH + KQ);            // largest chunk (a skip layer's), KiB
+  static constexpr int MAXL = (MAXQ + WV - 1) / WV;     // DMA pieces per wave per chunk
+  static constexpr int SLOTQ = MAXL * WV;
+  static constexpr int RING_BYTES = 2 * SLOTQ * 1024;
+  static constexpr int kOutOfRange = 0x40000000;
+  // LDS of one block: ring | basis (float4 per frequency) | biases | sphere table
+  static size_t lds_bytes(int F, size_t bias_bytes, size_t sphere_bytes) {
+    return RING_BYTES + (size_t)F * 16 + bias_bytes + sphere_bytes;
+  }
+  const float4* ring;
+  uint32_t ring_lds;
+  const float* lbias;
+  const float4* lbasis;
+  const float4* lspheres;   // [n][4] float4 (SdfDev layout), read by ring32::spheres_value16
+  const void* sbase;
+  int sbytes, bstride;
+  int off, next_off;        // piece offset of the current / next chunk in stream3 (wave-uniform)
+  int slot;
+  int lane, wv;
+
+  __device__ __forceinline__ void issue(int qoff, int nq, int s) {
+    const int w = __builtin_amdgcn_readfirstlane(wv);
+    const uint64_t sp = (uint64_t)(uintptr_t)sbase;
+    const uint64_t spu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sp >> 32)) << 32) |
+                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sp);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(uintptr_t)spu, 0, __builtin_amdgcn_readfirstlane(sbytes), 0x00020000);
+    const int q0 = __builtin_amdgcn_readfirstlane(qoff) + w;
+    const uint32_t dst0 = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)(s * SLOTQ * 1024)) +
+                          (uint32_t)w * 1024u;
+    const int n = __builtin_amdgcn_readfirstlane(nq);
+#pragma unroll
+    for (int q = 0; q < MAXL; ++q) {
+      const bool own = w + WV * q < n;  // fixed count per wave: pieces past the chunk load nothing
+      ring::lds_dma16(r, own ? lane * 16 : kOutOfRange + lane * 16, (q0 + WV * q) * 1024,
+                      dst0 + (uint32_t)(WV * q * 1024));
+    }
+  }
+
+  // block-wide; afterwards chunk 0 (the init layer's, nq0 pieces) is in flight to slot 0
+  __device__ __forceinline__ void init(const MlpDev& m, const SdfDev& s, char* lds, int nq0) {
+    ring = reinterpret_cast<const float4*>(lds);
+    ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
+    char* p = lds + RING_BYTES;
+    const int F = m.freqs;
+    float4* lq = reinterpret_cast<float4*>(p);
+    for (int q = threadIdx.x; q < F; q += blockDim.x)
+      lq[q] = make_float4(m.basis[q], m.basis[F + q], m.basis[2 * F + q], 0.f);
+    lbasis = lq;
+    p += (size_t)F * 16;
+    float* lb = reinterpret_cast<float*>(p);
+    const int nb = (m.n_hidden + 2) * m.bias16_stride;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) lb[i] = m.bias3[i];
+    lbias = lb;
+    p += (size_t)nb * 4;
+    float4* ls = reinterpret_cast<float4*>(p);
+    if (s.kind == 2)
+      for (int i = threadIdx.x; i < s.n_spheres * 4; i += blockDim.x)
+        ls[i] = reinterpret_cast<const float4*>(s.spheres)[i];
+    lspheres = ls;
+    bstride = m.bias16_stride;
+    sbase = m.stream3;
+    sbytes = m.stream3_bytes;
+    lane = threadIdx.x & 63;
+    wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    off = 0;
+    slot = 0;
+    issue(0, nq0, 0);
+    __syncthreads();
+  }
+  // start of the current chunk (nq pieces): wait for it, then DMA the next one (nq_next pieces;
+  // at offset 0 when `wrap`, i.e. the next evaluation's first chunk); returns this lane's A base
+  __device__ __forceinline__ const float4* begin(int nq, int nq_next, bool wrap) {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    next_off = wrap ? 0 : off + nq;
+    issue(next_off, nq_next, slot ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    return ring + slot * SLOTQ * 64 + lane;
+  }
+  __device__ __forceinline__ void end() {
+    off = next_off;
+    slot ^= 1;
+  }
+  __device__ __forceinline__ void drain() { __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0)); }
+  // acc[reg] = bias3[layer][16 sb + 4 g + reg]
+  __device__ __forceinline__ f4v bias_at(int layer, int sb) const {
+    const float4 q = *reinterpret_cast<const float4*>(lbias + layer * bstride + 16 * sb + 4 * (lane >> 4));
+    return f4v{q.x, q.y, q.z, q.w};
+  }
+};
+
+// One segment of a two-sub-block chunk: NU k-steps at ring pieces P0 + 4u + {hi b0, lo b0, hi b1,
+// lo b1}; chains a0 / a1 alternate so consecutive MFMAs are independent.  Each k-step's four LDS
+// reads are issued one k-step ahead.  side(u) runs before k-step u + 1's reads in program order.
+template <int NU, int P0, int NBV, class Side>
+__device__ __forceinline__ void seg(const float4* A, const u4v (&Bh)[NBV], const u4v (&Bl)[NBV],
+                                    f4v& a0, f4v& a1, Side&& side) {
+  float4 w0 = A[P0 * 64], w1 = A[(P0 + 1) * 64], w2 = A[(P0 + 2) * 64], w3 = A[(P0 + 3) * 64];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    side(u);
+    float4 n0 = w0, n1 = w1, n2 = w2, n3 = w3;
+    if (u + 1 < NU) {
+      n0 = A[(P0 + 4 * u + 4) * 64]; n1 = A[(P0 + 4 * u + 5) * 64];
+      n2 = A[(P0 + 4 * u + 6) * 64]; n3 = A[(P0 + 4 * u + 7) * 64];
+    }
+    const u4v h0 = __builtin_bit_cast(u4v, w0), l0 = __builtin_bit_cast(u4v, w1);
+    const u4v h1 = __builtin_bit_cast(u4v, w2), l1 = __builtin_bit_cast(u4v, w3);
+    a0 = mfma(h0, Bh[u], a0); a1 = mfma(h1, Bh[u], a1);
+    a0 = mfma(h0, Bl[u], a0); a1 = mfma(h1, Bl[u], a1);
+    a0 = mfma(l0, Bh[u], a0); a1 = mfma(l1, Bh[u], a1);
+    w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+  }
+}
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 16 rays; every lane of a ray gets the
+// value.  Every wave of the block must call it the same number of times.
+template <int KH, int KQ, int WV, int ACT>
+__device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, float x0, float x1,
+                                      float x2) {
+  constexpr int NC = KH;  // 32-row chunks per hidden layer (= k-steps of the next layer)
+  static_assert(KH == 4 || KH == 8, "hidden 128 or 256");
+  const int g = E.lane >> 4;
+  const int F = m.freqs, L = m.n_hidden, SK = m.skip;
+  // encoding: element e of k-step v in lane group g is slot 32 v + 8 g + e -- sin / cos of
+  // projection slot / 2 (utils.py:37-40, same fma order and accurate sincosf as the FP32 ring),
+  // then x, zeros.  Pairs (e, e + 1) share a projection.
+  u4v erh[KQ], erl[KQ], eah[KQ], eal[KQ];
+#pragma unroll
+  for (int v = 0; v < KQ; ++v) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float r[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int slot = 32 * v + 8 * g + 2 * q + t;
+        float val = 0.f;
+        if (slot < 2 * F) {
+          const float4 b = E.lbasis[slot >> 1];
+          float pr = x0 * b.x;
+          pr = fmaf(x1, b.y, pr);
+          pr = fmaf(x2, b.z, pr);
+          float sn, cs;
+          sincosf(pr, &sn, &cs);
+          val = t ? cs : sn;
+        } else if (slot == 2 * F) {
+          val = x0;
+        } else if (slot == 2 * F + 1) {
+          val = x1;
+        } else if (slot == 2 * F + 2) {
+          val = x2;
+        }
+        r[t] = val;
+      }
+      uint32_t hi, lo;
+      split2(r[0], r[1], hi, lo);
+      erh[v][q] = hi; erl[v][q] = lo;
+      split2(ring32::act<ACT>(r[0]), ring32::act<ACT>(r[1]), hi, lo);
+      eah[v][q] = hi; eal[v][q] = lo;
+    }
+  }
+  auto chunk_q = [&](int i) {  // pieces of hidden layer i's chunks (i == L: the out layer)
+    if (i >= L) return 2 * KH;
+    return 4 * (KH + ((i != L - 1 && i % SK == 0) ? KQ : 0));
+  };
+  u4v sh[KH], sl[KH], dh[KH], dl[KH];
+  f4v pend0, pend1;
+  // activation of chunk ib's accumulators (layer `layer`) into k-step ib of dst, one pair of
+  // elements at a time: pair q = elements 2q, 2q + 1 of the B fragment (registers 2q, 2q + 1 of
+  // sub-block 2 ib for q < 2, of sub-block 2 ib + 1 after).  The empty asm pins each result inside
+  // the chunk that computes it (dst is read only by the next layer).
+  auto retire2 = [&](int layer, int ib, int q) {
+    const float sc = m.scale3[layer];
+    const float z0 = (q < 2 ? pend0[2 * q] : pend1[2 * q - 4]) * sc;
+    const float z1 = (q < 2 ? pend0[2 * q + 1] : pend1[2 * q - 3]) * sc;
+    uint32_t hi, lo;
+    split2(ring32::act<ACT>(z0), ring32::act<ACT>(z1), hi, lo);
+    asm volatile("" : "+v"(hi), "+v"(lo));
+    dh[ib][q] = hi; dl[ib][q] = lo;
+  };
+  auto retire = [&](int layer, int ib) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) retire2(layer, ib, q);
+  };
+  // init layer (neural_blocks.py:80): raw encoding in
+#pragma unroll
+  for (int ib = 0; ib < NC; ++ib) {
+    const float4* A = E.begin(4 * KQ, ib + 1 < NC ? 4 * KQ : chunk_q(0), false);
+    f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
+    if (ib > 0) retire(0, ib - 1);
+    seg<KQ, 0>(A, erh, erl, a0, a1, [](int) {});
+    pend0 = a0; pend1 = a1;
+    E.end();
+  }
+  retire(0, NC - 1);
+  // hidden layers: x = layer(act(cat[x, enc] if skip else x)) (neural_blocks.py:81-84)
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int k = 0; k < KH; ++k) { sh[k] = dh[k]; sl[k] = dl[k]; }
+    const bool skip = i != L - 1 && i % SK == 0;
+    const int nq = chunk_q(i);
+#pragma unroll
+    for (int ib = 0; ib < NC; ++ib) {
+      const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
+      f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
+      // the previous chunk's four activation pairs, spread over the chunk's k-steps
+      seg<KH, 0>(A, sh, sl, a0, a1, [&](int u) {
+        if (ib > 0 && (KH == 4 || (u & 1) == 0)) retire2(1 + i, ib - 1, KH == 4 ? u : u >> 1);
+      });
+      if (skip) seg<KQ, 4 * KH>(A, eah, eal, a0, a1, [](int) {});
+      pend0 = a0; pend1 = a1;
+      E.end();
+    }
+    retire(1 + i, NC - 1);
+  }
+  // out layer (neural_blocks.py:86): one 16-row sub-block, pieces [k-step][hi, lo]; two chains
+  // (even / odd k-steps); row 0 of ray j sits in register 0 of lane j
+  const float4* A = E.begin(2 * KH, 4 * KQ, true);
+  f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+  {
+    float4 w0 = A[0], w1 = A[64], w2 = A[2 * 64], w3 = A[3 * 64];
+#pragma unroll
+    for (int u = 0; u < KH; u += 2) {
+      float4 n0 = w0, n1 = w1, n2 = w2, n3 = w3;
+      if (u + 2 < KH) {
+        n0 = A[(2 * u + 4) * 64]; n1 = A[(2 * u + 5) * 64];
+        n2 = A[(2 * u + 6) * 64]; n3 = A[(2 * u + 7) * 64];
+      }
+      const u4v h0 = __builtin_bit_cast(u4v, w0), l0 = __builtin_bit_cast(u4v, w1);
+      const u4v h1 = __builtin_bit_cast(u4v, w2), l1 = __builtin_bit_cast(u4v, w3);
+      o0 = mfma(h0, dh[u], o0); o1 = mfma(h1, dh[u + 1], o1);
+      o0 = mfma(h0, dl[u], o0); o1 = mfma(h1, dl[u + 1], o1);
+      o0 = mfma(l0, dh[u], o0); o1 = mfma(l1, dh[u + 1], o1);
+      w0 = n0; w1 = n1; w2 = n2; w3 = n3;
+    }
+  }
+  E.end();
+  const float o = (o0[0] + o1[0]) * m.scale3[L + 1];
+  return __shfl(o, E.lane & 15);
+}
+
+}  // namespace ring3
+}  // namespace nrt

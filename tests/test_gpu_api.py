@@ -92,7 +92,30 @@ def test_fp16_scan_best32_cuts_throughput_error():
                thr_over_0p1=int((err > 0.1).sum()), alpha_maxabs=alpha_err.max().item(),
                alpha_over_1e4=int((alpha_err > 1e-4).sum()))
     # the march itself is the same FP16 march either way
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    # (bitwise: the FP16 log2-domain softplus overflows to NaN on the shaped SDF's far points,
+    # pre-activations above 88, so some missed rays carry t = NaN -- DESIGN.md §3 k_march16)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1].view(torch.int32), res[1][1].view(torch.int32))
     e16, e32 = res[0][2], res[1][2]
     assert int((e32 > 0.1).sum()) < int((e16 > 0.1).sum())
     assert e32.median().item() < 0.25 * e16.median().item()
+
+
+def test_fp16_ring_march_repeatable():
+    """Two identical FP16 ring marches of the bare 8x256 MLP SDF give identical bits."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    _, mine = _mlp_sdf_pair()
+    rays = _camera_rays(40, 3).cuda()
+    set_precision("fp16")
+    outs = []
+    for _ in range(3):
+        random.seed(12)
+        with torch.no_grad():
+            it, hit = SDF(sdf=mine, max_steps=64).intersect(rays, primary=True)
+        outs.append((hit.cpu(), it.t.cpu(), it.throughput.cpu(), it.n.cpu()))
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            if a.dtype == torch.float32:
+                a, b = a.view(torch.int32), b.view(torch.int32)
+            assert torch.equal(a, b)
