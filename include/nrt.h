@@ -146,6 +146,11 @@ typedef struct {
   int32_t precision;   /* NRT_FP32 / NRT_FP16 / NRT_FP32_SPLIT                              */
   int32_t* scan_index; /* optional [P] output: the coarse-scan argmin idxs (sdfs.py:243-246), so a
                           training caller can rebuild best_pos = o + idx*step*d; NULL = unused  */
+  /* Batched tiles (pathtrace's chunk_size^2 tile loop in one call, main.py:63-90): when not NULL,
+   * a DEVICE array of per-group scan_max_t values (one random.random() draw per tile,
+   * sdfs.py:236); ray r uses group r / group_rays and scan_max_t is ignored.  NULL = one group. */
+  const double* scan_max_t_groups;
+  int64_t group_rays;
 } nrt_march_params;
 
 /* SDF.intersect (sdfs.py:111-160) for P rays.  Outputs (each [P] or [P,3]):
@@ -308,6 +313,11 @@ int nrt_composite(const float* rgb, const float* throughput, const uint8_t* hit,
  * workspace: nrt_nerfle_workspace_bytes(P, S, light_dim) bytes of device memory.
  * ------------------------------------------------------------------------------------- */
 size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim);
+/* The workspace the call with these MLPs and precision actually needs: 16 B per sample on the
+ * fused FP16 kernel (alpha_raw + rgb_raw), nrt_nerfle_workspace_bytes otherwise (the unfused
+ * path's [P S, 65 / 70] intermediates) -- so a caller chunks by the path that runs. */
+size_t nrt_nerfle_workspace_bytes_for(const nrt_mlp* first, const nrt_mlp* second, int64_t P,
+                                      int32_t S, int32_t light_dim, int32_t precision);
 int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float* rays, int64_t P,
                        const float* ts, int32_t S, const float* light, int32_t light_dim,
                        float* rgb, void* workspace, int precision, void* stream);

@@ -37,7 +37,8 @@ class MarchParams(ctypes.Structure):
     _fields_ = [("max_steps", ctypes.c_int32), ("epsilon", ctypes.c_float),
                 ("max_t", ctypes.c_float), ("primary", ctypes.c_int32),
                 ("scan_max_t", ctypes.c_double), ("precision", ctypes.c_int32),
-                ("scan_index", ctypes.c_void_p)]
+                ("scan_index", ctypes.c_void_p), ("scan_max_t_groups", ctypes.c_void_p),
+                ("group_rays", ctypes.c_int64)]
 
 
 class BsdfComponent(ctypes.Structure):
@@ -90,6 +91,7 @@ _SIGNATURES = {
     "nrt_path_bounce": (_I32, [_P, _P, _P, _I32, _P, _I32, _F, _P, _P, _P, _I64, _P, _P, _P, _P, _P,
                                _P, _P, _I32, _P]),
     "nrt_nerfle_workspace_bytes": (ctypes.c_size_t, [_I64, _I32, _I32]),
+    "nrt_nerfle_workspace_bytes_for": (ctypes.c_size_t, [_P, _P, _I64, _I32, _I32, _I32]),
     "nrt_nerfle_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _I32, _P, _P, _I32, _P]),
     "nrt_light_envmap": (_I32, [_P, _I32, _P, _P]),
     "nrt_plain_nerf_workspace_bytes": (ctypes.c_size_t, [_P, _P, _I64, _I32]),

@@ -613,6 +613,17 @@ size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim) {
   return a256(n * 3 * 4) + a256(n * 65 * 4) + a256(n * in2 * 4) + a256(n * 3 * 4);
 }
 
+size_t nrt_nerfle_workspace_bytes_for(const nrt_mlp* first, const nrt_mlp* second, int64_t P,
+                                       int32_t S, int32_t light_dim, int32_t precision) {
+  if (first && second && precision == NRT_FP16 && option(OPT_NERF_FUSED) != 0 && light_dim == 3 &&
+      nerf_fusable(first, second)) {
+    // fused k_nerfle16: alpha_raw [P S] + rgb_raw [P S, 3]
+    const size_t n = (size_t)std::max<int64_t>(P, 1) * (size_t)std::max(S, 1);
+    return a256(n * 4) + a256(n * 12);
+  }
+  return nrt_nerfle_workspace_bytes(P, S, light_dim);
+}
+
 int nrt_light_envmap(const nrt_light* l, int32_t bins, float* out, void* stream) {
   if (!l || bins < 1 || !out) { set_error("nrt_light_envmap: bad argument"); return NRT_EINVAL; }
   if (l->host_dev.kind != 1) {

@@ -180,6 +180,12 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   ma.step = a->scan_max_t / 128.0;
   ma.scan_idx = a->primary ? a->scan_index : nullptr;
   ma.evals = profile_eval_counter();
+  if (a->primary && a->scan_max_t_groups) {
+    if (a->group_rays < 1) { set_error("nrt_sdf_intersect: group_rays must be >= 1"); return NRT_EINVAL; }
+    if (a->scan_index) { set_error("nrt_sdf_intersect: scan_index with scan_max_t_groups is not supported"); return NRT_EINVAL; }
+    ma.groups = a->scan_max_t_groups;
+    ma.group_rays = a->group_rays;
+  }
   // the normal pass needs the list of hit rays; use the caller's or a workspace-backed one
   int32_t* idx = hit_idx;
   int32_t* cnt = hit_count;

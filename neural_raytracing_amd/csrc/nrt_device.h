@@ -85,7 +85,8 @@ struct MlpDev {
   const float4* stream32;
   int stream32_bytes;
   const float* bias32;             // [layer][bias16_stride], unfolded
-  // FP32-accurate split stream of the ring3 engine (nrt_ring3.h): every weight of layer l as
+  // FP32-accurate split stream of the ring3 engine (nrt_ring3.h): every weight of layer l (folded
+  // into the log2 domain for softplus MLPs, as stream16) as
   // W 2^s_l = hi + lo, two f16 (hi = RNE(W 2^s_l), lo = RNE(W 2^s_l - hi)), fragments of
   // v_mfma_f32_16x16x32_f16 on 16-ray tiles in consumption order (nrt_internal.h ring3_walk);
   // s_l puts the layer's largest |W| in [1, 2) so lo stays a normal f16 for all but the smallest

@@ -255,7 +255,16 @@ struct MarchArgs {
   double step;  // scan step = scan_max_t / 128 (python float)
   int32_t* scan_idx;  // optional [P] coarse-scan argmin output
   unsigned long long* evals = nullptr;  // profiling: ray-evaluations executed (nrt_profile_evals)
+  // batched tiles (nrt_march_params.scan_max_t_groups): ray r scans with scan_max_t of group
+  // r / group_rays (one random.random() draw per tile, sdfs.py:236); nullptr = `step` for all
+  const double* groups = nullptr;
+  int64_t group_rays = 1;
 };
+
+// the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
+__device__ __forceinline__ double scan_step_of(const MarchArgs& a, int64_t ray) {
+  return a.groups ? a.groups[ray / a.group_rays] / 128.0 : a.step;
+}
 
 template <bool F16, int NB>
 __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
@@ -274,6 +283,7 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
   const int64_t rr = valid ? ray : P - 1;
   const float ox = rays[rr * 6], oy = rays[rr * 6 + 1], oz = rays[rr * 6 + 2];
   const float dx = rays[rr * 6 + 3], dy = rays[rr * 6 + 4], dz = rays[rr * 6 + 5];
+  const double step = scan_step_of(a, rr);
 
   // Phase 1 (sdfs.py:119-131): sphere tracing.  The reference evaluates every ray at every step;
   // a ray that stopped marching never changes again, so the wave leaves the phase as soon as none
@@ -302,7 +312,7 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_intersect(
     } else if (j == -1) {
       px = ox; py = oy; pz = oz;
     } else {
-      float ts = (j < 128) ? (float)(a.step * (double)(j + 1)) : __fmul_rn((float)idx, (float)a.step);
+      float ts = (j < 128) ? (float)(step * (double)(j + 1)) : __fmul_rn((float)idx, (float)step);
       px = __fadd_rn(ox, __fmul_rn(ts, dx));
       py = __fadd_rn(oy, __fmul_rn(ts, dy));
       pz = __fadd_rn(oz, __fmul_rn(ts, dz));
@@ -440,7 +450,7 @@ struct RingPol3 {
   static constexpr int RPW = 16, WAVES = WV;
   using Eng = ring3::Engine<KH, KQ, WV>;
   __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds) {
-    E.init(m, s, lds, 4 * KQ);
+    E.init(m, s, lds, 4 * KQ, 4 * KQ);  // chunks 0 and 1: the init layer's
   }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
@@ -477,6 +487,7 @@ __device__ __forceinline__ void march_body(
   int64_t ray = 0;
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
   float t = 0.f, best = 0.f;
+  double step = a.step;  // this lane's scan step (per tile group when batched)
   int i = 0, j = 0, jend = 0, idx = 0;
   bool ended = false, hit = false, whole = false;
   int64_t cursor = 0;  // wave-uniform
@@ -542,6 +553,7 @@ __device__ __forceinline__ void march_body(
             ox = rp[0]; oy = rp[1]; oz = rp[2]; dx = rp[3]; dy = rp[4]; dz = rp[5];
           }
           ended = false;
+          step = scan_step_of(a, ray);
           if (mode == 2) {
             kind = 2;
             idx = 0;
@@ -576,7 +588,7 @@ __device__ __forceinline__ void march_body(
       } else if (mode == 2) {
         px = ox; py = oy; pz = oz;
       } else {
-        const float ts = kind == 1 ? (float)(a.step * (double)j) : __fmul_rn((float)idx, (float)a.step);
+        const float ts = kind == 1 ? (float)(step * (double)j) : __fmul_rn((float)idx, (float)step);
         px = __fadd_rn(ox, __fmul_rn(ts, dx));
         py = __fadd_rn(oy, __fmul_rn(ts, dy));
         pz = __fadd_rn(oz, __fmul_rn(ts, dz));

@@ -272,14 +272,19 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
   std::vector<float> bias32(layers.size() * (size_t)bstride, 0.f);
   for (size_t l = 0; l < layers.size(); ++l)
     for (int r = 0; r < layers[l].R; ++r) bias32[l * bstride + r] = layers[l].b[r];
-  // ---- split stream (nrt_ring3.h): per layer a power-of-two scale 2^s with max|W| 2^s in
-  // [1, 2), then W 2^s = hi + lo in two RNE f16 halves
+  // ---- split stream (nrt_ring3.h): softplus MLPs folded into the log2 domain like stream16
+  // (init W and init / hidden biases x log2 e, out W x ln 2), then per layer a power-of-two
+  // scale 2^s with max|W| 2^s in [1, 2), then W 2^s = hi + lo in two RNE f16 halves
   const int ke3 = (dp + 31) / 32 * 32;
+  auto wfold = [&](size_t l) {
+    return fold ? (l == 0 ? kLog2e : (l + 1 == layers.size() ? kLn2 : 1.f)) : 1.f;
+  };
+  auto bfold = [&](size_t l) { return fold && l + 1 < layers.size() ? kLog2e : 1.f; };
   std::vector<float> lscale(layers.size(), 1.f);
   for (size_t l = 0; l < layers.size(); ++l) {
     float mx = 0.f;
     const Layer& ly = layers[l];
-    for (size_t i = 0; i < (size_t)ly.R * ly.C; ++i) mx = std::max(mx, std::fabs(ly.W[i]));
+    for (size_t i = 0; i < (size_t)ly.R * ly.C; ++i) mx = std::max(mx, std::fabs(ly.W[i] * wfold(l)));
     int e = 0;
     if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &e);  // mx = f 2^e, f in [0.5, 1)
     lscale[l] = std::ldexp(1.f, std::max(-64, std::min(64, 1 - e)));  // mx * scale in [1, 2)
@@ -293,14 +298,14 @@ extern "C" int nrt_mlp_create(const nrt_mlp_desc* d, const float* basis,
       int col = -1;
       if (pos < H) col = col_of_hidden(pos);
       else if (pos - H < ke) col = col_of_slot(ly, pos - H);
-      const float w = wval(ly, row, col) * lscale[l];
+      const float w = (wval(ly, row, col) * wfold(l)) * lscale[l];
       const _Float16 hi = (_Float16)w;
       stream3.push_back(part == 0 ? hi : (_Float16)(w - (float)hi));
     });
   }
   std::vector<float> bias3(layers.size() * (size_t)bstride, 0.f);
   for (size_t l = 0; l < layers.size(); ++l)
-    for (int r = 0; r < layers[l].R; ++r) bias3[l * bstride + r] = layers[l].b[r] * lscale[l];
+    for (int r = 0; r < layers[l].R; ++r) bias3[l * bstride + r] = (layers[l].b[r] * bfold(l)) * lscale[l];
   size_t off_stream3 = blob.add(stream3.data(), stream3.size() * sizeof(_Float16));
   size_t off_b3 = blob.add(bias3.data(), bias3.size() * sizeof(float));
   size_t off_stream32 = blob.add(stream32.data(), stream32.size() * sizeof(float));

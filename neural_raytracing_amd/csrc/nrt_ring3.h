@@ -49,13 +49,36 @@ __device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t&
   lo = __builtin_bit_cast(uint32_t, l);
 }
 
-// KH = H / 32 hidden k-steps, KQ = ke3 / 32 encoding k-steps
+// The activation on the split path.  Softplus MLPs are folded into the log2 domain by the packer
+// (init W and every init / hidden bias x log2 e, out W x ln 2, as the FP16 ring stream), so the
+// device computes softplus(x) / ln 2 = log2(1 + 2^z) at z = x log2 e: v_exp + v_add + v_log, with
+// z itself above 64 (log2(1 + 2^z) == z in f32 there; 2^z would overflow at 128).  Against torch's
+// F.softplus (threshold 20, log1p(exp(x))) the difference is the rounding of 1 + 2^z and the
+// ~1-ulp v_exp / v_log: ~1e-7 absolute, the size of FP32 accumulation noise (the accuracy test
+// against float64, tests/test_gpu_split.py, holds the path to the FP32 fma chain's error).
+template <int ACT>
+__device__ __forceinline__ float act(float z) {
+  if (ACT == ACT_SOFTPLUS) {
+    const float l = __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(z));
+    return z > 64.f ? z : l;
+  }
+  return act_fwd<false>(z, ACT);
+}
+// the encoding's activation (skip-layer inputs): act(enc) in the fold's units
+template <int ACT>
+__device__ __forceinline__ float act_enc(float v) {
+  return ACT == ACT_SOFTPLUS ? act<ACT>(v * 1.4426950408889634f) : act<ACT>(v);
+}
+
+// KH = H / 32 hidden k-steps, KQ = ke3 / 32 encoding k-steps.  Ring depth: 3 slots (the DMA runs
+// two chunks ahead) where they fit beside the basis / bias / sphere tables in 160 KiB, else 2.
 template <int KH, int KQ, int WV>
 struct Engine {
   static constexpr int MAXQ = 4 * (KH + KQ);            // largest chunk (a skip layer's), KiB
   static constexpr int MAXL = (MAXQ + WV - 1) / WV;     // DMA pieces per wave per chunk
   static constexpr int SLOTQ = MAXL * WV;
-  static constexpr int RING_BYTES = 2 * SLOTQ * 1024;
+  static constexpr int D = 3 * SLOTQ * 1024 <= 128 * 1024 ? 3 : 2;
+  static constexpr int RING_BYTES = D * SLOTQ * 1024;
   static constexpr int kOutOfRange = 0x40000000;
   // LDS of one block: ring | basis (float4 per frequency) | biases | sphere table
   static size_t lds_bytes(int F, size_t bias_bytes, size_t sphere_bytes) {
@@ -68,7 +91,6 @@ struct Engine {
   const float4* lspheres;   // [n][4] float4 (SdfDev layout), read by ring32::spheres_value16
   const void* sbase;
   int sbytes, bstride;
-  int off, next_off;        // piece offset of the current / next chunk in stream3 (wave-uniform)
   int slot;
   int lane, wv;
 
@@ -91,8 +113,10 @@ struct Engine {
     }
   }
 
-  // block-wide; afterwards chunk 0 (the init layer's, nq0 pieces) is in flight to slot 0
-  __device__ __forceinline__ void init(const MlpDev& m, const SdfDev& s, char* lds, int nq0) {
+  // block-wide; afterwards chunk 0 (the init layer's, nq0 pieces) is in flight to slot 0 and,
+  // with a 3-slot ring, chunk 1 (nq1 pieces) to slot 1
+  __device__ __forceinline__ void init(const MlpDev& m, const SdfDev& s, char* lds, int nq0,
+                                       int nq1) {
     ring = reinterpret_cast<const float4*>(lds);
     ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
     char* p = lds + RING_BYTES;
@@ -117,27 +141,43 @@ struct Engine {
     sbytes = m.stream3_bytes;
     lane = threadIdx.x & 63;
     wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    off = 0;
     slot = 0;
+    // pieces of one whole evaluation (chunk offsets wrap at it): init NC x 4 KQ, hidden layers
+    // NC x 4 (KH + KQ on skip layers), out 2 KH
+    {
+      const int L = m.n_hidden, SK = m.skip;
+      int nskip = 0;
+      for (int i = 0; i < L; ++i) nskip += (i != L - 1 && i % SK == 0) ? 1 : 0;
+      tot = KH * 4 * KQ + 2 * KH + L * KH * 4 * KH + KH * 4 * KQ * nskip;
+    }
     issue(0, nq0, 0);
+    if (D == 3) {
+      issue(nq0, nq1, 1);
+      dma_off = nq0 + nq1;  // stream offset of the chunk after the two in flight
+    } else {
+      dma_off = nq0;
+    }
     __syncthreads();
   }
-  // start of the current chunk (nq pieces): wait for it, then DMA the next one (nq_next pieces;
-  // at offset 0 when `wrap`, i.e. the next evaluation's first chunk); returns this lane's A base
-  __device__ __forceinline__ const float4* begin(int nq, int nq_next, bool wrap) {
+  int dma_off;  // stream offset of the next chunk to DMA (wave-uniform)
+  int tot;      // pieces per evaluation
+  // Start of the current chunk: wait for it, then DMA a chunk ahead -- with 2 slots the next one,
+  // with 3 the one after (chunk c + 2 lands in the slot chunk c - 1 used, which every wave has
+  // left once it passes this barrier); nq_ahead pieces, the offset wrapping to the next
+  // evaluation's first chunk.  The pieces of one wave complete in issue order, so the wait for
+  // the current chunk leaves the younger chunk's MAXL pieces in flight (vmcnt(MAXL)).
+  __device__ __forceinline__ const float4* begin(int nq_ahead) {
     asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0));
+    __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(D == 3 ? MAXL : 0));
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    next_off = wrap ? 0 : off + nq;
-    issue(next_off, nq_next, slot ^ 1);
+    const int o = dma_off >= tot ? dma_off - tot : dma_off;
+    issue(o, nq_ahead, slot == 0 ? D - 1 : slot - 1);
+    dma_off = o + nq_ahead;
     __builtin_amdgcn_sched_barrier(0);
     return ring + slot * SLOTQ * 64 + lane;
   }
-  __device__ __forceinline__ void end() {
-    off = next_off;
-    slot ^= 1;
-  }
+  __device__ __forceinline__ void end() { slot = slot + 1 == D ? 0 : slot + 1; }
   __device__ __forceinline__ void drain() { __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0)); }
   // acc[reg] = bias3[layer][16 sb + 4 g + reg]
   __device__ __forceinline__ f4v bias_at(int layer, int sb) const {
@@ -212,7 +252,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
       uint32_t hi, lo;
       split2(r[0], r[1], hi, lo);
       erh[v][q] = hi; erl[v][q] = lo;
-      split2(ring32::act<ACT>(r[0]), ring32::act<ACT>(r[1]), hi, lo);
+      split2(act_enc<ACT>(r[0]), act_enc<ACT>(r[1]), hi, lo);
       eah[v][q] = hi; eal[v][q] = lo;
     }
   }
@@ -220,6 +260,16 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
     if (i >= L) return 2 * KH;
     return 4 * (KH + ((i != L - 1 && i % SK == 0) ? KQ : 0));
   };
+  // pieces of chunk c of the evaluation's chunk sequence (init NC, hidden L x NC, out 1; c past
+  // the end is the next evaluation's): the ring DMAs chunk c + D - 1 at the start of chunk c
+  const int NCH = NC + L * NC + 1;
+  auto size_at = [&](int c) {
+    if (c >= NCH) c -= NCH;
+    if (c < NC) return 4 * KQ;
+    if (c < NCH - 1) return chunk_q((c - NC) / NC);
+    return 2 * KH;
+  };
+  constexpr int AH = Engine<KH, KQ, WV>::D - 1;  // chunks the DMA runs ahead
   u4v sh[KH], sl[KH], dh[KH], dl[KH];
   f4v pend0, pend1;
   // activation of chunk ib's accumulators (layer `layer`) into k-step ib of dst, one pair of
@@ -231,7 +281,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
     const float z0 = (q < 2 ? pend0[2 * q] : pend1[2 * q - 4]) * sc;
     const float z1 = (q < 2 ? pend0[2 * q + 1] : pend1[2 * q - 3]) * sc;
     uint32_t hi, lo;
-    split2(ring32::act<ACT>(z0), ring32::act<ACT>(z1), hi, lo);
+    split2(act<ACT>(z0), act<ACT>(z1), hi, lo);
     asm volatile("" : "+v"(hi), "+v"(lo));
     dh[ib][q] = hi; dl[ib][q] = lo;
   };
@@ -242,7 +292,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   // init layer (neural_blocks.py:80): raw encoding in
 #pragma unroll
   for (int ib = 0; ib < NC; ++ib) {
-    const float4* A = E.begin(4 * KQ, ib + 1 < NC ? 4 * KQ : chunk_q(0), false);
+    const float4* A = E.begin(size_at(ib + AH));
     f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
     if (ib > 0) retire(0, ib - 1);
     seg<KQ, 0>(A, erh, erl, a0, a1, [](int) {});
@@ -258,7 +308,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
     const int nq = chunk_q(i);
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
-      const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
+      const float4* A = E.begin(size_at(NC + i * NC + ib + AH));
       f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
       // the previous chunk's four activation pairs, spread over the chunk's k-steps
       seg<KH, 0>(A, sh, sl, a0, a1, [&](int u) {
@@ -272,7 +322,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   }
   // out layer (neural_blocks.py:86): one 16-row sub-block, pieces [k-step][hi, lo]; two chains
   // (even / odd k-steps); row 0 of ray j sits in register 0 of lane j
-  const float4* A = E.begin(2 * KH, 4 * KQ, true);
+  const float4* A = E.begin(size_at(NCH - 1 + AH));
   f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
   {
     float4 w0 = A[0], w1 = A[64], w2 = A[2 * 64], w3 = A[3 * 64];

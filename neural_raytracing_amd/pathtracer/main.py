@@ -9,7 +9,7 @@ import random
 import torch
 
 from .differentiable import needs_grad
-from .render import fused_integrator, render_tile
+from .render import fused_integrator, render_tiles
 from .samplers import Sampler
 
 
@@ -79,13 +79,17 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
         fused = None  # training: integrator.sample carries the gradients
     if getattr(lights, "per_camera", lambda: None)() is not None:
         fused = None  # one light per camera: Direct.sample shades camera by camera
-    for ij in range(len(xs) * len(ys)):
+    if fused is not None:
+        # every tile in the reference's order, batched into few launch chains (render.py)
+        tiles = []
+        for ij in range(len(xs) * len(ys)):
+            i, j = divmod(ij, len(ys))
+            tiles.append((xs[j], ys[i]))
+        render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk_size, size,
+                     with_noise, background)
+    for ij in range(len(xs) * len(ys) if fused is None else 0):
         i, j = divmod(ij, len(ys))
         x0, y0 = xs[j], ys[i]
-        if fused is not None:
-            render_tile(fused, shapes, lights, cameras, bsdf, out, x0, y0, chunk_size, size,
-                        with_noise, background)
-            continue
         rays = _tile_rays(cameras, x0 - trim, y0 - trim, chunk_size + 2 * trim, size, sampler,
                           bundle_size, batch_dims, with_noise, device, positions=bool(trim))
         values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,

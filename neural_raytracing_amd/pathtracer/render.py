@@ -56,8 +56,10 @@ def _buffers(P, nb, device):
     return b
 
 
-def direct_kernels(direct, shapes, rays_flat, bsdf, lights):
-    """Run intersect + shade on flat rays [P,6]; returns the buffer set (rgb zero on misses)."""
+def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None):
+    """Run intersect + shade on flat rays [P,6]; returns the buffer set (rgb zero on misses).
+    scan_groups: for batched tiles, the number of tiles G; ray r belongs to tile r // (P // G)
+    and each tile draws its own scan jitter (random.random(), sdfs.py:236), in tile order."""
     P = rays_flat.shape[0]
     dev = rays_flat.device
     nb = len(getattr(bsdf, "bsdfs", [bsdf]))
@@ -69,10 +71,19 @@ def direct_kernels(direct, shapes, rays_flat, bsdf, lights):
         b.ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
     primary = bool(direct.training)
     scan_max_t = 0.0
+    groups = None
     if primary:
-        scan_max_t = getattr(shapes, "dist", 2.2) + random.random() * (2 / 128)
+        dist = getattr(shapes, "dist", 2.2)
+        if scan_groups is None:
+            scan_max_t = dist + random.random() * (2 / 128)
+        else:
+            groups = torch.tensor([dist + random.random() * (2 / 128) for _ in range(scan_groups)],
+                                  dtype=torch.float64).to(dev, non_blocking=True)
     mp = _lib.MarchParams(int(shapes.max_steps), float(shapes.epsilon), 10.0, int(primary),
                           float(scan_max_t), _lib.precision_code())
+    if groups is not None:
+        mp.scan_max_t_groups = groups.data_ptr()
+        mp.group_rays = P // scan_groups
     s = _lib.stream()
     _lib.call("nrt_sdf_intersect", sh, _lib.ptr(rays_flat), P, ctypes.byref(mp), _lib.ptr(b.t),
               _lib.ptr(b.hit), _lib.ptr(b.p), _lib.ptr(b.n), _lib.ptr(b.raw), _lib.ptr(b.wi),
@@ -103,6 +114,40 @@ def render_tile(fused, shapes, lights, cameras, bsdf, out, x0, y0, chunk, size, 
     b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights)
     composite(b, N, chunk, chunk, with_alpha, background, out, x0 - ox, y0 - oy)
     return b
+
+
+# rays per batched launch of pathtrace's fused tiles: 4M rays keep every buffer (rays, hits,
+# points, normals, frames, rgb: ~100 B a ray) under half a GB while filling the persistent marches
+# (65,536 ray slots per round on 256 CUs) many times over
+MAX_BATCH_RAYS = 1 << 22
+
+
+def render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk, size, with_noise,
+                 background, ox=0, oy=0):
+    """pathtrace's fused tile loop (main.py:63-90) as few launch chains as possible: the rays of
+    consecutive tiles are generated tile by tile (same camera-jitter draws, same order), marched,
+    scanned and shaded in one nrt_sdf_intersect + nrt_shade_direct over all of them -- each tile
+    keeps its own scan jitter (nrt_march_params.scan_max_t_groups) -- and composited tile by
+    tile.  Equal to rendering the tiles one at a time; the GPU sees up to MAX_BATCH_RAYS rays per
+    launch instead of chunk_size^2."""
+    direct, with_alpha = fused
+    N = len(cameras)
+    per_tile = N * chunk * chunk
+    dev = out.device
+    step = max(1, MAX_BATCH_RAYS // per_tile)
+    for t0 in range(0, len(tiles), step):
+        batch = tiles[t0:t0 + step]
+        rays = torch.empty(len(batch), per_tile, 6, device=dev)
+        for k, (x0, y0) in enumerate(batch):
+            rays[k] = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise).reshape(-1, 6)
+        b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights,
+                           scan_groups=len(batch) if len(batch) > 1 else None)
+        for k, (x0, y0) in enumerate(batch):
+            sl = slice(k * per_tile, (k + 1) * per_tile)
+            _lib.call("nrt_composite", _lib.ptr(b.rgb[sl]), _lib.ptr(b.thr[sl]), _lib.ptr(b.hit[sl]),
+                      N, chunk, chunk, int(with_alpha), int(not with_alpha), float(background),
+                      _lib.ptr(out), out.shape[1], out.shape[2], out.shape[3], int(x0 - ox),
+                      int(y0 - oy), _lib.stream())
 
 
 def row_shard(size, rank, world, tile_rows=16):

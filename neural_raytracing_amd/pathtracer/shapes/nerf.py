@@ -96,8 +96,10 @@ class NeRFLE(nn.Module):
     ``envmap=True`` its envmap over bins^2 directions (``nrt_light_envmap``, nerf.py:183-191).
     """
 
-    # samples per nrt_nerfle_forward call (bounds the [S*P, 65/70] intermediates to ~2.3 GB)
-    MAX_SAMPLES_PER_CALL = 1 << 22
+    # workspace bytes per nrt_nerfle_forward call: the unfused path keeps [S*P, 65/70] f32
+    # intermediates (~564 B a sample: 4M samples), the fused FP16 kernel 16 B a sample (134M
+    # samples: cfg5's 1600^2 x 256 frame in 5 calls instead of 157)
+    MAX_WORKSPACE_BYTES = 1 << 31
 
     def __init__(self, envmap=False, bins=4, device="cuda", steps=64):
         super().__init__()
@@ -145,16 +147,20 @@ class NeRFLE(nn.Module):
         else:
             light = lights.location.reshape(-1, 3)[0].detach().float().to(dev).contiguous()
         rgb = torch.empty(P, 3, device=dev)
-        chunk = max(1, min(P, self.MAX_SAMPLES_PER_CALL // self.steps))
-        ws = torch.empty(lib.nrt_nerfle_workspace_bytes(chunk, self.steps, light.numel()),
-                         dtype=torch.uint8, device=dev)
         first, second = self.first.nrt(), self.second.nrt()
+        prec = _lib.precision_code()
+        per_ray = lib.nrt_nerfle_workspace_bytes_for(first, second, 1024, self.steps,
+                                                     light.numel(), prec) / 1024
+        chunk = max(1, min(P, int(self.MAX_WORKSPACE_BYTES // per_ray)))
+        ws = torch.empty(lib.nrt_nerfle_workspace_bytes_for(first, second, chunk, self.steps,
+                                                            light.numel(), prec),
+                         dtype=torch.uint8, device=dev)
         for r0 in range(0, P, chunk):
             n = min(chunk, P - r0)
             _lib.call("nrt_nerfle_forward", first, second, _lib.ptr(flat[r0:r0 + n]), n,
                       _lib.ptr(ts), self.steps, _lib.ptr(light), light.numel(),
                       _lib.ptr(rgb[r0:r0 + n]),
-                      _lib.ptr(ws), _lib.precision_code(), _lib.stream())
+                      _lib.ptr(ws), prec, _lib.stream())
         return rgb.reshape(lead + (3,))
 
     def _forward_train(self, flat, ts, light):

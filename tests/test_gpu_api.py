@@ -119,3 +119,46 @@ def test_fp16_ring_march_repeatable():
             if a.dtype == torch.float32:
                 a, b = a.view(torch.int32), b.view(torch.int32)
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split"])
+def test_pathtrace_batched_tiles_with_jitter_match_oracle(prec):
+    """pathtrace's fused tiles are marched / shaded in one batch (render.render_tiles): 16 tiles,
+    each with its own scan jitter (random.random(), sdfs.py:236) and camera jitter (two rand_like
+    draws per tile, cameras.py:35-36) in tile order, vs the oracle's tile loop fed the same
+    draws."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import _lib, set_precision
+    from tests.test_gpu_parity import _scene_pair
+    ref, mine = _scene_pair()
+    size, chunk, amp = 64, 16, 0.5
+    n_tiles = (size // chunk) ** 2
+    torch.manual_seed(77)
+    draws = [torch.rand(2, chunk, chunk, device="cuda").cpu() for _ in range(n_tiles)]
+    it = iter(draws)
+
+    def camera_noise(pos):
+        nz = next(it)
+        return nz[0][..., None], nz[1][..., None]
+
+    random.seed(21)
+    with torch.no_grad():
+        want = R.render(ref["shape"], ref["lights"], ref["camera"], ref["integrator"], ref["bsdf"],
+                        size=size, chunk_size=chunk, background=0.25, with_noise=amp,
+                        camera_noise=camera_noise)
+    set_precision(prec)
+    torch.manual_seed(77)
+    random.seed(21)
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    with torch.no_grad():
+        got, _ = pt.pathtrace(mine["shape"], mine["lights"], mine["camera"], mine["integrator"],
+                              bsdf=mine["bsdf"], size=size, chunk_size=chunk, bundle_size=1,
+                              background=0.25, with_noise=amp, silent=True)
+    n_isect = _lib.profile_read("k_intersect")[1]
+    _lib.profile_enable(False)
+    assert n_isect == 1, "the 16 tiles were not batched into one intersect launch"
+    err = (got.cpu() - want).abs()
+    report(f"batched_tiles_vs_oracle[{prec}]", tiles=n_tiles, maxabs=err.max().item(),
+           pixels_over_1e4=int((err.amax(-1) > 1e-4).sum()))
+    assert err.max().item() <= 1e-4
