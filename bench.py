@@ -726,6 +726,8 @@ def bench_other(args):
     device = torch.device("cuda", 0)
     torch.cuda.set_device(device)
     _lib.load(require_device=True)
+    if args.scene == "nerfle" and not args.precision_set:
+        args.precision = "fp16"  # BASELINE cfg5 names the fp16 MFMA path
     nra.set_precision(args.precision)
     size = args.size
     sc = build_other_scene(args.scene, device, args.samples)
@@ -733,7 +735,7 @@ def bench_other(args):
         rr = RowRenderer(sc["shape"], sc["lights"], sc["cameras"], sc["integrator"], sc["bsdf"],
                          size, range(size), background=0.0, with_noise=1e-3, device=device)
         step = rr.render
-        kernel = "k_march16"
+        kernel = MARCH_KERNEL[args.precision]
     else:
         focal = float(0.5 * size / math.tan(0.5 * 0.6911))
         cam = pt.cameras.NeRFCamera(cam_to_world=sc["c2w"][None].to(device), focal=focal,
@@ -759,6 +761,8 @@ def bench_other(args):
     rays_total = size * size * args.steps
     if sc["kind"] == "march":
         flop = rays_total * (args.samples + MARCH_KERNEL_SCAN_EVALS) * sc["flop_eval"]
+        if args.precision == "fp32-split":
+            flop *= 3  # f16 MFMA products per f32 product
     else:
         flop = rays_total * args.samples * sc["flop_sample"]
     achieved = flop / (k_ms * 1e-3) / 1e12
@@ -776,7 +780,36 @@ def bench_other(args):
                      "flop_per_step": flop / args.steps,
                      "kernel_ms_per_step": k_ms / args.steps, "launches": k_n},
     }
+    if sc["kind"] == "march" and args.scene == "colocate":
+        line["valu_roofline"] = colocate_valu_roofline(size, args, k_ms / max(k_n, 1))
     print(json.dumps(line), flush=True)
+
+
+# VALU operations per SDF evaluation of the colocate scene's SphereSDF(n=64) (sdfs.py:37-43,
+# utils.py:386-387), counted per sphere as issued lane-operations: the (I + tfs) p transform 9
+# fma, the centre 3 sub, |q|^2 3 fma, sqrt, - r, * -k, exp, += : 20 ops, 2 of them quarter-rate
+# transcendentals (x4 issue slots) -> 26 slot-equivalents; plus the 8x128 shift MLP's activations
+# (softplus as exp + add + log, 2 transcendentals: 9 slot-equivalents per element) on 128 x 9
+# layers -- the work the MFMA roofline does not count.
+COLOCATE_SPHERES = 64
+VALU_SLOTS_PER_SPHERE = 26
+VALU_SLOTS_PER_ACT = 9
+
+
+def colocate_valu_roofline(size, args, kernel_ms):
+    """VALU roofline of the colocate march (k_march16): algorithmic lane-operations (every ray at
+    every march step and scan point, as the MFMA count) over the kernel time, against the VALU
+    issue peak -- 256 CUs x 4 SIMDs x 32 lanes per clock at 2.4 GHz = 78.6 T lane-ops/s (the
+    157.3 TFLOP/s FP32 vector peak counts an fma as 2)."""
+    evals = size * size * (args.samples + MARCH_KERNEL_SCAN_EVALS)
+    per_eval = COLOCATE_SPHERES * VALU_SLOTS_PER_SPHERE + VALU_SLOTS_PER_ACT * 128 * 9
+    ops = evals * per_eval
+    peak = 256 * 4 * 32 * 2.4e9 / 1e12  # T lane-ops/s
+    ach = ops / (kernel_ms * 1e-3) / 1e12
+    return {"bound": "valu", "unit": "T lane-ops/s", "achieved": ach, "peak": peak,
+            "frac": ach / peak, "ops_per_eval": per_eval,
+            "note": "smooth-min over 64 spheres + shift-MLP activations per evaluation; add the "
+                    "MFMA frac for the kernel's issue-bound picture"}
 
 
 def bench_train(args):

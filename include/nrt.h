@@ -82,9 +82,9 @@ int nrt_mlp_create(const nrt_mlp_desc* desc, const float* host_basis,
 int nrt_mlp_destroy(nrt_mlp* mlp);
 /* Re-pack an MLP handle from the caller's DEVICE weights after an optimiser step (training,
  * SURVEY §8f rank 1; the same nn.Linear layouts as nrt_mlp_create, stream-ordered, no host copy):
- * refreshes the fragments nrt_mlp_forward / nrt_mlp_backward / nrt_mlp_grad_backward read.  A
- * refreshed handle no longer serves the FP16 ring march or shading programs (NRT_EINVAL there);
- * render with a handle from nrt_mlp_create. */
+ * refreshes the fragments nrt_mlp_forward / nrt_mlp_backward / nrt_mlp_grad_backward read and the
+ * FP32 and fp32-split march streams.  A refreshed handle no longer serves the FP16 ring march or
+ * shading programs (those calls fall back or fail); render with a handle from nrt_mlp_create. */
 int nrt_mlp_refresh(nrt_mlp* mlp, const float* const* device_weights,
                     const float* const* device_biases, void* stream);
 

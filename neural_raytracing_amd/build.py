@@ -53,9 +53,7 @@ def build(force=False, verbose=True, jobs=None):
     jobs = jobs or min(len(SOURCES), os.cpu_count() or 4, 8)
     with ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    # rocBLAS: the batch-reduction GEMMs of the MLP weight gradients (nrt_api_train.hip)
-    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs,
-           "-L/opt/rocm/lib", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", OUT + ".tmp", *objs]
     subprocess.run(cmd, check=True, cwd=CSRC)
     os.replace(OUT + ".tmp", OUT)
     return OUT

@@ -7,10 +7,9 @@
 //                     row-local backward chain dZ_l = (dZ_{l+1} W_{l+1}) * act'(Z_l) with the W^T
 //                     fragments, the encoding gradient, and dL/dx, dL/dlatent.  TILE moves the
 //                     encoding and its gradient out of the slab into per-wave global tiles.
-//   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M): rocBLAS sgemm on the saved
-//                     activations; bias gradients = column sums of dZ_l (k_colsum_*).
-#include <rocblas/rocblas.h>
-
+//   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M): k_wgrad, split-K exact-f32 MFMA
+//                     on the saved activations, slices summed in order; bias gradients = column
+//                     sums of dZ_l (k_colsum_*).
 #include <mutex>
 
 #include "nrt_launch.h"
@@ -425,43 +424,80 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   return w;
 }
 
-// One rocBLAS handle per (thread, device): a handle is bound to the device that was current when
-// it was created, and rocblas_set_stream + the GEMM sequence that follows must not interleave
-// with another thread's.  Handles live for the process.
-rocblas_handle blas() {
-  thread_local std::vector<std::pair<int, rocblas_handle>> handles;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  for (auto& e : handles)
-    if (e.first == dev) return e.second;
-  rocblas_handle h = nullptr;
-  if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-  handles.emplace_back(dev, h);
-  return h;
-}
-
-int blas_fail(rocblas_status s, const char* what) {
-  set_error(std::string(what) + ": rocBLAS status " + std::to_string((int)s));
-  return NRT_EHIP;
-}
-
-// Split-K weight gradients.  dW = dZ^T In has a tiny output (R x C <= 256 x 550) and a huge
-// K (the batch, ~10^4-10^5): one sgemm covers a handful of output tiles, i.e. a handful of CUs.
-// The batch is cut into S equal chunks (one strided-batched sgemm, S x the tiles) plus a
-// remainder, and the partial products are summed in chunk order (deterministic).
+// Split-K weight gradients.  dW = dZ^T In has a small output (R x C <= 256 x 550) and a long K
+// (the batch, ~10^4-10^5): the batch is cut into S slices, one wave computes one 64 x 64 output
+// tile of one slice on exact-f32 MFMA, and the slice partials are summed in slice order
+// (deterministic).  S is chosen from the shape alone (same inputs, same bits).
 constexpr int kSplitMax = 64;
-constexpr int64_t kSplitRows = 1024;  // rows per chunk at least
+constexpr int64_t kSliceRows = 256;  // batch rows per slice at least
+constexpr int kWgradWaves = 4;        // waves per block
 
 size_t split_part_floats(const MlpDev& d) {
   const size_t rc = (size_t)std::max(d.hidden, d.out) * (size_t)(d.hidden + d.dp);
-  return (size_t)(kSplitMax + 1) * rc;
+  return (size_t)kSplitMax * rc;
 }
 
 struct GemmCtx {
-  rocblas_handle hb;
   float* part;  // split_part_floats(d) floats
   hipStream_t st;
 };
+
+// part[s][r][c] = sum over the rows m of slice s of dZ[m][r] In[m][c] (row-major dZ [M][R],
+// In [M][ldi] from column c0i).  v_mfma_f32_32x32x2_f32 (exact f32, an fma chain) with a 2 x 2
+// grid of 32x32 accumulators: lane (i = l & 31, h = l >> 5) loads dZ[m + h][r0 + 32a + i] (the A
+// operand, dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row segments per half-wave, eight
+// k-steps of loads in flight; out-of-range rows / columns load zeros.
+template <int = 0>
+__global__ void __launch_bounds__(64 * kWgradWaves) k_wgrad(
+    const float* __restrict__ dZ, int R, const float* __restrict__ In, int ldi, int C, int64_t M,
+    int tiles_c, int n_tiles, int64_t slice_rows, float* __restrict__ part) {
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  const int tile = blockIdx.x * kWgradWaves + (threadIdx.x >> 6);
+  if (tile >= n_tiles) return;
+  const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+  const int r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
+  const int64_t m0 = (int64_t)blockIdx.y * slice_rows;
+  const int64_t m1 = std::min<int64_t>(M, m0 + slice_rows);
+  const bool ra = r0 + i < R, rb = r0 + 32 + i < R, ca = c0 + i < C, cb = c0 + 32 + i < C;
+  f16v_ acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  constexpr int U = 8;  // k-steps (2 rows each) per group
+  for (int64_t m = m0; m < m1; m += 2 * U) {
+    float a0[U], a1[U], b0[U], b1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = m + 2 * u + h;
+      const bool ok = row < m1;
+      const float* zr = dZ + row * R + r0 + i;
+      const float* ir = In + row * ldi + c0 + i;
+      a0[u] = ok && ra ? zr[0] : 0.f;
+      a1[u] = ok && rb ? zr[32] : 0.f;
+      b0[u] = ok && ca ? ir[0] : 0.f;
+      b1[u] = ok && cb ? ir[32] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], acc00, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b1[u], acc01, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b0[u], acc10, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], acc11, 0, 0, 0);
+    }
+  }
+  // 32x32 accumulator: register q holds row (q & 3) + 8 (q >> 2) + 4 h, column i
+  float* out = part + (size_t)blockIdx.y * R * C;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = (q & 3) + 8 * (q >> 2) + 4 * h;
+    const int ra_ = r0 + rr, rb_ = r0 + 32 + rr;
+    if (ra_ < R) {
+      if (ca) out[(size_t)ra_ * C + c0 + i] = acc00[q];
+      if (cb) out[(size_t)ra_ * C + c0 + 32 + i] = acc01[q];
+    }
+    if (rb_ < R) {
+      if (ca) out[(size_t)rb_ * C + c0 + i] = acc10[q];
+      if (cb) out[(size_t)rb_ * C + c0 + 32 + i] = acc11[q];
+    }
+  }
+}
 
 // dW[r][c0 + c] = sum_{s < slots} part[s][r][c]
 template <int = 0>
@@ -479,31 +515,21 @@ __global__ void k_split_reduce(const float* __restrict__ part, int slots, int R,
 // row-major dW[R][ldw] (columns c0 .. c0+C) = dZ[M][R]^T @ In[M][C]
 int grad_gemm(const GemmCtx& g, const float* dZ, int R, const float* In, int C, int64_t M,
               float* dW, int ldw, int c0) {
-  const float one = 1.f, zero = 0.f;
-  const int S = (int)std::min<int64_t>(kSplitMax, M / kSplitRows);
-  rocblas_status s;
-  if (S <= 1) {
-    // column-major view: dW^T (C x R, ld ldw) = In^T (C x M, ld C) * dZ (M x R = (R x M, ld R)^T)
-    s = rocblas_sgemm(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
-                      (rocblas_int)M, &one, In, C, dZ, R, &zero, dW + c0, ldw);
-    return s == rocblas_status_success ? NRT_OK : blas_fail(s, "rocblas_sgemm");
-  }
-  const int64_t Mc = M / S, rem = M - (int64_t)S * Mc;
-  const rocblas_stride pc = (rocblas_stride)R * C;
-  s = rocblas_sgemm_strided_batched(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
-                                    (rocblas_int)Mc, &one, In, C, (rocblas_stride)(Mc * C), dZ, R,
-                                    (rocblas_stride)(Mc * R), &zero, g.part, C, pc, S);
-  if (s != rocblas_status_success) return blas_fail(s, "rocblas_sgemm_strided_batched");
-  int slots = S;
-  if (rem > 0) {
-    s = rocblas_sgemm(g.hb, rocblas_operation_none, rocblas_operation_transpose, C, R,
-                      (rocblas_int)rem, &one, In + S * Mc * C, C, dZ + S * Mc * R, R, &zero,
-                      g.part + (size_t)S * pc, C);
-    if (s != rocblas_status_success) return blas_fail(s, "rocblas_sgemm");
-    ++slots;
-  }
+  const int tiles_r = (R + 63) / 64, tiles_c = (C + 63) / 64, n_tiles = tiles_r * tiles_c;
+  // slices: about 16 waves per CU over the tiles, at least kSliceRows batch rows each
+  int64_t S = std::max<int64_t>(1, (256 * 16 + n_tiles - 1) / n_tiles);
+  S = std::min<int64_t>(S, kSplitMax);
+  S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
+  int64_t slice_rows = (M + S - 1) / S;
+  slice_rows = (slice_rows + 15) / 16 * 16;  // whole k-step groups
+  S = std::max<int64_t>(1, (M + slice_rows - 1) / slice_rows);
+  const dim3 grid((unsigned)((n_tiles + kWgradWaves - 1) / kWgradWaves), (unsigned)S);
+  ProfScope prof("k_wgrad", g.st);
+  k_wgrad<><<<grid, dim3(64 * kWgradWaves), 0, g.st>>>(dZ, R, In, C, C, M, tiles_c, n_tiles,
+                                                      slice_rows, g.part);
+  if (int rc = check_launch("k_wgrad")) return rc;
   const int64_t n = (int64_t)R * C;
-  k_split_reduce<><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g.st>>>(g.part, slots, R, C,
+  k_split_reduce<><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g.st>>>(g.part, (int)S, R, C,
                                                                             dW, ldw, c0);
   return check_launch("k_split_reduce");
 }
@@ -628,11 +654,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     if ((rc = check_launch("k_mlp_backward32"))) return rc;
   }
   if (!dweights && !dbiases) return NRT_OK;
-  rocblas_handle hb = blas();
-  if (!hb) { set_error("nrt_mlp_backward: rocblas_create_handle failed"); return NRT_EHIP; }
-  rocblas_status s = rocblas_set_stream(hb, st);
-  if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
-  const GemmCtx gc{hb, w.kpart, st};
+  const GemmCtx gc{w.kpart, st};
   const size_t lay = (size_t)M * H;
   for (int l = 0; l <= L + 1; ++l) {
     const bool outl = l == L + 1;
@@ -732,11 +754,7 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   k_fill<><<<dim3(std::min<int64_t>(ceil_div64(M * d.out, 256), 1024)), dim3(256), 0, st>>>(
       seed + (size_t)M * d.out, M * d.out, 1.f);
   if ((rc = check_launch("k_fill"))) return rc;
-  rocblas_handle hb = blas();
-  if (!hb) { set_error("nrt_mlp_grad_backward: rocblas_create_handle failed"); return NRT_EHIP; }
-  rocblas_status s = rocblas_set_stream(hb, st);
-  if (s != rocblas_status_success) return blas_fail(s, "rocblas_set_stream");
-  const GemmCtx gc{hb, buf[8], st};
+  const GemmCtx gc{buf[8], st};
   const size_t lay2 = (size_t)M2 * H;
   for (int l = 0; l <= L + 1; ++l) {
     const bool outl = l == L + 1;

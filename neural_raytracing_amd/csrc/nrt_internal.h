@@ -35,8 +35,9 @@ struct nrt_mlp {
   int64_t n_src = 0;
   std::vector<void*> gather_dst;   // per section: destination array, element count, FP16?
   std::vector<int64_t> gather_n;
-  std::vector<char> gather_f16;
+  std::vector<char> gather_f16;   // section kind (nrt_refresh.hip SecKind)
   bool refreshed = false;
+  bool split_refreshed = false;  // the refresh also re-split stream3 (fp32-split march)
   ~nrt_mlp();
 };
 

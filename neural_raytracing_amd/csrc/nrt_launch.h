@@ -170,10 +170,10 @@ int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
 int ring_scan_best32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
                      float* thr, unsigned long long* keys, hipStream_t st);
 // ---- fp32-split ring engine (nrt_ring_march3.hip, nrt_ring3.h): the ring32 configurations,
-// from a handle packed by nrt_mlp_create (a refreshed handle's split stream is not re-packed)
+// from a handle packed by nrt_mlp_create or refreshed by nrt_mlp_refresh (which re-splits it)
 constexpr int kRing3Waves = 8;
 inline bool ring3_supported(const nrt_sdf* s) {
-  if (!s->mlp || s->mlp->refreshed) return false;
+  if (!s->mlp || (s->mlp->refreshed && !s->mlp->split_refreshed)) return false;
   const MlpDev& m = s->mlp->host_dev;
   return ring32_supported(s) && (m.ke3 == 64 || m.ke3 == 96);
 }

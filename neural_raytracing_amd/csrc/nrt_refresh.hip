@@ -5,8 +5,9 @@
 // fragment arrays the training kernels read -- FP16 / FP32 A fragments, FP32 W^T fragments,
 // padded biases, out.weight row 0 -- through a per-element index map built once on the host by
 // the same loops as nrt_pack.hip.  The FP32 ring stream is refreshed too (the FP32 march of a
-// training loop runs on it); the FP16 ring / program streams are not, and a refreshed handle
-// refuses those paths (ring_supported, build_program).
+// training loop runs on it), and so is the fp32-split stream (folded, scaled and split into f16
+// halves on the device, k_gather_split); the FP16 ring / program streams are not, and a refreshed
+// handle refuses those paths (ring_supported, build_program).
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -25,10 +26,41 @@ __global__ void k_gather(T* __restrict__ dst, const int* __restrict__ map, int64
   dst[i] = (T)(k < 0 ? 0.f : src[k]);
 }
 
+// per-layer factors of the split stream (nrt_pack.hip): value = (x * fold[l]) * scale[l]
+struct SplitCoef {
+  float fold_w[kMaxLin], fold_b[kMaxLin], scale[kMaxLin];
+};
+// map entries of the split sections: source index | layer << 25 | part << 30 (-1 = padding)
+constexpr int kSplitIdxBits = 25;
+
+// split stream halves (part 0: hi = RNE_f16(v), part 1: lo = RNE_f16(v - hi)) or, BIAS, the
+// scaled f32 biases -- the packer's arithmetic, on the device
+template <bool BIAS>
+__global__ void k_gather_split(void* __restrict__ dst, const int* __restrict__ map, int64_t n,
+                               const float* __restrict__ src, SplitCoef c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int v = map[i];
+  if (v < 0) {
+    if (BIAS) reinterpret_cast<float*>(dst)[i] = 0.f;
+    else reinterpret_cast<_Float16*>(dst)[i] = (_Float16)0.f;
+    return;
+  }
+  const int k = v & ((1 << kSplitIdxBits) - 1), l = (v >> kSplitIdxBits) & 31, part = (v >> 30) & 1;
+  if (BIAS) {
+    reinterpret_cast<float*>(dst)[i] = (src[k] * c.fold_b[l]) * c.scale[l];
+    return;
+  }
+  const float w = (src[k] * c.fold_w[l]) * c.scale[l];
+  const _Float16 hi = (_Float16)w;
+  reinterpret_cast<_Float16*>(dst)[i] = part ? (_Float16)(w - (float)hi) : hi;
+}
+
+enum SecKind { SEC_F32 = 0, SEC_F16 = 1, SEC_SPLIT = 2, SEC_SPLIT_BIAS = 3 };
 struct Section {
   void* dst;
   int64_t n;
-  bool f16;
+  int kind;
 };
 
 // The fragment layouts of nrt_pack.hip, as source indices into [W_0 .. W_{L+1} | b_0 .. b_{L+1}]
@@ -66,14 +98,14 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
     const int c = slot_col[slot];
     return c < 0 ? -1 : (l.hid ? H + c : c);
   };
-  auto begin = [&](void* dst, bool f16) { secs.push_back({dst, (int64_t)map.size(), f16}); };
+  auto begin = [&](void* dst, int kind) { secs.push_back({dst, (int64_t)map.size(), kind}); };
   auto end = [&]() { secs.back().n = (int64_t)map.size() - secs.back().n; };
   for (size_t li = 0; li < ls.size(); ++li) {
     const Ly& l = ls[li];
     const int nrb = (l.R + 31) / 32;
     {  // FP16 A fragments
       const int ks_h = l.hid ? 2 * NB : 0, ks_e = l.enc ? ke / 16 : 0;
-      begin((void*)md.w16[li], true);
+      begin((void*)md.w16[li], SEC_F16);
       for (int s = 0; s < ks_h + ks_e; ++s)
         for (int ib = 0; ib < nrb; ++ib)
           for (int lane = 0; lane < 64; ++lane) {
@@ -88,7 +120,7 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
     }
     {  // FP32 A fragments
       const int ks_h = l.hid ? H / 2 : 0, ks_e = l.enc ? ke / 2 : 0;
-      begin((void*)md.w32[li], false);
+      begin((void*)md.w32[li], SEC_F32);
       for (int s = 0; s < ks_h + ks_e; ++s)
         for (int ib = 0; ib < nrb; ++ib)
           for (int lane = 0; lane < 64; ++lane) {
@@ -101,7 +133,7 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
     if (li + 1 < ls.size()) {  // FP32 W^T fragments
       const int npos = (l.hid ? H : 0) + (l.enc ? ke : 0);
       const int nrbt = (npos + 31) / 32;
-      begin((void*)md.wt32[li], false);
+      begin((void*)md.wt32[li], SEC_F32);
       for (int s = 0; s < H / 2; ++s)
         for (int ib = 0; ib < nrbt; ++ib)
           for (int lane = 0; lane < 64; ++lane) {
@@ -113,28 +145,50 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
           }
       end();
     }
-    begin((void*)md.bias[li], false);  // biases padded to row blocks
+    begin((void*)md.bias[li], SEC_F32);  // biases padded to row blocks
     for (int r = 0; r < nrb * 32; ++r) map.push_back(r < l.R ? (int)(l.boff + r) : -1);
     end();
   }
-  begin((void*)md.wout_row0, false);  // out.weight[0, :]
+  begin((void*)md.wout_row0, SEC_F32);  // out.weight[0, :]
   for (int k = 0; k < H; ++k) map.push_back(idx(ls.back(), 0, k));
   end();
   {  // FP32 ring stream (same walk as the packer)
     std::vector<Ring32Layer> rl;
     for (const Ly& l : ls) rl.push_back({l.R, l.hid, l.enc});
-    begin((void*)md.stream32, false);
+    begin((void*)md.stream32, SEC_F32);
     ring32_walk(rl, H, ke, [&](int li, int row, int pos) {
       const Ly& l = ls[li];
       map.push_back(idx(l, row, pos < H ? pos : col_slot(l, pos - H)));
     });
     end();
   }
-  begin((void*)md.bias32, false);  // [layer][bias16_stride]
+  begin((void*)md.bias32, SEC_F32);  // [layer][bias16_stride]
   for (size_t li = 0; li < ls.size(); ++li)
     for (int r = 0; r < md.bias16_stride; ++r)
       map.push_back(r < ls[li].R ? (int)(ls[li].boff + r) : -1);
   end();
+  // the split stream and its scaled biases (the fp32-split march of a training loop): the
+  // packer's walk, each entry tagged with its layer and half; the pack-time scales stay (they
+  // only keep the lo halves normal, and hi covers |W 2^s| up to 65504)
+  if (n_src < (1 << kSplitIdxBits)) {
+    std::vector<Ring32Layer> rl;
+    for (const Ly& l : ls) rl.push_back({l.R, l.hid, l.enc});
+    begin((void*)md.stream3, SEC_SPLIT);
+    ring3_walk(rl, H, md.ke3, [&](int li, int row, int pos, int part) {
+      const Ly& l = ls[li];
+      int col = -1;
+      if (pos < H) col = pos;
+      else if (pos - H < ke) col = col_slot(l, pos - H);
+      const int k = idx(l, row, col);
+      map.push_back(k < 0 ? -1 : (k | (li << kSplitIdxBits) | (part << 30)));
+    });
+    end();
+    begin((void*)md.bias3, SEC_SPLIT_BIAS);
+    for (size_t li = 0; li < ls.size(); ++li)
+      for (int r = 0; r < md.bias16_stride; ++r)
+        map.push_back(r < ls[li].R ? (int)((ls[li].boff + r) | ((int64_t)li << kSplitIdxBits)) : -1);
+    end();
+  }
 }
 
 }  // namespace
@@ -157,7 +211,7 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
     for (const Section& q : secs) {
       m->gather_dst.push_back(q.dst);
       m->gather_n.push_back(q.n);
-      m->gather_f16.push_back(q.f16 ? 1 : 0);
+      m->gather_f16.push_back((char)q.kind);
     }
   }
   // stage [W_0 .. W_{L+1} | b_0 .. b_{L+1}] from the caller's device tensors
@@ -176,21 +230,35 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
     off += n;
   }
   if ((int64_t)off != m->n_src) { set_error("nrt_mlp_refresh: layer sizes changed"); return NRT_EINVAL; }
+  const MlpDev& md = m->host_dev;
+  const bool fold = m->desc.activation == NRT_ACT_SOFTPLUS;
+  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  SplitCoef coef{};
+  for (int l = 0; l < n_lin && l < kMaxLin; ++l) {
+    coef.fold_w[l] = fold ? (l == 0 ? kLog2e : (l == n_lin - 1 ? kLn2 : 1.f)) : 1.f;
+    coef.fold_b[l] = fold && l < n_lin - 1 ? kLog2e : 1.f;
+    coef.scale[l] = 1.f / md.scale3[l];  // a power of two: exact
+  }
   int64_t moff = 0;
   for (size_t q = 0; q < m->gather_dst.size(); ++q) {
     const int64_t n = m->gather_n[q];
     const dim3 grid((unsigned)((n + 255) / 256)), block(256);
     if (n > 0) {
-      if (m->gather_f16[q])
-        k_gather<_Float16><<<grid, block, 0, st>>>((_Float16*)m->gather_dst[q],
-                                                   m->gather_map + moff, n, m->gather_src);
+      const int kind = m->gather_f16[q];
+      const int* mp = m->gather_map + moff;
+      if (kind == SEC_F16)
+        k_gather<_Float16><<<grid, block, 0, st>>>((_Float16*)m->gather_dst[q], mp, n, m->gather_src);
+      else if (kind == SEC_F32)
+        k_gather<float><<<grid, block, 0, st>>>((float*)m->gather_dst[q], mp, n, m->gather_src);
+      else if (kind == SEC_SPLIT)
+        k_gather_split<false><<<grid, block, 0, st>>>(m->gather_dst[q], mp, n, m->gather_src, coef);
       else
-        k_gather<float><<<grid, block, 0, st>>>((float*)m->gather_dst[q], m->gather_map + moff,
-                                                n, m->gather_src);
+        k_gather_split<true><<<grid, block, 0, st>>>(m->gather_dst[q], mp, n, m->gather_src, coef);
     }
     moff += n;
   }
   if (int rc = check_launch("k_gather")) return rc;
   m->refreshed = true;
+  m->split_refreshed = m->n_src < (1 << kSplitIdxBits);
   return NRT_OK;
 }

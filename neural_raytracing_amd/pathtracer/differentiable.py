@@ -255,6 +255,10 @@ def bsdf_eval(bsdf, it, wo, active):
     if isinstance(bsdf, Conductor):
         refl = local_reflect(it.wi)
         thresh = (refl * wo).sum(dim=-1, keepdim=True) > 0.94
+        # eta carries no gradient, as in the reference: Conductor.eval_and_pdf passes
+        # F.softplus(self.eta) into the @torch.jit.script fresnel_conductor whose eta_r parameter
+        # is annotated `float` (bsdfs.py:327-328, 371), so the scripted call receives a plain number
+        # and its result has requires_grad=False
         fres = fresnel_conductor(it.wi[..., 2], float(F.softplus(bsdf.eta.detach())), 0.0)
         fres = fres.reshape_as(thresh)
         f = torch.where(thresh, fres * bsdf.act(bsdf.specular.to(wo.device)),

@@ -10,6 +10,7 @@ from oracle import pathtracer_ref as R
 from oracle import recipes
 from tests.helpers import copy_mlp, product_mlp_like, seeded
 from tests.helpers import lib_opt as _lib_opt
+from tests.report import report
 
 pytestmark = pytest.mark.gpu
 
@@ -748,8 +749,20 @@ def test_colocate_fov_render_matches_oracle(prec):
                               background=0.5, with_noise=0.0)
     got = got.cpu()
     assert got.shape == want.shape == (64, 64, 3)
+    err = (got - want).abs().amax(-1)
+    # where the pixels past 1e-4 come from: primary-ray hit / step flips at the silhouette
+    # (ulp-level march differences) and the Conductor's (refl . wo) > 0.94 switch (bsdfs.py:371)
+    from tests.test_gpu_configs import _agreement
+    with torch.no_grad():
+        agree, rh, flips, steps = _agreement(
+            mine["shape"], ref["shape"], mine["camera"].rays_tile(0, 0, 64, 64, 64),
+            ref["camera"].sample_positions(R._tile_positions(0, 0, 64), 64))
+    agree = agree.reshape(64, 64)
+    report(f"colocate_fov_render[{prec}]", pixels=err.numel(), hits=int(rh.sum()), flips=flips,
+           step_flips=steps, over_1e4=int((err > 1e-4).sum()),
+           over_1e4_on_agreeing=int((err[agree] > 1e-4).sum()), maxabs=err.max().item())
     if prec == "fp32":
-        close = (got - want).abs().amax(-1) <= 1e-4
+        close = err <= 1e-4
         assert close.float().mean() >= 0.995, (got - want).abs().max()
     else:
         mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
@@ -949,6 +962,11 @@ def test_path_integrator_matches_oracle(prec, w_isect):
     assert torch.equal(mask.cpu(), wmask)
     assert got.shape == want.shape
     err = (got - want).abs().amax(-1)
+    # Path's pixels past 1e-4: a secondary (bounce) ray's hit / step flip or a shadow-ray flip
+    # changes that pixel's whole bounce contribution; reported with the count
+    report(f"path_integrator[{prec},{w_isect}]", pixels=err.numel(), hits=int(wmask.sum()),
+           over_1e4=int((err > 1e-4).sum()), over_1e2=int((err > 1e-2).sum()),
+           maxabs=err.max().item())
     if prec == "fp32":
         assert (err <= 1e-4).float().mean() >= 0.99, err.max()
     else:

@@ -82,8 +82,9 @@ def _march(sdf, rays, primary=True, steps=64, seed=12):
     return it, hit, n32
 
 
-def _intersect_raw(sh, rays, max_steps):
-    """nrt_sdf_intersect (FP32, primary) on a raw handle: (t, hit, p, n, throughput)."""
+def _intersect_raw(sh, rays, max_steps, precision=None):
+    """nrt_sdf_intersect (FP32 unless `precision`, primary) on a raw handle: (t, hit, p, n,
+    throughput)."""
     import ctypes
     from neural_raytracing_amd import _lib
     P, dev = rays.shape[0], rays.device
@@ -95,7 +96,8 @@ def _intersect_raw(sh, rays, max_steps):
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     lib = _lib.load(require_device=True)
     ws = torch.empty(max(lib.nrt_intersect_workspace_bytes(sh, P), 1), dtype=torch.uint8, device=dev)
-    mp = _lib.MarchParams(max_steps, 5e-3, 10.0, 1, 2.2, _lib.NRT_FP32)
+    mp = _lib.MarchParams(max_steps, 5e-3, 10.0, 1, 2.2,
+                          _lib.NRT_FP32 if precision is None else precision)
     _lib.call("nrt_sdf_intersect", sh, _lib.ptr(rays), P, ctypes.byref(mp), _lib.ptr(t),
               _lib.ptr(hit), _lib.ptr(p), _lib.ptr(n), _lib.ptr(raw), _lib.ptr(wi), _lib.ptr(thr),
               _lib.ptr(idx), _lib.ptr(cnt), _lib.ptr(ws), _lib.stream())

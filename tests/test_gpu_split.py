@@ -23,7 +23,7 @@ from oracle import pathtracer_ref as R
 from tests.helpers import lib_opt as _lib_opt
 from tests.report import report
 from tests.test_gpu_configs import _agreement, _camera_rays, _mlp_sdf_pair
-from tests.test_gpu_ring32 import _blob, _compare, _rays
+from tests.test_gpu_ring32 import _blob, _compare, _intersect_raw, _rays
 
 pytestmark = pytest.mark.gpu
 
@@ -213,3 +213,41 @@ def test_split_ragged_ray_counts(n):
         rit, rhit = R.MarchedSDF(sdf=ref, max_steps=64).intersect(rays, primary=True, jitter=jit)
     assert torch.isfinite(it.t).all() and torch.isfinite(it.throughput).all()
     _compare(f"split_ragged[{n}]", it, hit, rit, rhit, flip_frac=max(0.005, 1.0 / n))
+
+
+def test_split_after_device_refresh_matches_fresh_pack():
+    """nrt_mlp_refresh re-splits stream3 / bias3 on the device (fold, scale, hi / lo halves: the
+    packer's arithmetic): a training handle refreshed to new weights marches on k_march3 exactly
+    like a handle packed from them on the host."""
+    import ctypes
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer._handles import train_handle, mlp_handle
+    _, mine = _blob(64, 128, 32, "softplus", seed=13)
+    mlp = mine.shift
+    th = train_handle(mlp)
+    with torch.no_grad():
+        for lin in mlp._linears():
+            lin.weight.add_(0.01 * torch.randn_like(lin.weight))
+            lin.bias.add_(0.01 * torch.randn_like(lin.bias))
+    th2 = train_handle(mlp)  # same handle, refreshed on the device
+    assert th2 is th
+    fresh = mlp_handle(mlp)
+    assert fresh is not th
+    rays = _rays(24, 17, eye=(0.0, 0.2, 1.1)).cuda().reshape(-1, 6).contiguous()
+    c, r, t = (x.detach().cpu().contiguous() for x in (mine.centers, mine.radii, mine.tfs))
+    outs = []
+    for h in (th, fresh):
+        sh = ctypes.c_void_p()
+        _lib.check(_lib.load().nrt_sdf_create_sphere_blob(
+            c.shape[0], c.data_ptr(), r.data_ptr(), t.data_ptr(), 32.0, h.value, ctypes.byref(sh)),
+            "nrt_sdf_create_sphere_blob")
+        try:
+            _lib.profile_enable(True)
+            _lib.profile_reset()
+            outs.append(_intersect_raw(sh, rays, max_steps=64, precision=_lib.NRT_FP32_SPLIT))
+            assert _lib.profile_read("k_march3")[1] == 1, "the split march did not run"
+            _lib.profile_enable(False)
+        finally:
+            _lib.load().nrt_sdf_destroy(sh)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

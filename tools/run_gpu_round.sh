@@ -22,14 +22,18 @@ if [ "$STEP" = all ] || [ "$STEP" = prof ]; then
 fi
 if [ "$STEP" = all ] || [ "$STEP" = pmc ]; then
   rm -rf gpurun_out/pmc
-  SIZE=800 bash tools/pmc.sh k_march16 "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" || exit 1
+  SIZE=800 BENCH_ARGS="--size 800 --steps 1 --warmup 0 --no-cpu-baseline --no-extra-legs" bash tools/pmc.sh k_march32 "FETCH_SIZE" "WRITE_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" || exit 1
 fi
 if [ "$STEP" = all ] || [ "$STEP" = scenes ]; then
   rm -f gpurun_out/scenes.jsonl
-  for SC in colocate dtu nerfle; do
-    timeout -k 10 300 python -u bench.py --scene $SC --steps 3 --warmup 1 >> gpurun_out/scenes.jsonl 2> gpurun_out/scene_$SC.err
-    rc=$?; echo "SCENE $SC EXIT $rc"; [ $rc -eq 0 ] || exit $rc
+  for SC in colocate dtu; do
+    for PREC in fp32 fp32-split fp16; do
+      timeout -k 10 300 python -u bench.py --scene $SC --precision $PREC --steps 3 --warmup 1 >> gpurun_out/scenes.jsonl 2> gpurun_out/scene_$SC.err
+      rc=$?; echo "SCENE $SC $PREC EXIT $rc"; [ $rc -eq 0 ] || exit $rc
+    done
   done
+  timeout -k 10 300 python -u bench.py --scene nerfle --steps 3 --warmup 1 >> gpurun_out/scenes.jsonl 2> gpurun_out/scene_nerfle.err
+  rc=$?; echo "SCENE nerfle EXIT $rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nerfle -o run --output-format csv -- python3 bench.py --scene nerfle --steps 2 --warmup 1 > gpurun_out/prof_nerfle.log 2>&1
   rc=$?; echo "PROF NERFLE EXIT $rc"; [ $rc -eq 0 ] || exit $rc
 fi
