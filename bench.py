@@ -889,7 +889,7 @@ def bench_train(args):
     elapsed = time.perf_counter() - t0
     _lib.profile_enable(False)
     kms = {k: _lib.profile_read(k)[0] / args.steps
-           for k in ("k_intersect", "k_mlp_backward32", "k_mlp_grad_backward32")}
+           for k in ("k_intersect", "k_mlp_backward32", "k_mlp_grad_backward32", "k_wgrad")}
     rays = N * crop * crop
     line = {
         "metric": f"training ray-samples/sec/GPU (nerf_synthetic step, {N}x{crop}x{crop} crop "
@@ -898,12 +898,13 @@ def bench_train(args):
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32" if prec == "fp32" else "fp16 forward / fp32 backward",
+        "dtype": {"fp32": "fp32", "fp16": "fp16 forward / fp32 backward",
+                  "fp32-split": "fp32-split forward (f16 hi/lo MFMA) / fp32 backward"}[prec],
         "data": "synthetic (seeded random-init weights, random target crops)",
         "config": {"workload": "forward (fused march + scan) + backward (MLP backward, SDF-normal "
                                "double backward, shading autograd) + AdamW",
                    "views": N, "crop": crop, "image": [size, size],
-                   "samples_per_ray": args.samples},
+                   "samples_per_ray": args.samples, "precision": prec},
         "kernel_ms_per_step": kms, "final_loss": float(loss),
     }
     if not args.no_cpu_baseline:

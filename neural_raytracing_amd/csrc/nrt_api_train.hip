@@ -424,6 +424,10 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   return w;
 }
 
+}  // namespace
+// (outside the anonymous namespace: the HIP runtime could not find k_wgrad's device symbol under
+// internal linkage -- "Cannot find Symbol with name: _ZN3nrt12_GLOBAL__N_17k_wgrad...")
+
 // Split-K weight gradients.  dW = dZ^T In has a small output (R x C <= 256 x 550) and a long K
 // (the batch, ~10^4-10^5): the batch is cut into S slices, one wave computes one 64 x 64 output
 // tile of one slice on exact-f32 MFMA, and the slice partials are summed in slice order
@@ -443,60 +447,80 @@ struct GemmCtx {
 };
 
 // part[s][r][c] = sum over the rows m of slice s of dZ[m][r] In[m][c] (row-major dZ [M][R],
-// In [M][ldi] from column c0i).  v_mfma_f32_32x32x2_f32 (exact f32, an fma chain) with a 2 x 2
-// grid of 32x32 accumulators: lane (i = l & 31, h = l >> 5) loads dZ[m + h][r0 + 32a + i] (the A
-// operand, dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row segments per half-wave, eight
-// k-steps of loads in flight; out-of-range rows / columns load zeros.
+// In [M][ldi]).  One block of kWgradWaves waves per (64 x 64 output tile, slice): wave w takes
+// the slice's groups of 16 rows w, w + kWgradWaves, ... on v_mfma_f32_32x32x2_f32 (exact f32,
+// an fma chain) with a 2 x 2 grid of 32x32 accumulators -- lane (i = l & 31, h = l >> 5) loads
+// dZ[m + h][r0 + 32a + i] (the A operand, dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row
+// segments per half-wave -- then the waves' accumulators are summed in wave order through LDS
+// (deterministic).  Several waves per SIMD hide the load latency.
 template <int = 0>
-__global__ void __launch_bounds__(64 * kWgradWaves) k_wgrad(
+__global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_per_eu(3))) k_wgrad(
     const float* __restrict__ dZ, int R, const float* __restrict__ In, int ldi, int C, int64_t M,
     int tiles_c, int n_tiles, int64_t slice_rows, float* __restrict__ part) {
   typedef float f16v_ __attribute__((ext_vector_type(16)));
-  const int tile = blockIdx.x * kWgradWaves + (threadIdx.x >> 6);
-  if (tile >= n_tiles) return;
+  __shared__ float red[kWgradWaves - 1][16][64];
+  const int tile = blockIdx.x, w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
   const int r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
   const int64_t m0 = (int64_t)blockIdx.y * slice_rows;
   const int64_t m1 = std::min<int64_t>(M, m0 + slice_rows);
-  const bool ra = r0 + i < R, rb = r0 + 32 + i < R, ca = c0 + i < C, cb = c0 + 32 + i < C;
-  f16v_ acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+  f16v_ acc[4] = {};
   constexpr int U = 8;  // k-steps (2 rows each) per group
-  for (int64_t m = m0; m < m1; m += 2 * U) {
+  // clamped row / column indices: loads are unconditional; a row past the slice is zeroed in the
+  // A operand (its B values come from a real, finite row), clamped columns / rows feed only
+  // outputs that are never stored
+  const int ia = std::min(r0 + i, R - 1), ib = std::min(r0 + 32 + i, R - 1);
+  const int ja = std::min(c0 + i, C - 1), jb = std::min(c0 + 32 + i, C - 1);
+  for (int64_t m = m0 + (int64_t)w * 2 * U; m < m1; m += (int64_t)kWgradWaves * 2 * U) {
     float a0[U], a1[U], b0[U], b1[U];
+    int ok = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = m + 2 * u + h;
-      const bool ok = row < m1;
-      const float* zr = dZ + row * R + r0 + i;
-      const float* ir = In + row * ldi + c0 + i;
-      a0[u] = ok && ra ? zr[0] : 0.f;
-      a1[u] = ok && rb ? zr[32] : 0.f;
-      b0[u] = ok && ca ? ir[0] : 0.f;
-      b1[u] = ok && cb ? ir[32] : 0.f;
+      ok |= row < m1 ? (1 << u) : 0;
+      const int64_t rc = row < m1 ? row : m1 - 1;
+      const float* zr = dZ + rc * R;
+      const float* ir = In + rc * ldi;
+      a0[u] = zr[ia]; a1[u] = zr[ib]; b0[u] = ir[ja]; b1[u] = ir[jb];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b0[u], acc00, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[u], b1[u], acc01, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b0[u], acc10, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[u], b1[u], acc11, 0, 0, 0);
+      const bool o = (ok >> u) & 1;
+      const float x0 = o ? a0[u] : 0.f, x1 = o ? a1[u] : 0.f;
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, b0[u], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, b1[u], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, b0[u], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, b1[u], acc[3], 0, 0, 0);
     }
   }
-  // 32x32 accumulator: register q holds row (q & 3) + 8 (q >> 2) + 4 h, column i
-  float* out = part + (size_t)blockIdx.y * R * C;
+  // one accumulator at a time through a 12 KiB LDS buffer (keeps LDS small and occupancy up)
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int rr = (q & 3) + 8 * (q >> 2) + 4 * h;
-    const int ra_ = r0 + rr, rb_ = r0 + 32 + rr;
-    if (ra_ < R) {
-      if (ca) out[(size_t)ra_ * C + c0 + i] = acc00[q];
-      if (cb) out[(size_t)ra_ * C + c0 + 32 + i] = acc01[q];
+  for (int t = 0; t < 4; ++t) {
+    if (w > 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) red[w - 1][q][lane] = acc[t][q];
     }
-    if (rb_ < R) {
-      if (ca) out[(size_t)rb_ * C + c0 + i] = acc10[q];
-      if (cb) out[(size_t)rb_ * C + c0 + 32 + i] = acc11[q];
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int v = 0; v < kWgradWaves - 1; ++v)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[t][q] += red[v][q][lane];
     }
+    __syncthreads();
   }
+  if (w != 0) return;
+  // 32x32 accumulator: register q holds row (q & 3) + 8 (q >> 2) + 4 h, column i; acc[2a + b]
+  // is rows 32a.., columns 32b..
+  float* out = part + (size_t)blockIdx.y * R * C;
+  const bool cok[2] = {c0 + i < C, c0 + 32 + i < C};
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int rr = r0 + 32 * (t >> 1) + (q & 3) + 8 * (q >> 2) + 4 * h;
+      if (rr < R && cok[t & 1]) out[(size_t)rr * C + c0 + 32 * (t & 1) + i] = acc[t][q];
+    }
 }
 
 // dW[r][c0 + c] = sum_{s < slots} part[s][r][c]
@@ -516,14 +540,15 @@ __global__ void k_split_reduce(const float* __restrict__ part, int slots, int R,
 int grad_gemm(const GemmCtx& g, const float* dZ, int R, const float* In, int C, int64_t M,
               float* dW, int ldw, int c0) {
   const int tiles_r = (R + 63) / 64, tiles_c = (C + 63) / 64, n_tiles = tiles_r * tiles_c;
-  // slices: about 16 waves per CU over the tiles, at least kSliceRows batch rows each
-  int64_t S = std::max<int64_t>(1, (256 * 16 + n_tiles - 1) / n_tiles);
+  // slices: about 3 blocks (12 waves, the kernel's occupancy) per CU over the tiles, at least
+  // kSliceRows batch rows each -- fewer slices, less partial-sum traffic for k_split_reduce
+  int64_t S = std::max<int64_t>(1, (256 * 3 + n_tiles - 1) / n_tiles);
   S = std::min<int64_t>(S, kSplitMax);
   S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
   int64_t slice_rows = (M + S - 1) / S;
   slice_rows = (slice_rows + 15) / 16 * 16;  // whole k-step groups
   S = std::max<int64_t>(1, (M + slice_rows - 1) / slice_rows);
-  const dim3 grid((unsigned)((n_tiles + kWgradWaves - 1) / kWgradWaves), (unsigned)S);
+  const dim3 grid((unsigned)n_tiles, (unsigned)S);
   ProfScope prof("k_wgrad", g.st);
   k_wgrad<><<<grid, dim3(64 * kWgradWaves), 0, g.st>>>(dZ, R, In, C, C, M, tiles_c, n_tiles,
                                                       slice_rows, g.part);
@@ -533,6 +558,8 @@ int grad_gemm(const GemmCtx& g, const float* dZ, int R, const float* In, int C, 
                                                                             dW, ldw, c0);
   return check_launch("k_split_reduce");
 }
+
+namespace {
 
 // db[r] = sum_m dZ[m][r] (row-major dZ [M][R]) in a fixed order: per chunk of rows a partial
 // column sum (4 row groups x 64 consecutive columns per block, coalesced), then the partials in
