@@ -380,6 +380,11 @@ int nrt_profile_evals(uint64_t* evals);
  *   "shade_program" 1  FP16 shading MLPs in one fused program kernel (0: per component)
  *   "nerf_fused"    1  FP16 NeRFLE in the fused k_nerfle16 (0: separate MLP launches)
  *   "max_waves"     0  waves per block (1..4) of the per-wave kernels (0: 4)
+ *   "shade_ring"    1  FP32 / fp32-split shading MLPs (LightField 10x256, spatial weights 16x256,
+ *                      NeuralBSDF 6x96) on the row-program ring kernels k_light32 / k_bsdf32 and
+ *                      k_light3 / k_bsdf3 (0: the per-wave k_shade_direct)
+ *   "normals_ring"  1  after an FP32 / fp32-split ring march, normals by forward mode on the same
+ *                      engine (k_normal32 / k_normal3; 0: the per-wave FP32 backward k_sdf_grad)
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
 int nrt_set_option(const char* name, int64_t value);

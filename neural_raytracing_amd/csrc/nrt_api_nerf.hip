@@ -274,6 +274,21 @@ constexpr int kNerfKC1 = kNerfMaxF / 4;   // k-steps per chunk of the first MLP 
 constexpr int kNerfKC2 = kNerfMaxF / 2;   // ... of the second MLP (2 row blocks)
 constexpr int kNerfL1 = 5, kNerfL2 = 8, kNerfSkip = 3;  // nerf.py:162-172 (SkipConnMLP skip 3)
 
+// leaky_relu on packed halves (ring::kact's pk_mul + pk_max): act(enc) from the encoding's own
+// FP16 values instead of a second sin / cos pass
+__device__ __forceinline__ h8 leaky_h8(const h8& v) {
+  const ring::h2 k = {(_Float16)0.01f, (_Float16)0.01f};
+  h8 f;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const ring::h2 x = {v[j], v[j + 1]};
+    const ring::h2 r = __builtin_elementwise_max(x, x * k);
+    f[j] = r[0];
+    f[j + 1] = r[1];
+  }
+  return f;
+}
+
 // acc[ib] += W[ib] * [b1[0..KS1), b2[0..KS2)] over chunks of KC k-steps
 template <int NB, int KS1, int KS2, int KC, class Eng, int N1, int N2>
 __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
@@ -324,7 +339,7 @@ __device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, float x0,
   for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
   nerf_layer<NB, NE, 0, kNerfKC1>(E, acc, enc, enc);
 #pragma unroll
-  for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<ACT_LEAKY>(basis, s, NE - 1, h, x0, x1, x2);
+  for (int s = 0; s < NE; ++s) enc[s] = leaky_h8(enc[s]);  // act(enc) from the same halves
 #pragma unroll
   for (int i = 0; i < L; ++i) {
     ring::kact<NB, ACT_LEAKY>(acc, hv);
@@ -344,6 +359,20 @@ __device__ __forceinline__ h8 h8_of(const float (&v)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = (_Float16)v[j];
   return f;
+}
+
+// v (8 f32) -> FP16 halves hi = RNE(v) and residuals lo = RNE(v - hi) (ring3::split2: one
+// v_fma_mix per residual instead of a convert back and a subtract)
+__device__ __forceinline__ void split_h8(const float (&v)[8], h8& hi, h8& lo) {
+  ring3::u4v h, l;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t a, b;
+    ring3::split2(v[2 * q], v[2 * q + 1], a, b);
+    h[q] = a; l[q] = b;
+  }
+  hi = __builtin_bit_cast(h8, h);
+  lo = __builtin_bit_cast(h8, l);
 }
 
 template <int WV>
@@ -380,24 +409,17 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     h8 e[9], ea[9], lo[7];
 #pragma unroll
     for (int tt = 0; tt < 6; ++tt) {
-      float v[8], va[8], vl[8];
+      float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[j] = o[tt >> 1][8 * (tt & 1) + j];
-        va[j] = act_fwd<true>(v[j], ACT_LEAKY);
-        vl[j] = v[j] - (float)(_Float16)v[j];
-      }
-      e[2 + tt] = h8_of(v); ea[2 + tt] = h8_of(va); lo[tt] = h8_of(vl);
+      for (int j = 0; j < 8; ++j) v[j] = o[tt >> 1][8 * (tt & 1) + j];
+      split_h8(v, e[2 + tt], lo[tt]);
+      ea[2 + tt] = leaky_h8(e[2 + tt]);
     }
     {
-      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, va[8], vl[8];
+      float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (h == 0) { v[0] = dx; v[1] = dy; v[2] = dz; v[3] = lx; v[4] = ly; v[5] = lz; }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        va[j] = act_fwd<true>(v[j], ACT_LEAKY);
-        vl[j] = v[j] - (float)(_Float16)v[j];
-      }
-      e[8] = h8_of(v); ea[8] = h8_of(va); lo[6] = h8_of(vl);
+      split_h8(v, e[8], lo[6]);
+      ea[8] = leaky_h8(e[8]);
     }
     // projections x @ B (utils.py:37-40) as hi*hi + lo(A)*hi + hi*lo(x): FP32-accurate
     f16v pq;
@@ -416,15 +438,14 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     // rows q = (reg & 3) + 8 (reg >> 2) + 4h: regs 0..3 -> q = 4h + jj, regs 4..7 -> 8 + 4h + jj
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      float v[8], va[8];
+      float v[8];
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         v[2 * jj] = __sinf(pq[4 * s2 + jj]);
         v[2 * jj + 1] = __cosf(pq[4 * s2 + jj]);
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) va[j] = act_fwd<true>(v[j], ACT_LEAKY);
-      e[s2] = h8_of(v); ea[s2] = h8_of(va);
+      e[s2] = h8_of(v);
+      ea[s2] = leaky_h8(e[s2]);
     }
     // the second MLP (nerf.py:168-172: 8 x 64, 70 -> 3)
     constexpr int NB = 2;

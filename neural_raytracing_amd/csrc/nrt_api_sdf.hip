@@ -239,6 +239,9 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   if (ring16 && option(OPT_NORMALS16) != 0) {
     ProfScope prof("k_normal16", st);
     if (int rc = ring_normals(s, idx, cnt, P, raw_n, n, p, a->epsilon, st)) return rc;
+  } else if (ring32 && option(OPT_NORMALS_RING) != 0) {
+    // forward mode on the FP32 / split ring engine of the march (k_normal32 / k_normal3)
+    if (int rc = ring_normals32(s, idx, cnt, P, raw_n, n, p, a->epsilon, ring3, st)) return rc;
   } else if (int rc = launch_grad(s, p, idx, cnt, P, raw_n, n, p, a->epsilon, ws, st)) {
     return rc;
   }

@@ -97,7 +97,9 @@ int nrt_bsdf_destroy(nrt_bsdf* b) {
 namespace {
 int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                       const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
-                      const float* lscale, float* rgb, float* weights_out, bool f16, hipStream_t st) {
+                      const float* lscale, float* rgb, float* weights_out, int precision,
+                      hipStream_t st) {
+  const bool f16 = precision == NRT_FP16;
   int hidden = 32, ke = 16;
   auto upd = [&](const nrt_mlp* m) {
     if (!m) return;
@@ -111,6 +113,13 @@ int shade_direct_impl(const nrt_bsdf* b, const nrt_light* l, const float* p, con
   // their shapes (NRT_NO_PROGRAM keeps the per-wave register path)
   if (f16 && option(OPT_SHADE_PROGRAM) != 0) {
     const int rc = shade_program(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out, st);
+    if (rc != NRT_EUNSUPPORTED) return rc;
+  }
+  // FP32 / fp32-split: the row-program ring kernels (nrt_shade_ring.hip) for the reference's
+  // shading MLP shapes
+  if (!f16 && option(OPT_SHADE_RING) != 0) {
+    const int rc = shade_ring(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out,
+                              precision, st);
     if (rc != NRT_EUNSUPPORTED) return rc;
   }
   LdsPlan lp = plan_lds(hidden, ke, 64, f16, false);
@@ -141,7 +150,7 @@ int nrt_shade_direct(const nrt_bsdf* b, const nrt_light* l, const float* p, cons
   }
   if (P == 0) return NRT_OK;
   return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, nullptr, rgb, weights_out,
-                           precision == NRT_FP16, (hipStream_t)stream);
+                           precision, (hipStream_t)stream);
 }
 
 // workspace: shadow rays [P,6] | max_t [P] | visible [P] | occ inputs [P,5] | occ out [P,3] |
@@ -199,7 +208,8 @@ int shade_shadowed_impl(const char* who, const nrt_bsdf* b, const nrt_light* l, 
   k_light_scale<><<<grid, block, 0, st>>>(hit_count, vis, occ ? occ_out : nullptr,
                                           occ ? occ->desc.out : 1, lscale);
   if (int rc = check_launch("k_light_scale")) return rc;
-  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out, f16, st);
+  return shade_direct_impl(b, l, p, n, wi, hit_idx, hit_count, P, lscale, rgb, weights_out,
+                           precision, st);
 }
 }  // namespace
 

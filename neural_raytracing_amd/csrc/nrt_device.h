@@ -120,6 +120,29 @@ struct ProgDev {
   ProgMlp mlp[kMaxProgMlp];
 };
 
+// A "row program" (nrt_shade_ring.h): shading MLPs evaluated one after another per 16-ray tile by
+// the FP32 / fp32-split ring engines; concatenated weight streams, a chunk table driving the
+// LDS-DMA, and biases / split scales / bases copied to LDS.
+struct RProgMlp {
+  int L, skip, F, out;
+  int bias_off;      // floats into RProgDev::tables (layer stride bstride)
+  int bstride;
+  int basis_off;     // float4 index into RProgDev::basis
+  int scale_off;     // floats into RProgDev::tables: 2^-s per layer (split; 1 for FP32)
+};
+struct RProgDev {
+  const void* stream;      // all MLPs' streams, in evaluation order
+  int stream_bytes;
+  const int* chunks;       // [n_chunks][2]: KiB offset, KiB count, in evaluation order
+  int n_chunks;
+  const float* tables;     // biases | scales
+  int table_floats;
+  const float4* basis;
+  int basis_q;
+  int n_mlp;
+  RProgMlp mlp[kMaxProgMlp];
+};
+
 struct SdfDev {
   int kind;         // 0 unit sphere, 1 MLP, 2 sphere blob (+ optional shift MLP)
   int n_spheres;
@@ -1500,9 +1523,20 @@ __device__ __forceinline__ void seg2(const float4* A, const float (&B)[NBV], f4v
   seg2<NQ, P0, BO>(A, B, a0, a1, [](int) {});
 }
 
-// One SkipConnMLP evaluation (output row 0) for the wave's 16 rays, every lane of a ray gets
-// the value.  Every wave of the block must call it the same number of times.
-template <int KH, int KE, int WV, int ACT>
+// forward-mode activation (TAN): the lane's column is 4 ray + comp, comp 0 the value
+// pre-activation z, comps 1..3 the tangent dz/dx_{comp-1}; every lane takes its ray's z from the
+// quad leader and returns act(z) (comp 0) or act'(z) dz (torch's backward formulas, act_bwd)
+template <int ACT>
+__device__ __forceinline__ float act_tan32(float z, bool value) {
+  const float zv = ring::quad_leader(z);
+  return value ? act<ACT>(zv) : act_bwd(zv, ACT) * z;
+}
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 16 columns, every lane of a column
+// gets its value.  Columns are rays, or (TAN) 4 rays x (value, d/dx, d/dy, d/dz): forward-mode
+// gradient, tangent columns take the encoding's derivatives as input and no bias (as ring::eval).
+// Every wave of the block must call it the same number of times.
+template <int KH, int KE, int WV, int ACT, bool TAN = false>
 __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, float x0, float x1,
                                       float x2) {
   using En = Engine<KH, KE, WV>;
@@ -1510,6 +1544,8 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   constexpr int NC = KH / 8;  // 32-row chunks per layer
   static_assert(QH >= 8, "hidden chunks must have a quad per pending activation");
   const int g = E.lane >> 4;
+  const int comp = TAN ? (E.lane & 3) : 0;
+  const bool value = comp == 0;
   const int F = m.freqs, L = m.n_hidden, SK = m.skip;
   // encoding: k-step e of lane group g is slot 4 e + g: sin / cos of projection (4e + g) / 2
   // (utils.py:37-40, same fma order and accurate sincosf as the FP32 slab path), then x, zeros
@@ -1517,7 +1553,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     const int slot = 4 * e + g;
-    float v = 0.f;
+    float v = 0.f, tv = 0.f;  // value and (TAN) d/dx_{comp-1}
     if (slot < 2 * F) {
       const float4 b = E.lbasis[slot >> 1];
       float pr = x0 * b.x;
@@ -1526,16 +1562,34 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
       float sn, cs;
       sincosf(pr, &sn, &cs);
       v = (slot & 1) ? cs : sn;
+      if (TAN) {
+        const float bk = comp == 1 ? b.x : comp == 2 ? b.y : b.z;
+        tv = (slot & 1) ? -sn * bk : cs * bk;
+      }
     } else if (slot == 2 * F) {
       v = x0;
+      tv = comp == 1 ? 1.f : 0.f;
     } else if (slot == 2 * F + 1) {
       v = x1;
+      tv = comp == 2 ? 1.f : 0.f;
     } else if (slot == 2 * F + 2) {
       v = x2;
+      tv = comp == 3 ? 1.f : 0.f;
     }
-    eraw[e] = v;
-    eact[e] = act<ACT>(v);
+    if (TAN && !value) {
+      eraw[e] = tv;
+      eact[e] = act_bwd(v, ACT) * tv;
+    } else {
+      eraw[e] = v;
+      eact[e] = act<ACT>(v);
+    }
   }
+  const float bmask = value ? 1.f : 0.f;
+  auto bias = [&](int layer, int sb) {
+    f4v b = E.bias_at(layer, sb);
+    if (TAN) b *= bmask;
+    return b;
+  };
   auto chunk_q = [&](int i) {  // quads of hidden layer i's chunks (i == L: the out layer)
     if (i >= L) return QH;
     return 2 * QH + ((i != L - 1 && i % SK == 0) ? 2 * QE : 0);
@@ -1548,7 +1602,8 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   auto retire1 = [&](int ib, int k) {  // element k (< 8) of chunk ib
     const int r = k & 3;
     float& d = dst[8 * ib + k];
-    d = act<ACT>(k < 4 ? pend0[r] : pend1[r]);
+    if (TAN) d = act_tan32<ACT>(k < 4 ? pend0[r] : pend1[r], value);
+    else d = act<ACT>(k < 4 ? pend0[r] : pend1[r]);
     asm volatile("" : "+v"(d));
   };
   auto retire = [&](int ib) {
@@ -1559,7 +1614,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
 #pragma unroll
   for (int ib = 0; ib < NC; ++ib) {
     const float4* A = E.begin(2 * QE, ib + 1 < NC ? 2 * QE : chunk_q(0), false);
-    f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
+    f4v a0 = bias(0, 2 * ib), a1 = bias(0, 2 * ib + 1);
     if (ib > 0) retire(ib - 1);
     seg2<QE, 0, 0>(A, eraw, a0, a1);
     pend0 = a0; pend1 = a1;
@@ -1575,7 +1630,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
       const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
-      f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
+      f4v a0 = bias(1 + i, 2 * ib), a1 = bias(1 + i, 2 * ib + 1);
       // the previous chunk's activations: one per quad over the first 8 quads (QH >= 8)
       seg2<QH, 0, 0>(A, src, a0, a1, [&](int u) {
         if (ib > 0 && u < 8) retire1(ib - 1, u);
@@ -1589,7 +1644,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
   // out layer (neural_blocks.py:86): one 16-row sub-block, two half chains (k-steps of even /
   // odd quads) so consecutive MFMAs are independent; row 0 of ray j sits in register 0 of lane j
   const float4* A = E.begin(QH, 2 * QE, true);
-  f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+  f4v o0 = bias(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
   {
     float4 w0 = A[0], w1 = A[64];
 #pragma unroll

@@ -49,6 +49,16 @@ struct nrt_prog {
   ~nrt_prog() { if (buf) (void)hipFree(buf); }
 };
 
+// A row program (RProgDev) for the FP32 / fp32-split shading kernels (nrt_shade_ring.hip), built on
+// first use from the host copies of the MLPs' weights.
+struct nrt_rprog {
+  nrt::RProgDev d{};
+  void* buf = nullptr;
+  bool built = false;    // build attempted
+  bool ok = false;       // false: some MLP has a shape without a compiled kernel
+  ~nrt_rprog() { if (buf) (void)hipFree(buf); }
+};
+
 struct nrt_sdf {
   nrt::SdfDev host_dev;
   nrt::SdfDev* dev = nullptr;
@@ -89,6 +99,7 @@ struct nrt_light {
   nrt::LightDev* dev = nullptr;
   const nrt_mlp* mlp = nullptr;
   nrt_prog prog;          // [light field MLP]
+  mutable nrt_rprog rprog[2];  // FP32, fp32-split: [light field MLP]
 };
 
 struct nrt_bsdf {
@@ -97,6 +108,7 @@ struct nrt_bsdf {
   std::vector<const nrt_mlp*> mlps;
   const nrt_mlp* spatial = nullptr;
   nrt_prog prog;          // [spatial] + neural components, in component order
+  mutable nrt_rprog rprog[2];  // FP32, fp32-split: same order
 };
 
 namespace nrt {

@@ -440,6 +440,10 @@ struct RingPol32 {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
     return d + ring32::eval<KH, KE, WV, ACT>(E, m, x, y, z);
   }
+  // forward-mode column value (ring32::eval TAN): 4 rays x (value, d/dx, d/dy, d/dz)
+  __device__ __forceinline__ static float tan(Eng& E, const MlpDev& m, float x, float y, float z) {
+    return ring32::eval<KH, KE, WV, ACT, true>(E, m, x, y, z);
+  }
   __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
 };
 
@@ -455,6 +459,9 @@ struct RingPol3 {
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
     return d + ring3::eval<KH, KQ, WV, ACT>(E, m, x, y, z);
+  }
+  __device__ __forceinline__ static float tan(Eng& E, const MlpDev& m, float x, float y, float z) {
+    return ring3::eval<KH, KQ, WV, ACT, true>(E, m, x, y, z);
   }
   __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
 };
@@ -664,6 +671,49 @@ __global__ void __launch_bounds__(64 * WV, 1) k_sdf_eval32r(NRT_MARCH_ARGS) {
 }
 #undef NRT_MARCH_PASS
 #undef NRT_MARCH_ARGS
+
+// FP32 / fp32-split SDF normals on the hit list (sdfs.py:152-158 with the autograd normal of
+// sdfs.py:184-197) by forward mode on the ring32 / ring3 engines: a 16-column tile = 4 rays x
+// (value, d/dx, d/dy, d/dz), so one wave-evaluation yields 4 gradients at the MFMA cost of 16
+// value evaluations.  Same outputs as k_normal16 / k_sdf_grad: raw gradient (sphere blobs
+// analytic + the shift MLP's), normalize(g, 1e-6), p += 5 eps n.  Blocks stride over the
+// device-counted hit list; the loop bound is block-uniform.
+template <class Pol>
+__global__ void __launch_bounds__(64 * Pol::WAVES, 1) k_normal_r(
+    const SdfDev s, const MlpDev m, const int32_t* __restrict__ index,
+    const int32_t* __restrict__ count, int64_t M, float* __restrict__ grad,
+    float* __restrict__ n_out, float* __restrict__ p_io, float offset_eps) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  constexpr int WV = Pol::WAVES;
+  const int64_t total = count ? (int64_t)(*(const NRT_GLOBAL int32_t*)count) : M;
+  const int64_t per_block = 4 * WV;
+  if ((int64_t)blockIdx.x * per_block >= total) return;  // whole block, before the ring starts
+  typename Pol::Eng E;
+  Pol::init(E, s, m, smem_c);
+  const int lane = E.lane, comp = lane & 3;
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < total; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 4 * E.wv + ((lane & 15) >> 2);
+    const bool valid = i < total;
+    const int64_t ii = valid ? i : total - 1;
+    const int64_t idx = index ? (int64_t)index[ii] : ii;
+    const float x = p_io[idx * 3], y = p_io[idx * 3 + 1], z = p_io[idx * 3 + 2];
+    const float v = Pol::tan(E, m, x, y, z);
+    const float gx = __shfl(v, lane + 1), gy = __shfl(v, lane + 2), gz = __shfl(v, lane + 3);
+    if (valid && lane < 16 && comp == 0) {
+      float g[3] = {0.f, 0.f, 0.f};
+      if (s.kind == 2) spheres_grad(s, x, y, z, g);
+      g[0] += gx; g[1] += gy; g[2] += gz;
+      if (grad) { grad[idx * 3] = g[0]; grad[idx * 3 + 1] = g[1]; grad[idx * 3 + 2] = g[2]; }
+      float nx = g[0], ny = g[1], nz = g[2];
+      normalize3(nx, ny, nz, 1e-6f);
+      n_out[idx * 3] = nx; n_out[idx * 3 + 1] = ny; n_out[idx * 3 + 2] = nz;
+      p_io[idx * 3] = x + (nx * offset_eps) * 5.f;
+      p_io[idx * 3 + 1] = y + (ny * offset_eps) * 5.f;
+      p_io[idx * 3 + 2] = z + (nz * offset_eps) * 5.f;
+    }
+  }
+  Pol::finish(E);
+}
 
 // coarse-scan argmin index of each ray from the ring march's 64-bit keys ([ordered min | idx])
 template <int = 0>

@@ -24,6 +24,8 @@ enum Option {
   OPT_SHADE_PROGRAM,   // "shade_program"
   OPT_NERF_FUSED,      // "nerf_fused"
   OPT_MAX_WAVES,       // "max_waves"
+  OPT_SHADE_RING,      // "shade_ring"
+  OPT_NORMALS_RING,    // "normals_ring"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -183,6 +185,8 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
                 int32_t* cnt, unsigned long long* keys, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
 inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
+int ring_normals32(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
+                   float* n, float* p_io, float eps, bool split, hipStream_t st);
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
                  float* n, float* p_io, float eps, hipStream_t st);
 
@@ -197,5 +201,11 @@ int build_bsdf_program(nrt_bsdf* b);
 int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                   const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
                   const float* lscale, float* rgb, float* weights_out, hipStream_t st);
+
+// ---- FP32 / fp32-split shading on the row-program ring engines (nrt_shade_ring.hip) ----
+int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out);
+int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
+               const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+               const float* lscale, float* rgb, float* weights_out, int precision, hipStream_t st);
 
 }  // namespace nrt

@@ -210,14 +210,40 @@ __device__ __forceinline__ void seg(const float4* A, const u4v (&Bh)[NBV], const
   }
 }
 
-// One SkipConnMLP evaluation (output row 0) for the wave's 16 rays; every lane of a ray gets the
-// value.  Every wave of the block must call it the same number of times.
-template <int KH, int KQ, int WV, int ACT>
+// forward-mode activation (TAN, columns 4 ray + comp as ring32::eval): act(z) on the value column,
+// act'(z) dz on the tangent columns, z from the quad leader.  Softplus in the log2 fold:
+// d log2(1 + 2^z) / dz = 1 / (1 + 2^-z), and the fold's units carry through the tangent unchanged.
+template <int ACT>
+__device__ __forceinline__ float act_tan(float z, bool value) {
+  const float zv = ring::quad_leader(z);
+  if (ACT == ACT_SOFTPLUS) {
+    const float e = __builtin_amdgcn_exp2f(-fabsf(zv));
+    const float sig = (zv >= 0.f ? 1.f : e) * __builtin_amdgcn_rcpf(1.f + e);
+    return value ? act<ACT>(zv) : sig * z;
+  }
+  return value ? act<ACT>(zv) : act_bwd(zv, ACT) * z;
+}
+// tangent of the encoding's activation (skip-layer inputs) at raw value v, raw tangent t
+template <int ACT>
+__device__ __forceinline__ float act_enc_tan(float v, float t) {
+  if (ACT == ACT_SOFTPLUS) {
+    // d log2(1 + 2^(v log2e)) / dv = log2e sigmoid(v)
+    return 1.4426950408889634f * t * __builtin_amdgcn_rcpf(1.f + __expf(-v));
+  }
+  return act_bwd(v, ACT) * t;
+}
+
+// One SkipConnMLP evaluation (output row 0) for the wave's 16 columns; every lane of a column gets
+// the value.  Columns are rays, or (TAN) 4 rays x (value, d/dx, d/dy, d/dz) as ring32::eval.
+// Every wave of the block must call it the same number of times.
+template <int KH, int KQ, int WV, int ACT, bool TAN = false>
 __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, float x0, float x1,
                                       float x2) {
   constexpr int NC = KH;  // 32-row chunks per hidden layer (= k-steps of the next layer)
   static_assert(KH == 4 || KH == 8, "hidden 128 or 256");
   const int g = E.lane >> 4;
+  const int comp = TAN ? (E.lane & 3) : 0;
+  const bool value = comp == 0;
   const int F = m.freqs, L = m.n_hidden, SK = m.skip;
   // encoding: element e of k-step v in lane group g is slot 32 v + 8 g + e -- sin / cos of
   // projection slot / 2 (utils.py:37-40, same fma order and accurate sincosf as the FP32 ring),
@@ -227,11 +253,11 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   for (int v = 0; v < KQ; ++v) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float r[2];
+      float r[2], tr[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int slot = 32 * v + 8 * g + 2 * q + t;
-        float val = 0.f;
+        float val = 0.f, tv = 0.f;
         if (slot < 2 * F) {
           const float4 b = E.lbasis[slot >> 1];
           float pr = x0 * b.x;
@@ -240,20 +266,35 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
           float sn, cs;
           sincosf(pr, &sn, &cs);
           val = t ? cs : sn;
+          if (TAN) {
+            const float bk = comp == 1 ? b.x : comp == 2 ? b.y : b.z;
+            tv = t ? -sn * bk : cs * bk;
+          }
         } else if (slot == 2 * F) {
           val = x0;
+          tv = comp == 1 ? 1.f : 0.f;
         } else if (slot == 2 * F + 1) {
           val = x1;
+          tv = comp == 2 ? 1.f : 0.f;
         } else if (slot == 2 * F + 2) {
           val = x2;
+          tv = comp == 3 ? 1.f : 0.f;
         }
         r[t] = val;
+        tr[t] = tv;
       }
       uint32_t hi, lo;
-      split2(r[0], r[1], hi, lo);
-      erh[v][q] = hi; erl[v][q] = lo;
-      split2(act_enc<ACT>(r[0]), act_enc<ACT>(r[1]), hi, lo);
-      eah[v][q] = hi; eal[v][q] = lo;
+      if (TAN && !value) {
+        split2(tr[0], tr[1], hi, lo);
+        erh[v][q] = hi; erl[v][q] = lo;
+        split2(act_enc_tan<ACT>(r[0], tr[0]), act_enc_tan<ACT>(r[1], tr[1]), hi, lo);
+        eah[v][q] = hi; eal[v][q] = lo;
+      } else {
+        split2(r[0], r[1], hi, lo);
+        erh[v][q] = hi; erl[v][q] = lo;
+        split2(act_enc<ACT>(r[0]), act_enc<ACT>(r[1]), hi, lo);
+        eah[v][q] = hi; eal[v][q] = lo;
+      }
     }
   }
   auto chunk_q = [&](int i) {  // pieces of hidden layer i's chunks (i == L: the out layer)
@@ -281,9 +322,16 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
     const float z0 = (q < 2 ? pend0[2 * q] : pend1[2 * q - 4]) * sc;
     const float z1 = (q < 2 ? pend0[2 * q + 1] : pend1[2 * q - 3]) * sc;
     uint32_t hi, lo;
-    split2(act<ACT>(z0), act<ACT>(z1), hi, lo);
+    if (TAN) split2(act_tan<ACT>(z0, value), act_tan<ACT>(z1, value), hi, lo);
+    else split2(act<ACT>(z0), act<ACT>(z1), hi, lo);
     asm volatile("" : "+v"(hi), "+v"(lo));
     dh[ib][q] = hi; dl[ib][q] = lo;
+  };
+  const float bmask = value ? 1.f : 0.f;
+  auto bias = [&](int layer, int sb) {
+    f4v b = E.bias_at(layer, sb);
+    if (TAN) b *= bmask;
+    return b;
   };
   auto retire = [&](int layer, int ib) {
 #pragma unroll
@@ -293,7 +341,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
 #pragma unroll
   for (int ib = 0; ib < NC; ++ib) {
     const float4* A = E.begin(size_at(ib + AH));
-    f4v a0 = E.bias_at(0, 2 * ib), a1 = E.bias_at(0, 2 * ib + 1);
+    f4v a0 = bias(0, 2 * ib), a1 = bias(0, 2 * ib + 1);
     if (ib > 0) retire(0, ib - 1);
     seg<KQ, 0>(A, erh, erl, a0, a1, [](int) {});
     pend0 = a0; pend1 = a1;
@@ -309,7 +357,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
       const float4* A = E.begin(size_at(NC + i * NC + ib + AH));
-      f4v a0 = E.bias_at(1 + i, 2 * ib), a1 = E.bias_at(1 + i, 2 * ib + 1);
+      f4v a0 = bias(1 + i, 2 * ib), a1 = bias(1 + i, 2 * ib + 1);
       // the previous chunk's four activation pairs, spread over the chunk's k-steps
       seg<KH, 0>(A, sh, sl, a0, a1, [&](int u) {
         if (ib > 0 && (KH == 4 || (u & 1) == 0)) retire2(1 + i, ib - 1, KH == 4 ? u : u >> 1);
@@ -323,7 +371,7 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   // out layer (neural_blocks.py:86): one 16-row sub-block, pieces [k-step][hi, lo]; two chains
   // (even / odd k-steps); row 0 of ray j sits in register 0 of lane j
   const float4* A = E.begin(size_at(NCH - 1 + AH));
-  f4v o0 = E.bias_at(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+  f4v o0 = bias(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
   {
     float4 w0 = A[0], w1 = A[64], w2 = A[2 * 64], w3 = A[3 * 64];
 #pragma unroll

@@ -1,0 +1,346 @@
+// FP32 / fp32-split shading on the row-program ring engines (nrt_shade_ring.h): program builder
+// and launcher.  Direct.sample's emitter and BSDF evaluation (integrators.py:173-189) for the
+// reference's shading MLPs at its precision:
+//   LightField            10 x 256, F = 16   (lights.py:159-164)
+//   ComposeSpatialVarying 16 x 256, F = 128  (bsdfs.py:487-494), <= 16 components
+//   NeuralBSDF             6 x 96,  F = 64   (bsdfs.py:616-621)
+// all leaky_relu (the SkipConnMLP default, neural_blocks.py:26), 3 inputs, no latent.  Anything
+// else keeps the per-wave k_shade_direct.
+#include "nrt_launch.h"
+#include "nrt_shade_ring.h"
+
+namespace nrt {
+
+namespace {
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct ShapeSpec {
+  int H, F;
+};
+constexpr ShapeSpec kLightSpec{256, 16}, kSpatialSpec{256, 128}, kBsdfSpec{96, 64};
+
+bool shape_ok(const nrt_mlp* m, ShapeSpec s) {
+  const nrt_mlp_desc& d = m->desc;
+  return d.hidden == s.H && d.freqs == s.F && d.in_size == 3 && d.latent == 0 && d.out <= 16 &&
+         d.activation == NRT_ACT_LEAKY_RELU && d.num_layers + 2 <= kMaxLin && !m->refreshed &&
+         (int)m->host_w.size() == d.num_layers + 2;
+}
+
+// Emits one MLP's stream in the order its evaluation consumes it (nrt_shade_ring.h eval32 /
+// eval3) and records each chunk's (KiB offset, KiB count).  Layer l's inputs: the init layer the
+// encoding, hidden layer i (l = 1 + i) the H hidden features and, on skip layers, the encoding;
+// the out layer the hidden features (neural_blocks.py:46-55, 80-86).  Encoding slot s: 2q / 2q + 1
+// = sin / cos of projection q, then x0..x2 -- reference columns [x, sin, cos] (utils.py:37-40).
+//   FP32 piece  [lane 64][4 k-steps] floats: lane (g, i) = A[row 16 b + i][input of k-step s for
+//               lane group g]: hidden k-step s -> feature 16 (s >> 2) + 4 g + (s & 3), encoding
+//               k-step s -> slot 4 s + g.
+//   split piece [lane 64][8] f16 halves of W 2^s_l: lane (g, i) = A[row 16 b + i][k = 8 g + e]:
+//               hidden k-step u -> feature 16 (2u + (e >> 2)) + 4 g + (e & 3), encoding k-step v
+//               -> slot 32 v + 8 g + e.
+//   encoding part of a layer (k-outer): chunks of EQ quads (FP32) / EK k-steps (split) x every
+//   sub-block [quad or k-step][sub-block]([hi, lo]); hidden part (row-outer): one chunk per 32 rows
+//   [quad][b] / [k-step][b][hi, lo]; out layer: one chunk [quad] / [k-step][hi, lo] of sub-block 0.
+//   A skip layer's hidden chunks come before its encoding chunks.
+struct Walker {
+  bool split;
+  std::vector<float>* s32;
+  std::vector<_Float16>* s3;
+  std::vector<int>* chunks;
+  size_t pieces() const { return split ? s3->size() / 512 : s32->size() / 256; }
+  void chunk_begin() { chunks->push_back((int)pieces()); chunks->push_back(0); }
+  void chunk_end() { chunks->back() = (int)pieces() - chunks->at(chunks->size() - 2); }
+};
+
+int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
+  const nrt_mlp_desc& d = m->desc;
+  const int H = d.hidden, L = d.num_layers, F = d.freqs, in = 3;
+  const int dp = in + 2 * F;
+  const int ke = (dp + 15) / 16 * 16, ke3 = (dp + 31) / 32 * 32;
+  const int NSB = H / 16, NC = H / 32;
+  // slot -> column of the encoding [x, sin, cos]
+  auto slot_col = [&](int s) -> int {
+    if (s < 2 * F) return (s & 1) ? in + F + (s >> 1) : in + (s >> 1);
+    if (s < 2 * F + in) return s - 2 * F;
+    return -1;
+  };
+  const int nl = L + 2;
+  std::vector<int> R(nl), C(nl);
+  std::vector<char> hid(nl), enc(nl);
+  for (int l = 0; l < nl; ++l) {
+    const bool skip = l >= 1 && l <= L && (l - 1) != L - 1 && ((l - 1) % d.skip) == 0;
+    hid[l] = l >= 1;
+    enc[l] = l == 0 || skip;
+    R[l] = l == nl - 1 ? d.out : H;
+    C[l] = (hid[l] ? H : 0) + (enc[l] ? dp : 0);
+    if ((int64_t)m->host_w[l].size() != (int64_t)R[l] * C[l]) {
+      set_error("shading program: weight shape mismatch");
+      return NRT_EINVAL;
+    }
+  }
+  lscale.assign(nl, 1.f);
+  if (w.split)
+    for (int l = 0; l < nl; ++l) {
+      float mx = 0.f;
+      for (float v : m->host_w[l]) mx = std::max(mx, std::fabs(v));
+      int e = 0;
+      if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &e);
+      lscale[l] = std::ldexp(1.f, std::max(-64, std::min(64, 1 - e)));  // max|W| scale in [1, 2)
+    }
+  auto W = [&](int l, int row, int col) -> float {
+    if (row >= R[l] || col < 0 || col >= C[l]) return 0.f;
+    return m->host_w[l][(size_t)row * C[l] + col];
+  };
+  auto enc_col = [&](int l, int slot) -> int {
+    const int c = slot_col(slot);
+    return c < 0 ? -1 : (hid[l] ? H + c : c);
+  };
+  auto put32 = [&](float v) { w.s32->push_back(v); };
+  auto put3 = [&](int l, float v, int part) {
+    const float x = v * lscale[l];
+    const _Float16 hi = (_Float16)x;
+    w.s3->push_back(part == 0 ? hi : (_Float16)(x - (float)hi));
+  };
+  auto enc_part = [&](int l) {
+    if (!w.split) {
+      const int QE = ke / 16, EQ = NSB >= 16 ? 2 : 32 / NSB;
+      for (int u0 = 0; u0 < QE; u0 += EQ) {
+        w.chunk_begin();
+        for (int u = u0; u < std::min(QE, u0 + EQ); ++u)
+          for (int sb = 0; sb < NSB; ++sb)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int t = 0; t < 4; ++t) {
+                const int g = lane >> 4, s = 4 * u + t;
+                put32(W(l, 16 * sb + (lane & 15), enc_col(l, 4 * s + g)));
+              }
+        w.chunk_end();
+      }
+    } else {
+      const int KQ = ke3 / 32, EK = NSB >= 16 ? 1 : 16 / NSB;
+      for (int v0 = 0; v0 < KQ; v0 += EK) {
+        w.chunk_begin();
+        for (int v = v0; v < std::min(KQ, v0 + EK); ++v)
+          for (int sb = 0; sb < NSB; ++sb)
+            for (int part = 0; part < 2; ++part)
+              for (int lane = 0; lane < 64; ++lane)
+                for (int e = 0; e < 8; ++e) {
+                  const int g = lane >> 4;
+                  put3(l, W(l, 16 * sb + (lane & 15), enc_col(l, 32 * v + 8 * g + e)), part);
+                }
+        w.chunk_end();
+      }
+    }
+  };
+  // hidden part of layer l, rows 32 ib + 16 b (nb = 2 sub-blocks, or 1 for the out layer)
+  auto hidden_chunk = [&](int l, int ib, int nb) {
+    w.chunk_begin();
+    if (!w.split) {
+      for (int u = 0; u < H / 16; ++u)
+        for (int b = 0; b < nb; ++b)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int t = 0; t < 4; ++t) {
+              const int g = lane >> 4, s = 4 * u + t;
+              put32(W(l, 32 * ib + 16 * b + (lane & 15), 16 * (s >> 2) + 4 * g + (s & 3)));
+            }
+    } else {
+      for (int u = 0; u < H / 32; ++u)
+        for (int b = 0; b < nb; ++b)
+          for (int part = 0; part < 2; ++part)
+            for (int lane = 0; lane < 64; ++lane)
+              for (int e = 0; e < 8; ++e) {
+                const int g = lane >> 4;
+                put3(l, W(l, 32 * ib + 16 * b + (lane & 15), 16 * (2 * u + (e >> 2)) + 4 * g + (e & 3)),
+                     part);
+              }
+    }
+    w.chunk_end();
+  };
+  enc_part(0);
+  for (int i = 0; i < L; ++i) {  // skip layers: hidden part first, then the encoding part
+    for (int ib = 0; ib < NC; ++ib) hidden_chunk(1 + i, ib, 2);
+    if (enc[1 + i]) enc_part(1 + i);
+  }
+  hidden_chunk(L + 1, 0, 1);
+  return NRT_OK;
+}
+
+}  // namespace
+
+int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out) {
+  out.built = true;
+  out.ok = false;
+  if (mlps.empty() || (int)mlps.size() > kMaxProgMlp) return NRT_OK;
+  RProgDev& d = out.d;
+  std::memset(&d, 0, sizeof(d));
+  std::vector<float> s32;
+  std::vector<_Float16> s3;
+  std::vector<int> chunks;
+  std::vector<float> bias, scales;
+  std::vector<float4> basis;
+  Walker w{split, &s32, &s3, &chunks};
+  for (size_t k = 0; k < mlps.size(); ++k) {
+    const nrt_mlp* m = mlps[k];
+    const nrt_mlp_desc& md = m->desc;
+    std::vector<float> lscale;
+    if (int rc = walk_mlp(m, w, lscale)) return rc;
+    RProgMlp& pm = d.mlp[k];
+    pm.L = md.num_layers; pm.skip = md.skip; pm.F = md.freqs; pm.out = md.out;
+    pm.bstride = md.hidden;  // >= 16 rows of the out layer's sub-block
+    pm.bias_off = (int)bias.size();
+    const int hs = m->host_dev.bias16_stride;
+    for (int l = 0; l < md.num_layers + 2; ++l) {
+      const int rows = l == md.num_layers + 1 ? md.out : md.hidden;
+      for (int r = 0; r < pm.bstride; ++r)
+        bias.push_back(r < rows ? m->host_bias[(size_t)l * hs + r] * lscale[l] : 0.f);
+    }
+    pm.scale_off = -1;  // filled below (scales follow the biases)
+    for (int l = 0; l < md.num_layers + 2; ++l) scales.push_back(1.f / lscale[l]);
+    pm.basis_off = (int)basis.size();
+    const int F = md.freqs;
+    for (int q = 0; q < F; ++q)
+      basis.push_back(make_float4(m->host_basis[q], m->host_basis[F + q], m->host_basis[2 * F + q], 0.f));
+  }
+  {
+    int off = (int)bias.size();
+    for (size_t k = 0; k < mlps.size(); ++k) {
+      d.mlp[k].scale_off = off;
+      off += mlps[k]->desc.num_layers + 2;
+    }
+  }
+  std::vector<float> tables(bias);
+  tables.insert(tables.end(), scales.begin(), scales.end());
+  d.n_mlp = (int)mlps.size();
+  d.n_chunks = (int)chunks.size() / 2;
+  d.table_floats = (int)tables.size();
+  d.basis_q = (int)basis.size();
+  const size_t sbytes = split ? s3.size() * sizeof(_Float16) : s32.size() * sizeof(float);
+  if (sbytes >= (size_t)1 << 30) return NRT_OK;
+  const size_t o_chunks = align256(sbytes);
+  const size_t o_tab = align256(o_chunks + chunks.size() * 4);
+  const size_t o_basis = align256(o_tab + tables.size() * 4);
+  const size_t total = align256(o_basis + std::max<size_t>(basis.size(), 1) * 16);
+  char* buf = nullptr;
+  NRT_HIP(hipMalloc((void**)&buf, total));
+  out.buf = buf;
+  NRT_HIP(hipMemcpy(buf, split ? (const void*)s3.data() : (const void*)s32.data(), sbytes,
+                    hipMemcpyHostToDevice));
+  NRT_HIP(hipMemcpy(buf + o_chunks, chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice));
+  NRT_HIP(hipMemcpy(buf + o_tab, tables.data(), tables.size() * 4, hipMemcpyHostToDevice));
+  if (!basis.empty())
+    NRT_HIP(hipMemcpy(buf + o_basis, basis.data(), basis.size() * 16, hipMemcpyHostToDevice));
+  d.stream = buf;
+  d.stream_bytes = (int)sbytes;
+  d.chunks = reinterpret_cast<const int*>(buf + o_chunks);
+  d.tables = reinterpret_cast<const float*>(buf + o_tab);
+  d.basis = reinterpret_cast<const float4*>(buf + o_basis);
+  out.ok = true;
+  return NRT_OK;
+}
+
+namespace {
+constexpr int kRWaves = 8;
+
+template <class K>
+int persistent_grid(K kern, int threads, size_t lds, int64_t want) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  }
+  int per_cu = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kern),
+                                                   threads, lds) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)cus * per_cu));
+}
+
+// ring depth: 3 slots where they fit beside the tables in the CU's LDS, else 2
+template <int PREC, int WV, class F>
+int with_depth(const RProgDev& d, F&& f) {
+  if (rprog::Engine<3, WV>::lds_bytes(d) <= (size_t)kLdsBytes) return f(std::integral_constant<int, 3>{});
+  if (rprog::Engine<2, WV>::lds_bytes(d) <= (size_t)kLdsBytes) return f(std::integral_constant<int, 2>{});
+  return NRT_EUNSUPPORTED;
+}
+}  // namespace
+
+// NRT_EUNSUPPORTED when the row-program kernels do not cover this light / BSDF pair
+int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
+               const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
+               const float* lscale, float* rgb, float* weights_out, int precision, hipStream_t st) {
+  const bool split = precision == NRT_FP32_SPLIT;
+  const int pi = split ? 1 : 0;
+  const bool field = l->host_dev.kind == 0;
+  if (b->host_dev.n > 16) return NRT_EUNSUPPORTED;
+  // build on first use
+  nrt_rprog& lp = l->rprog[pi];
+  nrt_rprog& bp = b->rprog[pi];
+  if (field && !lp.built) {
+    if (l->mlp && shape_ok(l->mlp, kLightSpec) && l->mlp->desc.out == 3) {
+      if (int rc = build_rprog({l->mlp}, split, lp)) return rc;
+    } else {
+      lp.built = true;
+    }
+  }
+  if (!bp.built) {
+    std::vector<const nrt_mlp*> v;
+    bool ok = true;
+    if (b->spatial) {
+      ok = shape_ok(b->spatial, kSpatialSpec);
+      v.push_back(b->spatial);
+    }
+    for (const nrt_mlp* m : b->mlps) ok = ok && shape_ok(m, kBsdfSpec) && m->desc.out == 3;
+    v.insert(v.end(), b->mlps.begin(), b->mlps.end());
+    if (ok && !v.empty()) {
+      if (int rc = build_rprog(v, split, bp)) return rc;
+    } else {
+      bp.built = true;
+    }
+  }
+  if ((field && !lp.ok) || !bp.ok) return NRT_EUNSUPPORTED;
+  constexpr int WV = kRWaves;
+  float* ls = nullptr;
+  NRT_HIP(hipMallocAsync((void**)&ls, (size_t)std::max<int64_t>(P, 1) * kLsStride * sizeof(float), st));
+  const int64_t want = ceil_div64(P, 16 * WV);
+  int rc = NRT_OK;
+  auto run = [&]<int PREC>() -> int {
+    {
+      ProfScope prof(PREC == 2 ? "k_light3" : "k_light32", st);
+      if (field) {
+        rc = with_depth<PREC, WV>(lp.d, [&](auto dd) -> int {
+          constexpr int D = decltype(dd)::value;
+          auto kern = rprog::k_light_r<PREC, D, WV>;
+          const size_t lds = rprog::Engine<D, WV>::lds_bytes(lp.d);
+          if (int r = set_lds(kern, lds)) return r;
+          kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want)), dim3(64 * WV), lds, st>>>(
+              lp.d, l->dev, p, n, wi, hit_idx, hit_count, lscale, ls);
+          return check_launch("k_light_r");
+        });
+      } else {
+        auto kern = k_light16<WV, false>;  // point light: VALU only, FP32 math
+        kern<<<dim3(persistent_grid(kern, 64 * WV, 0, ceil_div64(P, 32 * WV))), dim3(64 * WV), 0, st>>>(
+            ProgDev{}, l->dev, p, n, wi, hit_idx, hit_count, lscale, ls);
+        rc = check_launch("k_light16");
+      }
+    }
+    if (rc) return rc;
+    ProfScope prof(PREC == 2 ? "k_bsdf3" : "k_bsdf32", st);
+    return with_depth<PREC, WV>(bp.d, [&](auto dd) -> int {
+      constexpr int D = decltype(dd)::value;
+      const size_t lds = rprog::Engine<D, WV>::lds_bytes(bp.d);
+      auto launch = [&](auto kern) -> int {
+        if (int r = set_lds(kern, lds)) return r;
+        kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want)), dim3(64 * WV), lds, st>>>(
+            bp.d, b->dev, p, wi, hit_idx, hit_count, ls, rgb, weights_out);
+        return check_launch("k_bsdf_r");
+      };
+      return b->spatial ? launch(rprog::k_bsdf_r<PREC, D, WV, true>)
+                        : launch(rprog::k_bsdf_r<PREC, D, WV, false>);
+    });
+  };
+  rc = split ? run.template operator()<2>() : run.template operator()<0>();
+  (void)hipFreeAsync(ls, st);
+  return rc;
+}
+
+}  // namespace nrt
