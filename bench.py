@@ -60,6 +60,8 @@ def parse():
                          "BASELINE.json configs[2..4] as one-GPU workloads")
     ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
     ap.add_argument("--crop", type=int, default=80, help="--scene train: crop side")
+    ap.add_argument("--torch-profile", default=None,
+                    help="--scene train: write a torch.profiler op table of one step here")
     args = ap.parse_args()
     import sys
     args.precision_set = any(a.startswith("--precision") for a in sys.argv[1:])
@@ -221,7 +223,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # a torch.distributed.run launch takes the process-group path even at one rank (so the RCCL
+    # broadcast / all-gather / all-reduce run on a one-GPU box too)
+    dist_on = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    if dist_on:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -236,7 +241,7 @@ def main():
 
     size = args.size
     scene = build_scene(device, args.samples, light_gain=LIGHT_GAIN)
-    if world > 1:
+    if dist_on:
         # every rank built the scene from the same seed; broadcasting rank 0's tensors makes the
         # replication explicit (a model loaded from file on rank 0 is replicated the same way)
         from neural_raytracing_amd.pathtracer.render import broadcast_module
@@ -249,13 +254,13 @@ def main():
     rows = row_shard(size, rank, world, args.tile_rows)
     rr = RowRenderer(scene["shape"], scene["lights"], cameras, scene["integrator"], scene["bsdf"],
                      size, rows, background=0.0, with_noise=1e-3, device=device)
-    step = make_step(rr.render, rows, size, rank, world, args.tile_rows, device)
+    step = make_step(rr.render, rows, size, rank, world, args.tile_rows, device, gather=dist_on)
 
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             torch.distributed.barrier()
         _lib.profile_reset()
         _lib.profile_enable(True)
@@ -264,7 +269,7 @@ def main():
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on:
             torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
@@ -272,7 +277,7 @@ def main():
         k_ms, k_n = _lib.profile_read(march_kernel)
         i_ms, i_n = _lib.profile_read("k_intersect")
         evals = count_evals(step)
-        elapsed = max_over_ranks(elapsed, world, device)
+        elapsed = max_over_ranks(elapsed, world, device, force=dist_on)
 
     ms_step = 1000 * elapsed / args.steps
     rays_per_rank = len(rows) * size * world  # this rank's rows of every view
@@ -327,7 +332,7 @@ def main():
             line["cpu_baseline"] = extra.pop("cpu_baseline")
         line.update(extra)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         torch.distributed.destroy_process_group()
 
 
@@ -443,15 +448,18 @@ def fp16_leg(rr, args, rows, size, steps=5, warmup=2):
                                                  t.cpu(), rt.cpu())}
 
 
-def make_step(render, rows, size, rank, world, tile_rows, device, channels=4):
+def make_step(render, rows, size, rank, world, tile_rows, device, channels=4, gather=None):
     """One bench step's frame assembly: `render()` gives this rank's rows of every view
     ([world, len(rows), size, channels]); the step returns the full [world, size, size, channels]
-    frames on every rank -- a RowGather all-gather (RCCL) for world > 1, an index copy on one GPU.
-    The buffers and index tensors are built here, once."""
+    frames on every rank -- a RowGather all-gather (RCCL) under a process group (world > 1, or
+    `gather` forced on), an index copy otherwise.  The buffers and index tensors are built here,
+    once."""
     from neural_raytracing_amd.pathtracer.render import RowGather
     full = torch.zeros(world, size, size, channels, device=device)
     rows_idx = torch.tensor(rows, dtype=torch.long, device=device)
-    gather = RowGather(size, rank, world, tile_rows, (world, size, channels), device) if world > 1 else None
+    if gather is None:
+        gather = world > 1
+    gather = RowGather(size, rank, world, tile_rows, (world, size, channels), device) if gather else None
 
     def step():
         img = render()
@@ -463,9 +471,9 @@ def make_step(render, rows, size, rank, world, tile_rows, device, channels=4):
     return step
 
 
-def max_over_ranks(elapsed, world, device):
+def max_over_ranks(elapsed, world, device, force=False):
     """The bench's time: the slowest rank's (all-reduce MAX), on every rank."""
-    if world <= 1:
+    if world <= 1 and not force:
         return elapsed
     t = torch.tensor([elapsed], device=device, dtype=torch.float64)
     torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -880,6 +888,40 @@ def bench_train(args):
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    if args.torch_profile:
+        # op counts of one step by Python call site (tools: where the launches come from)
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+            step(10_000)
+            torch.cuda.synchronize()
+        # host synchronisations of one step by call site (torch.cuda sync debug mode)
+        import collections
+        import traceback
+        import warnings
+        sites = collections.Counter()
+
+        def show(message, category, filename, lineno, file=None, line=None):
+            stack = [f for f in traceback.extract_stack()[:-1]
+                     if "site-packages" not in f.filename and "warnings" not in f.filename]
+            sites[" <- ".join(f"{f.filename.split('/')[-1]}:{f.lineno}" for f in stack[-4:])] += 1
+        old_show = warnings.showwarning
+        warnings.showwarning = show
+        torch.cuda.set_sync_debug_mode("warn")
+        try:
+            with warnings.catch_warnings():
+                warnings.simplefilter("always")
+                warnings.showwarning = show
+                step(10_001)
+                torch.cuda.synchronize()
+        finally:
+            torch.cuda.set_sync_debug_mode(0)
+            warnings.showwarning = old_show
+        with open(args.torch_profile, "w") as f:
+            f.write(prof.key_averages().table(sort_by="count", row_limit=120,
+                                              max_name_column_width=40))
+            f.write("\n\nhost syncs by call site (one step)\n")
+            for site, n in sites.most_common():
+                f.write(f"{n:6d}  {site}\n")
     _lib.profile_reset()
     _lib.profile_enable(True)
     t0 = time.perf_counter()

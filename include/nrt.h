@@ -129,6 +129,11 @@ int nrt_sdf_create_mlp(const nrt_mlp* mlp, nrt_sdf** out);
 int nrt_sdf_create_sphere_blob(int32_t n, const float* host_centers, const float* host_radii,
                                const float* host_tfs, float k, const nrt_mlp* shift,
                                nrt_sdf** out);
+/* Rewrite a sphere-blob SDF's sphere table from device tensors (same layout as the host
+ * arguments of nrt_sdf_create_sphere_blob), stream-ordered: the training path's per-step update
+ * after an optimiser step, with no host round trip.  NRT_EINVAL for other SDF kinds. */
+int nrt_sdf_refresh_spheres(nrt_sdf* sdf, const float* device_centers, const float* device_radii,
+                            const float* device_tfs, void* stream);
 int nrt_sdf_destroy(nrt_sdf* sdf);
 
 /* out[M] = sdf(p[M,3]) */

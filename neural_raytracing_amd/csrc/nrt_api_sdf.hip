@@ -64,6 +64,39 @@ int nrt_sdf_create_sphere_blob(int32_t n, const float* centers, const float* rad
   return sdf_finish(s, out);
 }
 
+}  // extern "C"
+
+namespace {
+// the SphereSDF table of nrt_sdf_create_sphere_blob from device tensors: row i = (I + tfs_i)
+// row-major (9), centre (3), radius (1), pad (3)
+template <int = 0>
+__global__ void k_pack_spheres(int n, const float* __restrict__ c, const float* __restrict__ r,
+                               const float* __restrict__ t, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float* d = out + (size_t)i * 16;
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) d[3 * a + b] = t[(size_t)i * 9 + 3 * a + b] + (a == b ? 1.f : 0.f);
+  d[9] = c[i * 3]; d[10] = c[i * 3 + 1]; d[11] = c[i * 3 + 2];
+  d[12] = r[i];
+  d[13] = 0.f; d[14] = 0.f; d[15] = 0.f;
+}
+}  // namespace
+
+extern "C" {
+int nrt_sdf_refresh_spheres(nrt_sdf* s, const float* centers, const float* radii, const float* tfs,
+                            void* stream) {
+  if (!s || !centers || !radii || !tfs) { set_error("nrt_sdf_refresh_spheres: null argument"); return NRT_EINVAL; }
+  if (s->host_dev.kind != 2 || !s->spheres) {
+    set_error("nrt_sdf_refresh_spheres: not a sphere-blob SDF");
+    return NRT_EINVAL;
+  }
+  const int n = s->host_dev.n_spheres;
+  k_pack_spheres<><<<dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream>>>(n, centers, radii,
+                                                                                tfs, s->spheres);
+  return check_launch("k_pack_spheres");
+}
+
 int nrt_sdf_destroy(nrt_sdf* s) {
   if (!s) return NRT_OK;
   if (s->spheres) (void)hipFree(s->spheres);

@@ -59,8 +59,16 @@ class NeRFCamera(Camera):
         return self.cam_to_world.shape[0]
 
     def _structs(self, size):
-        return [_cam_struct(_lib.NRT_CAM_NERF, size, self.focal, mat=self.cam_to_world[n, :3, :4])
-                for n in range(len(self))]
+        # the matrices go to the host once per (tensor, version, size, focal), not once per tile
+        c2w = self.cam_to_world
+        key = (c2w.data_ptr(), c2w._version, tuple(c2w.shape), int(size), float(self.focal))
+        cached = getattr(self, "_nrt_structs", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        structs = [_cam_struct(_lib.NRT_CAM_NERF, size, self.focal, mat=c2w[n, :3, :4])
+                   for n in range(len(self))]
+        object.__setattr__(self, "_nrt_structs", (key, structs))
+        return structs
 
     def rays_tile(self, x0, y0, W, H, size, with_noise=False, positions=None):
         """[N, W, H, 1, 6] rays for tile rows x0.. and cols y0.. (u = col, v = row)."""

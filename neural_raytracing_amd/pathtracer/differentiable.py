@@ -31,7 +31,7 @@ def coordinate_system(n):
     x, y, z = n.split(1, dim=-1)
     sign = torch.where(z >= 0, 1., -1.)
     s_z = sign + z
-    a = -torch.where(s_z.abs() < 1e-6, torch.tensor(1e-6, device=z.device), s_z).reciprocal()
+    a = -torch.where(s_z.abs() < 1e-6, 1e-6, s_z).reciprocal()
     b = x * y * a
     s = torch.cat([(x * x * a * sign) + 1, b * sign, x * -sign], dim=-1)
     s = F.normalize(s, eps=1e-7, dim=-1)
@@ -43,7 +43,22 @@ def coordinate_system(n):
 # ---- BSDF helpers (utils.py:43-51, 152-155, 234-258; bsdfs.py:127-129, 327-343) --------------
 
 def nonzero_eps(v, eps: float = 1e-7):
-    return torch.where(v.abs() < eps, torch.tensor(eps, device=v.device), v)
+    # a Python scalar branch: no host -> device copy (and no stream sync) per call
+    return torch.where(v.abs() < eps, eps, v)
+
+
+_AXES = {}
+
+
+def _axis(i, like):
+    """Unit axis e_i on like's device, built once per device (no per-call host copy)."""
+    key = (like.device, i)
+    t = _AXES.get(key)
+    if t is None:
+        t = torch.zeros(3, device=like.device, dtype=torch.float)
+        t[i] = 1.0
+        _AXES[key] = t
+    return t.expand_as(like)
 
 
 def rotate_vector(v, axis, c, s):
@@ -55,8 +70,8 @@ def param_rusin2(wo, wi):
     """[cos phi_d, cos theta_h, cos theta_d] (utils.py:234-258)."""
     wo = F.normalize(wo, dim=-1)
     wi = F.normalize(wi, dim=-1)
-    e_1 = torch.tensor([0, 1, 0], device=wo.device, dtype=torch.float).expand_as(wo)
-    e_2 = torch.tensor([0, 0, 1], device=wo.device, dtype=torch.float).expand_as(wo)
+    e_1 = _axis(1, wo)
+    e_2 = _axis(2, wo)
     H = F.normalize(wo + wi, dim=-1)
     cos_theta_h = H[..., 2]
     r = nonzero_eps(H[..., 1]).hypot(nonzero_eps(H[..., 0])).clamp(min=1e-6)

@@ -257,10 +257,10 @@ class Direct(Integrator):
             # sample_emitter_dir_w_isect (scene.py:290-298): shadow ray to the point light,
             # marched like SDF.intersect_test (sdfs.py:162-181); with an occlusion MLP,
             # sample_emitter_dir_w_learned_occ (scene.py:301-319)
-            from ..shapes.sdfs import sdf_handle
+            from ..shapes.sdfs import march_handle
             lib = _lib.load(require_device=True)
             ws = torch.empty(lib.nrt_shadow_workspace_bytes(P), dtype=torch.uint8, device=device)
-            head = (_bsdf_handle(bsdf), _light_handle(lights), sdf_handle(shapes.sdf))
+            head = (_bsdf_handle(bsdf), _light_handle(lights), march_handle(shapes.sdf))
             steps = (int(shapes.max_steps), float(shapes.epsilon))
             if occ is None:
                 _lib.call("nrt_shade_direct_shadowed", *head, *steps, *args, None, _lib.ptr(ws),
@@ -357,6 +357,18 @@ class NeRFReproduce(Integrator):
         return result, torch.tensor(True, device=result.device), Dummy()
 
 
+_TRUE = {}
+
+
+def _true(device):
+    """The integrator's all-active flag (integrators.py:257) as a cached device tensor: one host
+    copy per device instead of one (and a stream sync) per call."""
+    t = _TRUE.get(device)
+    if t is None:
+        t = _TRUE[device] = torch.tensor(True, device=device)
+    return t
+
+
 class NeRFIntegrator(Integrator):
     """Appends sigmoid(throughput) as alpha (integrators.py:243-257)."""
 
@@ -373,4 +385,4 @@ class NeRFIntegrator(Integrator):
         if mi.with_logits:
             alpha = alpha.sigmoid()
         result = torch.cat([result, alpha], dim=-1)
-        return result, torch.tensor(True, device=result.device), mi
+        return result, _true(result.device), mi

@@ -9,7 +9,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ... import _lib
-from .._handles import _Handle, _cache, _host, mlp_handle
+from .._handles import _Handle, _cache, _host, mlp_handle, train_handle
 from ..interaction import MixedInteraction
 from ..differentiable import coordinate_system, needs_grad, sdf_gradient, sdf_value
 from ..neural_blocks import SkipConnMLP
@@ -81,6 +81,55 @@ def sdf_handle(sdf):
     raise _lib.NrtError(f"SDF callable {getattr(sdf, '__name__', type(sdf).__name__)} has no HIP "
                         "implementation (supported: SPHERE_SDF, SphereSDF, SkipConnMLP and their "
                         "TorchScript modules)")
+
+
+def train_sdf_handle(sdf):
+    """nrt_sdf for the training loop's march: built over the SDF MLP's training handle
+    (``train_handle``: re-packed on the device by nrt_mlp_refresh after each optimiser step) and,
+    for a SphereSDF, a sphere table rewritten on the device (nrt_sdf_refresh_spheres) when its
+    tensors change -- where ``sdf_handle`` would copy every weight to the host and pack it again
+    each step.  The FP16 ring kernels refuse refreshed handles, so FP16 keeps ``sdf_handle``."""
+    from ..script_modules import resolve
+    s = resolve(sdf)
+    if _lib.precision_code() == _lib.NRT_FP16:
+        return sdf_handle(sdf)
+    if isinstance(s, SkipConnMLP):
+        th = train_handle(s)
+        cached = getattr(s, "_nrt_train_sdf", None)
+        if cached is None or cached[0] is not th:
+            out = ctypes.c_void_p()
+            _lib.check(_lib.load().nrt_sdf_create_mlp(th.value, ctypes.byref(out)), "nrt_sdf_create_mlp")
+            cached = (th, _Handle(out, "nrt_sdf_destroy", [th]))
+            object.__setattr__(s, "_nrt_train_sdf", cached)
+        return cached[1].value
+    if _is_sphere_sdf(s) and getattr(s, "shift", None) is not None:
+        sph = (s.centers, s.radii, s.tfs)
+        if not all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in sph):
+            return sdf_handle(sdf)
+        th = train_handle(s.shift)
+        shapes = tuple((t.data_ptr(), tuple(t.shape)) for t in sph)
+        vers = tuple(t._version for t in sph)
+        cached = getattr(s, "_nrt_train_sdf", None)
+        if cached is None or cached[0] is not th or cached[2] != shapes:
+            c, r, t = _host(s.centers), _host(s.radii), _host(s.tfs)
+            out = ctypes.c_void_p()
+            _lib.check(_lib.load().nrt_sdf_create_sphere_blob(
+                c.shape[0], c.data_ptr(), r.data_ptr(), t.data_ptr(), 32.0, th.value,
+                ctypes.byref(out)), "nrt_sdf_create_sphere_blob")
+            cached = [th, _Handle(out, "nrt_sdf_destroy", [th]), shapes, vers]
+            object.__setattr__(s, "_nrt_train_sdf", cached)
+        elif cached[3] != vers:
+            _lib.call("nrt_sdf_refresh_spheres", cached[1].value, _lib.ptr(s.centers.detach()),
+                      _lib.ptr(s.radii.detach()), _lib.ptr(s.tfs.detach()), _lib.stream())
+            cached[3] = vers
+        return cached[1].value
+    return sdf_handle(sdf)
+
+
+def march_handle(sdf):
+    """The SDF handle a march uses: the training one while the SDF's parameters take
+    gradients (the training loop), else the host-packed render handle."""
+    return train_sdf_handle(sdf) if needs_grad(sdf) else sdf_handle(sdf)
 
 
 def _looks_like_sphere_sdf(m):
@@ -176,7 +225,7 @@ class SDF:
         lead = rays.shape[:-1]
         flat = rays.reshape(-1, 6).float().contiguous()
         P = flat.shape[0]
-        h = sdf_handle(self.sdf)
+        h = march_handle(self.sdf)
         t = torch.empty(P, device=dev)
         hit = torch.empty(P, dtype=torch.uint8, device=dev)
         p = torch.empty(P, 3, device=dev)
@@ -259,7 +308,7 @@ class SDF:
         mt = torch.as_tensor(max_t, dtype=torch.float32, device=rays.device)
         mt = mt.expand(lead + (1,)).reshape(P).contiguous() if mt.dim() > 0 else mt.expand(P).contiguous()
         vis = torch.empty(P, dtype=torch.uint8, device=rays.device)
-        _lib.call("nrt_sdf_occlusion", sdf_handle(self.sdf), _lib.ptr(flat), P, _lib.ptr(mt),
+        _lib.call("nrt_sdf_occlusion", march_handle(self.sdf), _lib.ptr(flat), P, _lib.ptr(mt),
                   int(self.max_steps), float(self.epsilon), _lib.ptr(vis), _lib.precision_code(),
                   _lib.stream())
         return vis.bool().reshape(lead)
