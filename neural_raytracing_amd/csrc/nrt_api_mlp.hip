@@ -11,11 +11,16 @@ int nrt_mlp_forward(const nrt_mlp* m, const float* x, const float* latent, int64
   if (!x || !y) { set_error("nrt_mlp_forward: null x / y"); return NRT_EINVAL; }
   if (m->desc.latent > 0 && !latent) { set_error("nrt_mlp_forward: latent required"); return NRT_EINVAL; }
   const bool f16 = precision == NRT_FP16;
+  hipStream_t st = (hipStream_t)stream;
+  // FP32: the shading MLP shapes on the ring engine (nrt_shade_ring.hip), same arithmetic class
+  if (!f16 && !latent && option(OPT_SHADE_RING) != 0) {
+    const int rc = solo_forward(m, x, M, y, st);
+    if (rc != NRT_EUNSUPPORTED) return rc;
+  }
   LdsPlan p = plan_lds(m->desc.hidden, m->host_dev.ke, m->desc.out, f16, false);
   if (!f16) spread_waves(p);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, p.waves)), block(64 * p.waves);
-  hipStream_t st = (hipStream_t)stream;
   int rc = NRT_OK;
   ProfScope prof("k_mlp_forward", st);
   NRT_NB_SWITCH(m->desc.hidden / 32, {

@@ -7,10 +7,10 @@
 //                     row-local backward chain dZ_l = (dZ_{l+1} W_{l+1}) * act'(Z_l) with the W^T
 //                     fragments, the encoding gradient, and dL/dx, dL/dlatent.  TILE moves the
 //                     encoding and its gradient out of the slab into per-wave global tiles.
-//   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M): k_wgrad, split-K exact-f32 MFMA
-//                     on the saved activations, slices summed in order; bias gradients = column
-//                     sums of dZ_l (k_colsum_*).
-#include <mutex>
+//   weight gradients  dW_l = dZ_l^T In_l over the batch (K = M) and bias gradients (In = ones):
+//                     every layer of one backward call in one k_wgrad_batch launch (split-K
+//                     exact-f32 MFMA on the saved activations) + k_split_reduce_batch (slices
+//                     summed in order: deterministic).
 
 #include "nrt_launch.h"
 
@@ -394,8 +394,7 @@ __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
 namespace {
 size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
 
-constexpr int kBiasChunks = 256;  // bias-gradient partial sums (k_colsum_*)
-constexpr int kBiasMaxR = 256;
+constexpr size_t kWgradTableBytes = 16384;  // device copy of a WgradBatch's job table
 
 struct TrainWs {
   float *Z, *A, *dZ, *Eraw, *Eact, *Et, *Gt, *part, *kpart;
@@ -419,8 +418,8 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   w.Eact = (float*)p; p += a256(enc);
   w.Et = (float*)p; p += a256(enc_tile_bytes(d, M));
   w.Gt = (float*)p; p += a256(enc_tile_bytes(d, M));
-  w.part = (float*)p; p += a256((size_t)kBiasChunks * kBiasMaxR * 4);
-  w.kpart = (float*)p;
+  w.part = (float*)p; p += a256(kWgradTableBytes);  // weight-gradient job table
+  w.kpart = (float*)p;  // batched partial products
   return w;
 }
 
@@ -429,48 +428,56 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
 // internal linkage -- "Cannot find Symbol with name: _ZN3nrt12_GLOBAL__N_17k_wgrad...")
 
 // Split-K weight gradients.  dW = dZ^T In has a small output (R x C <= 256 x 550) and a long K
-// (the batch, ~10^4-10^5): the batch is cut into S slices, one wave computes one 64 x 64 output
-// tile of one slice on exact-f32 MFMA, and the slice partials are summed in slice order
-// (deterministic).  S is chosen from the shape alone (same inputs, same bits).
+// (the batch, ~10^4-10^5): the batch is cut into S slices, one block computes one 64 x 64 output
+// tile of one slice on exact-f32 MFMA (v_mfma_f32_32x32x2_f32, an fma chain) with a 2 x 2 grid of
+// 32x32 accumulators -- wave w of kWgradWaves takes the slice's groups of 16 rows w, w +
+// kWgradWaves, ...; lane (i = l & 31, h = l >> 5) loads dZ[m + h][r0 + 32a + i] (the A operand,
+// dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row segments per half-wave -- then the waves'
+// accumulators are summed in wave order through LDS and the slice partials in slice order
+// (deterministic).  S is chosen from the shapes alone (same inputs, same bits).
 constexpr int kSplitMax = 64;
 constexpr int64_t kSliceRows = 256;  // batch rows per slice at least
 constexpr int kWgradWaves = 4;        // waves per block
 
-size_t split_part_floats(const MlpDev& d) {
-  const size_t rc = (size_t)std::max(d.hidden, d.out) * (size_t)(d.hidden + d.dp);
-  return (size_t)kSplitMax * rc;
-}
-
-struct GemmCtx {
-  float* part;  // split_part_floats(d) floats
-  hipStream_t st;
+// ---- every weight and bias gradient of one backward call in two launches --------------------
+// A job is dW[r][c0 + c] (ldw) = sum_m dZ[m][r] In[m][c] (row-major dZ [M][R], In [M][ldi]), or
+// (bias) db[r] = sum_m dZ[m][r] -- the same product with In a column of ones.  All jobs share the
+// slice count S (from the shapes alone: same inputs, same bits); blocks are (job, 64 x 64 tile,
+// slice), the partials of slice s of job j sit at part + part_off + s R C, and k_split_reduce_batch
+// sums them in slice order.  Per training step this replaces ~500 launches (round 2: a k_wgrad +
+// k_split_reduce pair per layer part, two column-sum launches per bias) by two per MLP backward.
+struct WgradJob {
+  const float* dZ;
+  const float* In;   // nullptr: bias job (a column of ones)
+  float* dW;
+  int64_t M, slice_rows, part_off, out0;
+  int R, C, ldi, ldw, c0, tiles_c, n_tiles, block0;
 };
 
-// part[s][r][c] = sum over the rows m of slice s of dZ[m][r] In[m][c] (row-major dZ [M][R],
-// In [M][ldi]).  One block of kWgradWaves waves per (64 x 64 output tile, slice): wave w takes
-// the slice's groups of 16 rows w, w + kWgradWaves, ... on v_mfma_f32_32x32x2_f32 (exact f32,
-// an fma chain) with a 2 x 2 grid of 32x32 accumulators -- lane (i = l & 31, h = l >> 5) loads
-// dZ[m + h][r0 + 32a + i] (the A operand, dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row
-// segments per half-wave -- then the waves' accumulators are summed in wave order through LDS
-// (deterministic).  Several waves per SIMD hide the load latency.
 template <int = 0>
-__global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_per_eu(3))) k_wgrad(
-    const float* __restrict__ dZ, int R, const float* __restrict__ In, int ldi, int C, int64_t M,
-    int tiles_c, int n_tiles, int64_t slice_rows, float* __restrict__ part) {
+__global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_per_eu(3))) k_wgrad_batch(
+    const WgradJob* __restrict__ jobs, int n_jobs, int S, float* __restrict__ part) {
   typedef float f16v_ __attribute__((ext_vector_type(16)));
   __shared__ float red[kWgradWaves - 1][16][64];
-  const int tile = blockIdx.x, w = threadIdx.x >> 6;
+  int j = 0;
+  while (j + 1 < n_jobs && (int)blockIdx.x >= jobs[j + 1].block0) ++j;
+  const WgradJob& jb = jobs[j];
+  const int b = (int)blockIdx.x - jb.block0;
+  const int tile = b % jb.n_tiles, slice = b / jb.n_tiles;
+  const float* __restrict__ dZ = jb.dZ;
+  const float* __restrict__ In = jb.In;
+  const int R = jb.R, C = jb.C, ldi = jb.ldi;
+  const int w = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-  const int r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
-  const int64_t m0 = (int64_t)blockIdx.y * slice_rows;
-  const int64_t m1 = std::min<int64_t>(M, m0 + slice_rows);
+  const int r0 = (tile / jb.tiles_c) * 64, c0 = (tile % jb.tiles_c) * 64;
+  const int64_t m0 = (int64_t)slice * jb.slice_rows;
+  const int64_t m1 = std::min<int64_t>(jb.M, m0 + jb.slice_rows);
   f16v_ acc[4] = {};
   constexpr int U = 8;  // k-steps (2 rows each) per group
-  // clamped row / column indices: loads are unconditional; a row past the slice is zeroed in the
-  // A operand (its B values come from a real, finite row), clamped columns / rows feed only
-  // outputs that are never stored
+  // clamped indices as in k_wgrad: loads are unconditional, rows past the slice are zeroed in
+  // the A operand, clamped columns / rows feed only outputs that are never stored
   const int ia = std::min(r0 + i, R - 1), ib = std::min(r0 + 32 + i, R - 1);
-  const int ja = std::min(c0 + i, C - 1), jb = std::min(c0 + 32 + i, C - 1);
+  const int ja = std::min(c0 + i, C - 1), jbb = std::min(c0 + 32 + i, C - 1);
   for (int64_t m = m0 + (int64_t)w * 2 * U; m < m1; m += (int64_t)kWgradWaves * 2 * U) {
     float a0[U], a1[U], b0[U], b1[U];
     int ok = 0;
@@ -480,8 +487,13 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
       ok |= row < m1 ? (1 << u) : 0;
       const int64_t rc = row < m1 ? row : m1 - 1;
       const float* zr = dZ + rc * R;
-      const float* ir = In + rc * ldi;
-      a0[u] = zr[ia]; a1[u] = zr[ib]; b0[u] = ir[ja]; b1[u] = ir[jb];
+      a0[u] = zr[ia]; a1[u] = zr[ib];
+      if (In) {
+        const float* ir = In + rc * ldi;
+        b0[u] = ir[ja]; b1[u] = ir[jbb];
+      } else {
+        b0[u] = 1.f; b1[u] = 1.f;
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -493,7 +505,6 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
       acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, b1[u], acc[3], 0, 0, 0);
     }
   }
-  // one accumulator at a time through a 12 KiB LDS buffer (keeps LDS small and occupancy up)
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (w > 0) {
@@ -510,9 +521,7 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
     __syncthreads();
   }
   if (w != 0) return;
-  // 32x32 accumulator: register q holds row (q & 3) + 8 (q >> 2) + 4 h, column i; acc[2a + b]
-  // is rows 32a.., columns 32b..
-  float* out = part + (size_t)blockIdx.y * R * C;
+  float* out = part + jb.part_off + (size_t)slice * R * C;
   const bool cok[2] = {c0 + i < C, c0 + 32 + i < C};
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -523,88 +532,125 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
     }
 }
 
-// dW[r][c0 + c] = sum_{s < slots} part[s][r][c]
+// element e of the concatenated outputs (job j owns [out0, out0 + R C)): the sum over slices in
+// slice order
 template <int = 0>
-__global__ void k_split_reduce(const float* __restrict__ part, int slots, int R, int C,
-                               float* __restrict__ dW, int ldw, int c0) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t n = (int64_t)R * C;
-  if (i >= n) return;
+__global__ void k_split_reduce_batch(const WgradJob* __restrict__ jobs, int n_jobs, int S,
+                                     int64_t total, const float* __restrict__ part) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  int j = 0;
+  while (j + 1 < n_jobs && e >= jobs[j + 1].out0) ++j;
+  const WgradJob& jb = jobs[j];
+  const int64_t n = (int64_t)jb.R * jb.C, i = e - jb.out0;
+  const float* p = part + jb.part_off + i;
   float acc = 0.f;
-  for (int k = 0; k < slots; ++k) acc += part[(int64_t)k * n + i];
-  const int r = (int)(i / C), c = (int)(i % C);
-  dW[(int64_t)r * ldw + c0 + c] = acc;
-}
-
-// row-major dW[R][ldw] (columns c0 .. c0+C) = dZ[M][R]^T @ In[M][C]
-int grad_gemm(const GemmCtx& g, const float* dZ, int R, const float* In, int C, int64_t M,
-              float* dW, int ldw, int c0) {
-  const int tiles_r = (R + 63) / 64, tiles_c = (C + 63) / 64, n_tiles = tiles_r * tiles_c;
-  // slices: about 3 blocks (12 waves, the kernel's occupancy) per CU over the tiles, at least
-  // kSliceRows batch rows each -- fewer slices, less partial-sum traffic for k_split_reduce
-  int64_t S = std::max<int64_t>(1, (256 * 3 + n_tiles - 1) / n_tiles);
-  S = std::min<int64_t>(S, kSplitMax);
-  S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
-  int64_t slice_rows = (M + S - 1) / S;
-  slice_rows = (slice_rows + 15) / 16 * 16;  // whole k-step groups
-  S = std::max<int64_t>(1, (M + slice_rows - 1) / slice_rows);
-  const dim3 grid((unsigned)n_tiles, (unsigned)S);
-  ProfScope prof("k_wgrad", g.st);
-  k_wgrad<><<<grid, dim3(64 * kWgradWaves), 0, g.st>>>(dZ, R, In, C, C, M, tiles_c, n_tiles,
-                                                      slice_rows, g.part);
-  if (int rc = check_launch("k_wgrad")) return rc;
-  const int64_t n = (int64_t)R * C;
-  k_split_reduce<><<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, g.st>>>(g.part, (int)S, R, C,
-                                                                            dW, ldw, c0);
-  return check_launch("k_split_reduce");
+  for (int k = 0; k < S; ++k) acc += p[(int64_t)k * n];
+  const int r = (int)(i / jb.C), c = (int)(i % jb.C);
+  jb.dW[(int64_t)r * jb.ldw + jb.c0 + c] = acc;
 }
 
 namespace {
+constexpr int kMaxWgradJobs = 3 * kMaxLin;
+static_assert(kMaxWgradJobs * sizeof(WgradJob) <= kWgradTableBytes, "job table");
 
-// db[r] = sum_m dZ[m][r] (row-major dZ [M][R]) in a fixed order: per chunk of rows a partial
-// column sum (4 row groups x 64 consecutive columns per block, coalesced), then the partials in
-// chunk order.  Replaces a rocBLAS gemv that took ~0.3 ms per bias at M = 38k.
-
-template <int = 0>
-__global__ void __launch_bounds__(256) k_colsum_partial(const float* __restrict__ dZ, int R,
-                                                        int64_t M, int64_t rows_per_chunk,
-                                                        float* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.y * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
-  const int64_t m0 = (int64_t)blockIdx.x * rows_per_chunk;
-  const int64_t m1 = m0 + rows_per_chunk < M ? m0 + rows_per_chunk : M;
-  float acc = 0.f;
-  if (c < R)
-    for (int64_t m = m0 + g; m < m1; m += 4) acc += dZ[m * R + c];
-  red[g][threadIdx.x & 63] = acc;
-  __syncthreads();
-  if (g == 0 && c < R)
-    part[(int64_t)blockIdx.x * R + c] = ((red[0][c & 63] + red[1][c & 63]) + red[2][c & 63]) + red[3][c & 63];
+// the slice count of a batch: about 3 blocks (12 waves, the kernel's occupancy) per CU over all
+// the batch's tiles, at least kSliceRows rows per slice
+int batch_slices(int64_t total_tiles, int64_t M) {
+  int64_t S = std::max<int64_t>(1, (256 * 3 + total_tiles - 1) / total_tiles);
+  S = std::min<int64_t>(S, kSplitMax);
+  S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
+  return (int)S;
 }
 
-// one wave per column: lane l sums chunks l, l + 64, ... in order, then a fixed xor-butterfly
-// (deterministic; a thread per column walking all chunks was latency-bound at ~55 us a call)
-template <int = 0>
-__global__ void __launch_bounds__(256) k_colsum_final(const float* __restrict__ part, int R,
-                                                      int chunks, float* __restrict__ db) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (c >= R) return;  // whole wave
-  float acc = 0.f;
-  for (int k = lane; k < chunks; k += 64) acc += part[(int64_t)k * R + c];
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d);
-  if (lane == 0) db[c] = acc;
+struct WgradBatch {
+  std::vector<WgradJob> jobs;
+  void weight(const float* dZ, int R, const float* In, int C, int64_t M, float* dW, int ldw, int c0) {
+    WgradJob j{};
+    j.dZ = dZ; j.In = In; j.dW = dW; j.M = M; j.R = R; j.C = C; j.ldi = C; j.ldw = ldw; j.c0 = c0;
+    jobs.push_back(j);
+  }
+  void bias(const float* dZ, int R, int64_t M, float* db) {
+    WgradJob j{};
+    j.dZ = dZ; j.In = nullptr; j.dW = db; j.M = M; j.R = R; j.C = 1; j.ldi = 1; j.ldw = 1; j.c0 = 0;
+    jobs.push_back(j);
+  }
+  // lay out tiles, slices and partial offsets; returns the partial floats needed
+  size_t plan(int& S) {
+    int64_t tiles = 0, Mmax = 1;
+    for (auto& j : jobs) {
+      j.tiles_c = (j.C + 63) / 64;
+      j.n_tiles = ((j.R + 63) / 64) * j.tiles_c;
+      tiles += j.n_tiles;
+      Mmax = std::max(Mmax, j.M);
+    }
+    S = batch_slices(std::max<int64_t>(tiles, 1), Mmax);
+    int64_t block = 0, out = 0;
+    size_t off = 0;
+    for (auto& j : jobs) {
+      j.slice_rows = ((j.M + S - 1) / S + 15) / 16 * 16;
+      j.block0 = (int)block;
+      block += (int64_t)j.n_tiles * S;
+      j.part_off = (int64_t)off;
+      off += (size_t)S * j.R * j.C;
+      j.out0 = out;
+      out += (int64_t)j.R * j.C;
+    }
+    return off;
+  }
+  // table: kMaxWgradJobs * sizeof(WgradJob) bytes of device memory; part: the plan's floats
+  int run(void* table, float* part, hipStream_t st) {
+    if (jobs.empty()) return NRT_OK;
+    if ((int)jobs.size() > kMaxWgradJobs) { set_error("weight gradients: too many jobs"); return NRT_EINVAL; }
+    int S = 1;
+    plan(S);
+    int64_t blocks = 0, total = 0;
+    for (auto& j : jobs) { blocks += (int64_t)j.n_tiles * S; total += (int64_t)j.R * j.C; }
+    NRT_HIP(hipMemcpyAsync(table, jobs.data(), jobs.size() * sizeof(WgradJob), hipMemcpyHostToDevice, st));
+    const WgradJob* tj = (const WgradJob*)table;
+    {
+      ProfScope prof("k_wgrad", st);
+      k_wgrad_batch<><<<dim3((unsigned)blocks), dim3(64 * kWgradWaves), 0, st>>>(tj, (int)jobs.size(), S, part);
+      if (int rc = check_launch("k_wgrad_batch")) return rc;
+    }
+    k_split_reduce_batch<><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
+        tj, (int)jobs.size(), S, total, part);
+    return check_launch("k_split_reduce_batch");
+  }
+};
+
+// the jobs of one nrt_mlp_backward (rows M) or nrt_mlp_grad_backward (weights over the stacked
+// 2M rows, biases over the M primal rows): shared by the workspace size and the launch
+template <class F>
+void backward_jobs(const MlpDev& d, bool grad_bwd, F&& f) {
+  const int L = d.n_hidden, H = d.hidden;
+  for (int l = 0; l <= L + 1; ++l) {
+    const bool outl = l == L + 1;
+    const int R = outl ? d.out : H;
+    if (l == 0) {
+      f(l, R, 0, d.dp, d.dp, 0);
+    } else {
+      const int i = l - 1;
+      const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
+      const int C = H + (skip ? d.dp : 0);
+      f(l, R, 1, H, C, 0);
+      if (skip) f(l, R, 2, d.dp, C, H);
+    }
+    if (!(grad_bwd && outl)) f(l, R, 3, 1, 1, 0);  // bias
+  }
 }
 
-int grad_bias(const float* dZ, int R, int64_t M, float* part, float* db, hipStream_t st) {
-  if (R > kBiasMaxR) { set_error("bias gradient: more than 256 rows"); return NRT_EINVAL; }
-  const int64_t rpc = std::max<int64_t>(64, (M + kBiasChunks - 1) / kBiasChunks);
-  const int chunks = (int)((M + rpc - 1) / rpc);
-  k_colsum_partial<><<<dim3(chunks, (R + 63) / 64), dim3(256), 0, st>>>(dZ, R, M, rpc, part);
-  k_colsum_final<><<<dim3((R + 3) / 4), dim3(256), 0, st>>>(part, R, chunks, db);
-  return check_launch("k_colsum");
+size_t batch_part_floats(const MlpDev& d, int64_t M, bool grad_bwd) {
+  WgradBatch b;
+  backward_jobs(d, grad_bwd, [&](int, int R, int kind, int C, int ldw, int c0) {
+    if (kind == 3) b.bias(nullptr, R, M, nullptr);
+    else b.weight(nullptr, R, nullptr, C, grad_bwd ? 2 * M : M, nullptr, ldw, c0);
+  });
+  int S = 1;
+  return b.plan(S);
 }
 }  // namespace
+
 
 }  // namespace nrt
 
@@ -619,7 +665,7 @@ size_t nrt_mlp_backward_workspace_bytes(const nrt_mlp* m, int64_t M) {
   const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
   const size_t enc = (size_t)M * d.dp * 4;
   return 3 * a256(lay) + 2 * a256(enc) + 2 * a256(enc_tile_bytes(d, M)) +
-         a256((size_t)kBiasChunks * kBiasMaxR * 4) + a256(split_part_floats(d) * 4);
+         a256(kWgradTableBytes) + a256(batch_part_floats(d, M, false) * 4);
 }
 
 int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int64_t M,
@@ -681,27 +727,20 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     if ((rc = check_launch("k_mlp_backward32"))) return rc;
   }
   if (!dweights && !dbiases) return NRT_OK;
-  const GemmCtx gc{w.kpart, st};
+  // every weight and bias gradient in one batched split-K launch (+ its slice reduction)
   const size_t lay = (size_t)M * H;
-  for (int l = 0; l <= L + 1; ++l) {
-    const bool outl = l == L + 1;
-    const int R = outl ? d.out : H;
-    const float* dZ = outl ? dy : w.dZ + (size_t)l * lay;
-    if (dweights && dweights[l]) {
-      if (l == 0) {
-        rc = grad_gemm(gc, dZ, R, w.Eraw, d.dp, M, dweights[0], d.dp, 0);
-      } else {
-        const int i = l - 1;
-        const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
-        const int C = H + (skip ? d.dp : 0);
-        rc = grad_gemm(gc, dZ, R, w.A + (size_t)(l - 1) * lay, H, M, dweights[l], C, 0);
-        if (!rc && skip) rc = grad_gemm(gc, dZ, R, w.Eact, d.dp, M, dweights[l], C, H);
-      }
-      if (rc) return rc;
+  WgradBatch batch;
+  backward_jobs(d, false, [&](int l, int R, int kind, int C, int ldw, int c0) {
+    const float* dZ = l == L + 1 ? dy : w.dZ + (size_t)l * lay;
+    if (kind == 3) {
+      if (dbiases && dbiases[l]) batch.bias(dZ, R, M, dbiases[l]);
+      return;
     }
-    if (dbiases && dbiases[l] && (rc = grad_bias(dZ, R, M, w.part, dbiases[l], st))) return rc;
-  }
-  return NRT_OK;
+    if (!dweights || !dweights[l]) return;
+    const float* In = kind == 0 ? w.Eraw : kind == 1 ? w.A + (size_t)(l - 1) * lay : w.Eact;
+    batch.weight(dZ, R, In, C, M, dweights[l], ldw, c0);
+  });
+  return batch.run(w.part, w.kpart, st);
 }
 
 static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {
@@ -713,8 +752,8 @@ static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {
   sz[4] = (size_t)2 * M * d.dp * 4;   // E0
   sz[5] = sz[4];                      // E1
   sz[6] = (size_t)2 * M * d.out * 4;  // output seed
-  sz[7] = (size_t)kBiasChunks * kBiasMaxR * 4;  // bias partial sums
-  sz[8] = split_part_floats(d) * 4;             // split-K partial products
+  sz[7] = kWgradTableBytes;                          // weight-gradient job table
+  sz[8] = batch_part_floats(d, M, true) * 4;        // batched split-K partial products
   size_t tot = 0;
   for (int i = 0; i < 9; ++i) tot += a256(sz[i]);
   return tot;
@@ -781,30 +820,21 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   k_fill<><<<dim3(std::min<int64_t>(ceil_div64(M * d.out, 256), 1024)), dim3(256), 0, st>>>(
       seed + (size_t)M * d.out, M * d.out, 1.f);
   if ((rc = check_launch("k_fill"))) return rc;
-  const GemmCtx gc{buf[8], st};
   const size_t lay2 = (size_t)M2 * H;
-  for (int l = 0; l <= L + 1; ++l) {
-    const bool outl = l == L + 1;
-    const int R = outl ? d.out : H;
-    const float* dZ = outl ? seed : buf[3] + (size_t)l * lay2;
-    if (dweights && dweights[l]) {
-      if (l == 0) {
-        rc = grad_gemm(gc, dZ, R, buf[4], d.dp, M2, dweights[0], d.dp, 0);
-      } else {
-        const int i = l - 1;
-        const bool skip = !outl && i != L - 1 && (i % d.skip) == 0;
-        const int C = H + (skip ? d.dp : 0);
-        rc = grad_gemm(gc, dZ, R, buf[2] + (size_t)(l - 1) * lay2, H, M2, dweights[l], C, 0);
-        if (!rc && skip) rc = grad_gemm(gc, dZ, R, buf[5], d.dp, M2, dweights[l], C, H);
-      }
-      if (rc) return rc;
+  // the out layer's bias takes no gradient from J (its tangent rows carry no bias)
+  if (dbiases && dbiases[L + 1]) NRT_HIP(hipMemsetAsync(dbiases[L + 1], 0, (size_t)d.out * 4, st));
+  WgradBatch batch;
+  backward_jobs(d, true, [&](int l, int R, int kind, int C, int ldw, int c0) {
+    const float* dZ = l == L + 1 ? seed : buf[3] + (size_t)l * lay2;
+    if (kind == 3) {  // bias: the primal rows only
+      if (dbiases && dbiases[l]) batch.bias(dZ, R, M, dbiases[l]);
+      return;
     }
-    if (dbiases && dbiases[l]) {
-      if (outl) NRT_HIP(hipMemsetAsync(dbiases[l], 0, (size_t)R * 4, st));
-      else if ((rc = grad_bias(dZ, R, M, part, dbiases[l], st))) return rc;
-    }
-  }
-  return NRT_OK;
+    if (!dweights || !dweights[l]) return;
+    const float* In = kind == 0 ? buf[4] : kind == 1 ? buf[2] + (size_t)(l - 1) * lay2 : buf[5];
+    batch.weight(dZ, R, In, C, M2, dweights[l], ldw, c0);
+  });
+  return batch.run(part, buf[8], st);
 }
 
 }  // extern "C"

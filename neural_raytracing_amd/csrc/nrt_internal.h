@@ -12,6 +12,16 @@
 
 struct nrt_prog;
 
+// A row program (RProgDev) for the FP32 / fp32-split shading kernels (nrt_shade_ring.hip), built on
+// first use from the host copies of the MLPs' weights.
+struct nrt_rprog {
+  nrt::RProgDev d{};
+  void* buf = nullptr;
+  bool built = false;    // build attempted
+  bool ok = false;       // false: some MLP has a shape without a compiled kernel
+  ~nrt_rprog() { if (buf) (void)hipFree(buf); }
+};
+
 struct nrt_mlp {
   nrt_mlp_desc desc;
   nrt::MlpDev host_dev;          // host copy of the device descriptor
@@ -38,6 +48,10 @@ struct nrt_mlp {
   std::vector<char> gather_f16;   // section kind (nrt_refresh.hip SecKind)
   bool refreshed = false;
   bool split_refreshed = false;  // the refresh also re-split stream3 (fp32-split march)
+  // single-MLP FP32 row program (nrt_shade_ring.hip) for nrt_mlp_forward on the ring engine;
+  // nrt_mlp_refresh gathers its stream and bias table too once it exists
+  mutable nrt_rprog solo32;
+  bool solo_in_refresh = false;  // the refresh maps cover solo32
   ~nrt_mlp();
 };
 
@@ -47,16 +61,6 @@ struct nrt_prog {
   void* buf = nullptr;
   bool ok = false;       // false: some MLP has a shape without a compiled program kernel
   ~nrt_prog() { if (buf) (void)hipFree(buf); }
-};
-
-// A row program (RProgDev) for the FP32 / fp32-split shading kernels (nrt_shade_ring.hip), built on
-// first use from the host copies of the MLPs' weights.
-struct nrt_rprog {
-  nrt::RProgDev d{};
-  void* buf = nullptr;
-  bool built = false;    // build attempted
-  bool ok = false;       // false: some MLP has a shape without a compiled kernel
-  ~nrt_rprog() { if (buf) (void)hipFree(buf); }
 };
 
 struct nrt_sdf {

@@ -204,6 +204,9 @@ int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const f
 
 // ---- FP32 / fp32-split shading on the row-program ring engines (nrt_shade_ring.hip) ----
 int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out);
+int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st);
+bool solo_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
+                       void*& stream_dst, void*& bias_dst);
 int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
                const float* lscale, float* rgb, float* weights_out, int precision, hipStream_t st);

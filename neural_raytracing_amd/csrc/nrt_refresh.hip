@@ -6,7 +6,7 @@
 // padded biases, out.weight row 0 -- through a per-element index map built once on the host by
 // the same loops as nrt_pack.hip.  The FP32 ring stream is refreshed too (the FP32 march of a
 // training loop runs on it), and so is the fp32-split stream (folded, scaled and split into f16
-// halves on the device, k_gather_split); the FP16 ring / program streams are not, and a refreshed
+// halves on the device, k_refresh_all); the FP16 ring / program streams are not, and a refreshed
 // handle refuses those paths (ring_supported, build_program).
 #include <hip/hip_runtime.h>
 
@@ -17,15 +17,6 @@
 namespace nrt {
 namespace {
 
-template <typename T>
-__global__ void k_gather(T* __restrict__ dst, const int* __restrict__ map, int64_t n,
-                         const float* __restrict__ src) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int k = map[i];
-  dst[i] = (T)(k < 0 ? 0.f : src[k]);
-}
-
 // per-layer factors of the split stream (nrt_pack.hip): value = (x * fold[l]) * scale[l]
 struct SplitCoef {
   float fold_w[kMaxLin], fold_b[kMaxLin], scale[kMaxLin];
@@ -33,30 +24,72 @@ struct SplitCoef {
 // map entries of the split sections: source index | layer << 25 | part << 30 (-1 = padding)
 constexpr int kSplitIdxBits = 25;
 
-// split stream halves (part 0: hi = RNE_f16(v), part 1: lo = RNE_f16(v - hi)) or, BIAS, the
-// scaled f32 biases -- the packer's arithmetic, on the device
-template <bool BIAS>
-__global__ void k_gather_split(void* __restrict__ dst, const int* __restrict__ map, int64_t n,
-                               const float* __restrict__ src, SplitCoef c) {
+enum SecKind { SEC_F32 = 0, SEC_F16 = 1, SEC_SPLIT = 2, SEC_SPLIT_BIAS = 3 };
+
+// Split sections: part 0 hi = RNE_f16(v), part 1 lo = RNE_f16(v - hi), or the scaled f32 biases
+// -- the packer's arithmetic, on the device.
+// One launch for the staging copy of every weight / bias tensor and one for every section's
+// gather (round 2 issued a hipMemcpyAsync per tensor and a k_gather per section: ~60 launches per
+// MLP, ~600 per training step).  Tables ride in the kernel arguments.
+constexpr int kMaxStage = 2 * kMaxLin;
+struct StageTable {
+  const float* src[kMaxStage];
+  int64_t off[kMaxStage + 1];  // prefix offsets into gather_src
+  int n;
+};
+constexpr int kMaxSections = 96;  // 4 per layer + the streams (the 16-layer spatial MLP: 78)
+struct SectionTable {
+  void* dst[kMaxSections];
+  int64_t off[kMaxSections + 1];  // prefix offsets into the concatenated map
+  int kind[kMaxSections];
+  int n;
+};
+
+__global__ void k_stage(StageTable t, float* __restrict__ dst) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int v = map[i];
-  if (v < 0) {
-    if (BIAS) reinterpret_cast<float*>(dst)[i] = 0.f;
-    else reinterpret_cast<_Float16*>(dst)[i] = (_Float16)0.f;
-    return;
+  if (i >= t.off[t.n]) return;
+  int lo = 0, hi = t.n - 1;  // the last tensor whose offset is <= i (binary search)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.off[mid] <= i) lo = mid; else hi = mid - 1;
   }
-  const int k = v & ((1 << kSplitIdxBits) - 1), l = (v >> kSplitIdxBits) & 31, part = (v >> 30) & 1;
-  if (BIAS) {
-    reinterpret_cast<float*>(dst)[i] = (src[k] * c.fold_b[l]) * c.scale[l];
-    return;
-  }
-  const float w = (src[k] * c.fold_w[l]) * c.scale[l];
-  const _Float16 hi = (_Float16)w;
-  reinterpret_cast<_Float16*>(dst)[i] = part ? (_Float16)(w - (float)hi) : hi;
+  const int q = lo;
+  dst[i] = t.src[q][i - t.off[q]];
 }
 
-enum SecKind { SEC_F32 = 0, SEC_F16 = 1, SEC_SPLIT = 2, SEC_SPLIT_BIAS = 3 };
+__global__ void k_refresh_all(SectionTable t, const int* __restrict__ map,
+                              const float* __restrict__ src, SplitCoef c) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.off[t.n]) return;
+  int lo = 0, hi = t.n - 1;  // the last section whose offset is <= i (empty sections: skipped)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (t.off[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  const int q = lo;
+  const int64_t j = i - t.off[q];
+  const int v = map[i];
+  switch (t.kind[q]) {
+    case SEC_F32: reinterpret_cast<float*>(t.dst[q])[j] = v < 0 ? 0.f : src[v]; break;
+    case SEC_F16: reinterpret_cast<_Float16*>(t.dst[q])[j] = (_Float16)(v < 0 ? 0.f : src[v]); break;
+    default: {
+      const bool bias = t.kind[q] == SEC_SPLIT_BIAS;
+      if (v < 0) {
+        if (bias) reinterpret_cast<float*>(t.dst[q])[j] = 0.f;
+        else reinterpret_cast<_Float16*>(t.dst[q])[j] = (_Float16)0.f;
+        break;
+      }
+      const int k = v & ((1 << kSplitIdxBits) - 1), l = (v >> kSplitIdxBits) & 31, part = (v >> 30) & 1;
+      if (bias) {
+        reinterpret_cast<float*>(t.dst[q])[j] = (src[k] * c.fold_b[l]) * c.scale[l];
+      } else {
+        const float w = (src[k] * c.fold_w[l]) * c.scale[l];
+        const _Float16 hi = (_Float16)w;
+        reinterpret_cast<_Float16*>(t.dst[q])[j] = part ? (_Float16)(w - (float)hi) : hi;
+      }
+    }
+  }
+}
 struct Section {
   void* dst;
   int64_t n;
@@ -66,7 +99,8 @@ struct Section {
 // The fragment layouts of nrt_pack.hip, as source indices into [W_0 .. W_{L+1} | b_0 .. b_{L+1}]
 // (row-major nn.Linear weights), -1 for padding.
 void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& secs,
-                int64_t& n_src) {
+                int64_t& n_src, bool& solo) {
+  solo = false;
   const nrt_mlp_desc& d = m->desc;
   const MlpDev& md = m->host_dev;
   const int in = d.in_size, H = d.hidden, L = d.num_layers, O = d.out, F = d.freqs;
@@ -189,6 +223,20 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
         map.push_back(r < ls[li].R ? (int)((ls[li].boff + r) | ((int64_t)li << kSplitIdxBits)) : -1);
     end();
   }
+  // the single-MLP FP32 row program of nrt_mlp_forward on the ring engine (nrt_shade_ring.hip)
+  {
+    std::vector<int> smap, bmap;
+    void *sdst = nullptr, *bdst = nullptr;
+    if (solo_refresh_maps(m, smap, bmap, sdst, bdst)) {
+      begin(sdst, SEC_F32);
+      map.insert(map.end(), smap.begin(), smap.end());
+      end();
+      begin(bdst, SEC_F32);
+      map.insert(map.end(), bmap.begin(), bmap.end());
+      end();
+      solo = true;
+    }
+  }
 }
 
 }  // namespace
@@ -203,7 +251,9 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
   if (!m->gather_map) {
     std::vector<int> map;
     std::vector<Section> secs;
-    build_maps(m, map, secs, m->n_src);
+    bool solo = false;
+    build_maps(m, map, secs, m->n_src, solo);
+    m->solo_in_refresh = solo;
     if (map.size() > (size_t)INT32_MAX) { set_error("nrt_mlp_refresh: MLP too large"); return NRT_EINVAL; }
     NRT_HIP(hipMalloc(&m->gather_map, map.size() * sizeof(int)));
     NRT_HIP(hipMemcpy(m->gather_map, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -214,22 +264,28 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
       m->gather_f16.push_back((char)q.kind);
     }
   }
-  // stage [W_0 .. W_{L+1} | b_0 .. b_{L+1}] from the caller's device tensors
+  // stage [W_0 .. W_{L+1} | b_0 .. b_{L+1}] from the caller's device tensors (one launch)
   const int n_lin = m->desc.num_layers + 2;
-  size_t off = 0;
-  for (int l = 0; l < n_lin; ++l) {
-    const size_t n = m->host_w[l].size();
-    if (!weights[l]) { set_error("nrt_mlp_refresh: null weight"); return NRT_EINVAL; }
-    NRT_HIP(hipMemcpyAsync(m->gather_src + off, weights[l], n * 4, hipMemcpyDeviceToDevice, st));
-    off += n;
+  if (2 * n_lin > kMaxStage || m->gather_dst.size() > (size_t)kMaxSections) {
+    set_error("nrt_mlp_refresh: too many layers");
+    return NRT_EINVAL;
   }
-  for (int l = 0; l < n_lin; ++l) {
-    const size_t n = (size_t)(l == n_lin - 1 ? m->desc.out : m->desc.hidden);
-    if (!biases[l]) { set_error("nrt_mlp_refresh: null bias"); return NRT_EINVAL; }
-    NRT_HIP(hipMemcpyAsync(m->gather_src + off, biases[l], n * 4, hipMemcpyDeviceToDevice, st));
-    off += n;
+  StageTable stg{};
+  int64_t off = 0;
+  for (int l = 0; l < 2 * n_lin; ++l) {
+    const bool w = l < n_lin;
+    const int ll = w ? l : l - n_lin;
+    const float* p = w ? weights[ll] : biases[ll];
+    if (!p) { set_error(w ? "nrt_mlp_refresh: null weight" : "nrt_mlp_refresh: null bias"); return NRT_EINVAL; }
+    stg.src[l] = p;
+    stg.off[l] = off;
+    off += w ? (int64_t)m->host_w[ll].size() : (int64_t)(ll == n_lin - 1 ? m->desc.out : m->desc.hidden);
   }
-  if ((int64_t)off != m->n_src) { set_error("nrt_mlp_refresh: layer sizes changed"); return NRT_EINVAL; }
+  stg.off[2 * n_lin] = off;
+  stg.n = 2 * n_lin;
+  if (off != m->n_src) { set_error("nrt_mlp_refresh: layer sizes changed"); return NRT_EINVAL; }
+  k_stage<<<dim3((unsigned)((off + 255) / 256)), dim3(256), 0, st>>>(stg, m->gather_src);
+  if (int rc = check_launch("k_stage")) return rc;
   const MlpDev& md = m->host_dev;
   const bool fold = m->desc.activation == NRT_ACT_SOFTPLUS;
   const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
@@ -239,25 +295,22 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
     coef.fold_b[l] = fold && l < n_lin - 1 ? kLog2e : 1.f;
     coef.scale[l] = 1.f / md.scale3[l];  // a power of two: exact
   }
+  // every section's gather (one launch)
+  SectionTable sec{};
   int64_t moff = 0;
   for (size_t q = 0; q < m->gather_dst.size(); ++q) {
-    const int64_t n = m->gather_n[q];
-    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
-    if (n > 0) {
-      const int kind = m->gather_f16[q];
-      const int* mp = m->gather_map + moff;
-      if (kind == SEC_F16)
-        k_gather<_Float16><<<grid, block, 0, st>>>((_Float16*)m->gather_dst[q], mp, n, m->gather_src);
-      else if (kind == SEC_F32)
-        k_gather<float><<<grid, block, 0, st>>>((float*)m->gather_dst[q], mp, n, m->gather_src);
-      else if (kind == SEC_SPLIT)
-        k_gather_split<false><<<grid, block, 0, st>>>(m->gather_dst[q], mp, n, m->gather_src, coef);
-      else
-        k_gather_split<true><<<grid, block, 0, st>>>(m->gather_dst[q], mp, n, m->gather_src, coef);
-    }
-    moff += n;
+    sec.dst[q] = m->gather_dst[q];
+    sec.kind[q] = m->gather_f16[q];
+    sec.off[q] = moff;
+    moff += m->gather_n[q];
   }
-  if (int rc = check_launch("k_gather")) return rc;
+  sec.n = (int)m->gather_dst.size();
+  sec.off[sec.n] = moff;
+  if (moff > 0) {
+    k_refresh_all<<<dim3((unsigned)((moff + 255) / 256)), dim3(256), 0, st>>>(sec, m->gather_map,
+                                                                             m->gather_src, coef);
+    if (int rc = check_launch("k_refresh_all")) return rc;
+  }
   m->refreshed = true;
   m->split_refreshed = m->n_src < (1 << kSplitIdxBits);
   return NRT_OK;

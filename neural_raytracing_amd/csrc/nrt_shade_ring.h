@@ -548,5 +548,28 @@ __global__ void __launch_bounds__(64 * WV, 1) k_bsdf_r(
   E.drain();
 }
 
+// nrt_mlp_forward of one MLP on its single-MLP row program: y [M, out] row-major
+template <int PREC, int D, int WV, class S>
+__global__ void __launch_bounds__(64 * WV, 1) k_mlp_ring(const RProgDev prog, const float* __restrict__ x,
+                                                        int64_t M, float* __restrict__ y, int out) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int64_t per_block = 16 * WV;
+  if ((int64_t)blockIdx.x * per_block >= M) return;
+  Engine<D, WV> E;
+  E.init(prog, smem_c);
+  const int lane = E.lane, j = lane & 15, g = lane >> 4;
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < M; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 16 * E.wv + j;
+    const bool valid = i < M;
+    const int64_t ii = valid ? i : M - 1;
+    const f4v o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
+    if (valid)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < out) y[i * out + 4 * g + r] = o[r];
+  }
+  E.drain();
+}
+
 }  // namespace rprog
 }  // namespace nrt

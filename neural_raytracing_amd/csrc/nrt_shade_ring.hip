@@ -47,7 +47,12 @@ struct Walker {
   std::vector<float>* s32;
   std::vector<_Float16>* s3;
   std::vector<int>* chunks;
-  size_t pieces() const { return split ? s3->size() / 512 : s32->size() / 256; }
+  // map mode (nrt_mlp_refresh): the source index of every FP32 stream element into
+  // [W_0 .. W_{L+1} | b_0 .. b_{L+1}] instead of its value (-1: padding)
+  std::vector<int>* map = nullptr;
+  size_t pieces() const {
+    return map ? map->size() / 256 : split ? s3->size() / 512 : s32->size() / 256;
+  }
   void chunk_begin() { chunks->push_back((int)pieces()); chunks->push_back(0); }
   void chunk_end() { chunks->back() = (int)pieces() - chunks->at(chunks->size() - 2); }
 };
@@ -87,15 +92,25 @@ int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
       if (mx > 0.f && std::isfinite(mx)) (void)std::frexp(mx, &e);
       lscale[l] = std::ldexp(1.f, std::max(-64, std::min(64, 1 - e)));  // max|W| scale in [1, 2)
     }
+  std::vector<int64_t> woff(nl + 1, 0);
+  for (int l = 0; l < nl; ++l) woff[l + 1] = woff[l] + (int64_t)R[l] * C[l];
   auto W = [&](int l, int row, int col) -> float {
     if (row >= R[l] || col < 0 || col >= C[l]) return 0.f;
     return m->host_w[l][(size_t)row * C[l] + col];
+  };
+  auto Widx = [&](int l, int row, int col) -> int {
+    if (row >= R[l] || col < 0 || col >= C[l]) return -1;
+    return (int)(woff[l] + (int64_t)row * C[l] + col);
   };
   auto enc_col = [&](int l, int slot) -> int {
     const int c = slot_col(slot);
     return c < 0 ? -1 : (hid[l] ? H + c : c);
   };
-  auto put32 = [&](float v) { w.s32->push_back(v); };
+  // FP32 element (l, row, col): its value, or in map mode its source index
+  auto put32 = [&](int l, int row, int col) {
+    if (w.map) w.map->push_back(Widx(l, row, col));
+    else w.s32->push_back(W(l, row, col));
+  };
   auto put3 = [&](int l, float v, int part) {
     const float x = v * lscale[l];
     const _Float16 hi = (_Float16)x;
@@ -111,7 +126,7 @@ int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
             for (int lane = 0; lane < 64; ++lane)
               for (int t = 0; t < 4; ++t) {
                 const int g = lane >> 4, s = 4 * u + t;
-                put32(W(l, 16 * sb + (lane & 15), enc_col(l, 4 * s + g)));
+                put32(l, 16 * sb + (lane & 15), enc_col(l, 4 * s + g));
               }
         w.chunk_end();
       }
@@ -140,7 +155,7 @@ int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
           for (int lane = 0; lane < 64; ++lane)
             for (int t = 0; t < 4; ++t) {
               const int g = lane >> 4, s = 4 * u + t;
-              put32(W(l, 32 * ib + 16 * b + (lane & 15), 16 * (s >> 2) + 4 * g + (s & 3)));
+              put32(l, 32 * ib + 16 * b + (lane & 15), 16 * (s >> 2) + 4 * g + (s & 3));
             }
     } else {
       for (int u = 0; u < H / 32; ++u)
@@ -341,6 +356,80 @@ int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const floa
   rc = split ? run.template operator()<2>() : run.template operator()<0>();
   (void)hipFreeAsync(ls, st);
   return rc;
+}
+
+// ---- nrt_mlp_forward on the ring engine (training forwards of the shading MLPs) -------------
+namespace {
+// the compiled shapes; 0 = none
+int solo_shape(const nrt_mlp* m) {
+  const nrt_mlp_desc& d = m->desc;
+  if (d.in_size != 3 || d.latent != 0 || d.out > 16 || d.activation != NRT_ACT_LEAKY_RELU ||
+      d.num_layers + 2 > kMaxLin || (int)m->host_w.size() != d.num_layers + 2)
+    return 0;
+  if (d.hidden == kLightSpec.H && d.freqs == kLightSpec.F) return 1;
+  if (d.hidden == kSpatialSpec.H && d.freqs == kSpatialSpec.F) return 2;
+  if (d.hidden == kBsdfSpec.H && d.freqs == kBsdfSpec.F) return 3;
+  return 0;
+}
+}  // namespace
+
+// the refresh's gather maps of the solo program: its FP32 stream and bias table as source
+// indices into [W_0 .. W_{L+1} | b_0 .. b_{L+1}] (-1 padding); builds the program first
+// (from the host copies, which the refresh then overwrites).  false: not eligible.
+bool solo_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
+                       void*& stream_dst, void*& bias_dst) {
+  if (!solo_shape(m)) return false;
+  nrt_rprog& sp = m->solo32;
+  if (!sp.built && build_rprog({m}, false, sp) != NRT_OK) return false;
+  if (!sp.ok) return false;
+  std::vector<int> chunks;
+  std::vector<float> lscale;
+  Walker w{false, nullptr, nullptr, &chunks, &stream_map};
+  if (walk_mlp(m, w, lscale) != NRT_OK) return false;
+  const nrt_mlp_desc& d = m->desc;
+  int64_t wtot = 0;
+  for (const auto& v : m->host_w) wtot += (int64_t)v.size();
+  int64_t boff = wtot;
+  const int bstride = d.hidden;
+  for (int l = 0; l < d.num_layers + 2; ++l) {
+    const int rows = l == d.num_layers + 1 ? d.out : d.hidden;
+    for (int r = 0; r < bstride; ++r) bias_map.push_back(r < rows ? (int)(boff + r) : -1);
+    boff += rows;
+  }
+  if ((int64_t)stream_map.size() * 4 != sp.d.stream_bytes) return false;
+  stream_dst = const_cast<void*>(sp.d.stream);
+  bias_dst = const_cast<float*>(sp.d.tables);  // biases first (scales follow, 1 in FP32)
+  return true;
+}
+
+// NRT_EUNSUPPORTED when the MLP has no compiled ring shape (or a refreshed handle whose solo
+// program the refresh does not cover)
+int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st) {
+  const int shape = solo_shape(m);
+  if (!shape) return NRT_EUNSUPPORTED;
+  nrt_rprog& sp = m->solo32;
+  if (m->refreshed && !m->solo_in_refresh) return NRT_EUNSUPPORTED;
+  if (!sp.built)
+    if (int rc = build_rprog({m}, false, sp)) return rc;
+  if (!sp.ok) return NRT_EUNSUPPORTED;
+  constexpr int WV = kRWaves;
+  const int64_t want = ceil_div64(M, 16 * WV);
+  const int out = m->desc.out;
+  auto run = [&](auto sh) -> int {
+    using S = decltype(sh);
+    return with_depth<0, WV>(sp.d, [&](auto dd) -> int {
+      constexpr int D = decltype(dd)::value;
+      auto kern = rprog::k_mlp_ring<0, D, WV, S>;
+      const size_t lds = rprog::Engine<D, WV>::lds_bytes(sp.d);
+      if (int r = set_lds(kern, lds)) return r;
+      ProfScope prof("k_mlp_ring32", st);
+      kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want)), dim3(64 * WV), lds, st>>>(sp.d, x, M, y, out);
+      return check_launch("k_mlp_ring32");
+    });
+  };
+  if (shape == 1) return run(rprog::LightShape{});
+  if (shape == 2) return run(rprog::SpatialShape{});
+  return run(rprog::BsdfShape{});
 }
 
 }  // namespace nrt

@@ -242,16 +242,23 @@ def shadowed_light(shapes, lights, it, active, w_isect):
     return d, le, pdf
 
 
-def bsdf_eval(bsdf, it, wo, active):
-    """eval_and_pdf of the supported BSDFs (bsdfs.py:108-118, 364-388, 515-536, 634-637)."""
+def bsdf_eval(bsdf, it, wo, active, feat=None):
+    """eval_and_pdf of the supported BSDFs (bsdfs.py:108-118, 364-388, 515-536, 634-637).
+    `feat`: param_rusin2(it.wi, wo) when the caller already has it."""
     from .bsdf.bsdfs import ComposeSpatialVarying, Conductor, Diffuse, NeuralBSDF, identity_div_pi
     if isinstance(bsdf, ComposeSpatialVarying):
         k = bsdf.sp_var_fn(bsdf.preprocess(it.p)).reshape(it.p.shape[:-1] + (len(bsdf.bsdfs),))
         setattr(it, "nonnormalized_weights", k)
         k = k.sigmoid()
+        # every NeuralBSDF of the mixture reads the same Rusinkiewicz features of (wi, wo): the
+        # reference recomputes them per component (bsdfs.py:634-637); computing them once gives
+        # the same values and the same gradient (autograd sums the components' contributions),
+        # with ~40 forward and ~80 backward launches per component fewer
+        if sum(isinstance(b, NeuralBSDF) for b in bsdf.bsdfs) > 1:
+            feat = param_rusin2(it.wi, wo)
         parts = []
         for b in bsdf.bsdfs:
-            f, pdf = bsdf_eval(b, it, wo, active)
+            f, pdf = bsdf_eval(b, it, wo, active, feat)
             parts.append(torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1))
         spec_pdf = torch.stack(parts, dim=-1)
         setattr(it, "normalized_weights", k)
@@ -260,7 +267,7 @@ def bsdf_eval(bsdf, it, wo, active):
         f, pdf = spec_pdf.sum(dim=-1).split([3, 1], dim=-1)
         return f, pdf.squeeze(-1)
     if isinstance(bsdf, NeuralBSDF):
-        f = bsdf.act(bsdf.mlp(param_rusin2(it.wi, wo)))
+        f = bsdf.act(bsdf.mlp(param_rusin2(it.wi, wo) if feat is None else feat))
         return f, torch.ones(f.shape[:-1], device=f.device)
     if isinstance(bsdf, Diffuse):
         refl = bsdf.reflectance.to(wo.device)

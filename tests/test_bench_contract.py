@@ -6,8 +6,11 @@ import json
 import pathlib
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-BENCH = ROOT / "profiles" / "r02_final/bench.json"
-STATS = ROOT / "profiles" / "r02_final/kernel_stats.csv"
+# the round's final line (bench.py with the CPU baseline) and the rocprofv3 --kernel-trace --stats
+# summary of the same frame (bench.py --no-cpu-baseline --no-extra-legs)
+BENCH = ROOT / "profiles" / "r03" / "final" / "bench.json"
+STATS = ROOT / "profiles" / "r03" / "final" / "kernel_stats.csv"
+PEAK = {"fp32": 157.3, "fp16": 2500.0, "fp32-split": 2500.0}
 
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
@@ -15,6 +18,9 @@ REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 
 def _line():
+    import pytest
+    if not BENCH.exists():
+        pytest.skip("the round's final bench line is not committed yet (tools/r03_final.sh)")
     return json.loads(BENCH.read_text().strip().splitlines()[-1])
 
 
@@ -29,8 +35,11 @@ def test_bench_line_schema():
 
 
 def test_roofline_consistent():
-    r = _line()["roofline"]
-    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s" and r["peak"] == 2500.0
+    b = _line()
+    r = b["roofline"]
+    # the headline is the reference's precision: FP32 on the FP32 MFMA peak
+    assert b["dtype"] == "fp32"
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] == "TFLOP/s" and r["peak"] == PEAK[b["dtype"]]
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-9
     assert abs(r["achieved"] - r["flop_per_launch"] / (r["avg_kernel_ms"] / 1e3) / 1e12) \
         / r["achieved"] < 1e-6
@@ -41,7 +50,7 @@ def test_roofline_consistent():
 def test_rocprof_agrees_with_live_timing():
     r = _line()["roofline"]
     with STATS.open() as f:
-        rows = [row for row in csv.DictReader(f) if "k_march16" in row["Name"]]
-    assert rows, "k_march16 missing from the rocprof summary"
+        rows = [row for row in csv.DictReader(f) if f"{r['kernel']}<" in row["Name"]]
+    assert rows, f"{r['kernel']} missing from the rocprof summary"
     avg_ms = float(rows[0]["AverageNs"]) / 1e6
     assert abs(avg_ms - r["avg_kernel_ms"]) / avg_ms < 0.05

@@ -70,3 +70,67 @@ def test_train_sdf_handle_marches_like_a_fresh_pack(prec):
                     q.mul_(1.01)
     finally:
         nra.set_precision("fp32")
+
+
+SHAPES = {  # the shading MLPs nrt_mlp_forward runs on the ring engine (nrt_shade_ring.hip)
+    "light_10x256_f16": dict(num_layers=10, hidden_size=256, out=3, freqs=16),
+    "spatial_16x256_f128": dict(num_layers=16, hidden_size=256, out=8, freqs=128, sigma=2 << 6),
+    "bsdf_6x96_f64": dict(num_layers=6, hidden_size=96, out=3, freqs=64),
+}
+
+
+def _forward(handle, x, ring=True):
+    from neural_raytracing_amd import _lib
+    from tests.helpers import lib_opt
+    y = torch.empty(x.shape[0], handle_out(handle), device="cuda")
+    lib_opt("shade_ring", 1 if ring else 0)
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    _lib.call("nrt_mlp_forward", handle.value, _lib.ptr(x), None, x.shape[0], _lib.ptr(y),
+              _lib.NRT_FP32, _lib.stream())
+    torch.cuda.synchronize()
+    n = _lib.profile_read("k_mlp_ring32")[1]
+    _lib.profile_enable(False)
+    lib_opt("shade_ring", 1)
+    return y.cpu(), n
+
+
+_OUT = {}
+
+
+def handle_out(h):
+    return _OUT[id(h)]
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_mlp_forward_on_the_ring_engine(shape):
+    """nrt_mlp_forward (FP32) of the shading MLP shapes on the ring engine against the per-wave slab
+    kernel (option shade_ring = 0): exact-f32 MFMA both, different summation orders (1e-5 of the
+    output scale); then the training handle after an in-place weight change (nrt_mlp_refresh
+    gathers the ring program too) against a freshly packed handle of the same weights: equal."""
+    from neural_raytracing_amd.pathtracer._handles import mlp_handle, train_handle
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    torch.manual_seed(11)
+    mlp = SkipConnMLP(in_size=3, device="cpu", **SHAPES[shape]).cuda()
+    x = (torch.rand(5003, 3) * 2 - 1).cuda()
+    h = mlp_handle(mlp)
+    _OUT[id(h)] = mlp.out.out_features
+    ring, n = _forward(h, x, True)
+    slab, n0 = _forward(h, x, False)
+    assert n >= 1 and n0 == 0
+    scale = slab.abs().max().clamp_min(1e-3)
+    assert ((ring - slab).abs().max() / scale) < 1e-5, (ring - slab).abs().max()
+    th = train_handle(mlp)
+    _OUT[id(th)] = mlp.out.out_features
+    for rnd in range(2):
+        with torch.no_grad():
+            for q in mlp.parameters():
+                q.mul_(1.02)
+        th = train_handle(mlp)            # refreshed on the device
+        _OUT[id(th)] = mlp.out.out_features
+        got, n1 = _forward(th, x, True)
+        fresh = mlp_handle(mlp)           # re-packed on the host (the version changed)
+        _OUT[id(fresh)] = mlp.out.out_features
+        want, _ = _forward(fresh, x, True)
+        assert n1 >= 1
+        assert torch.equal(got, want), (rnd, (got - want).abs().max())

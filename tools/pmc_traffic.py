@@ -1,10 +1,10 @@
-"""HBM traffic of one k_march16 launch from the FETCH_SIZE / WRITE_SIZE passes of tools/pmc.sh
--> profiles/pmc_k_march16.json (read by bench.py for roofline.traffic).
+"""HBM traffic of one march launch from the FETCH_SIZE / WRITE_SIZE passes of tools/pmc.sh
+-> profiles/pmc_<kernel>.json (read by bench.py for roofline.traffic).
 
 Corrections (MI355X_MICROARCH.md, HBM): on gfx950 FETCH_SIZE reports half of the bytes of a
 16-B/lane streaming read (x2 here; the ring's buffer_load...lds weight pieces and the ray loads are
 that access form); WRITE_SIZE counts bytes for 16-B stores and per-lane atomics; both are in KiB.
-Usage: python tools/pmc_traffic.py gpurun_out/pmc/p3 gpurun_out/pmc/p4 [size] [precision]
+Usage: python tools/pmc_traffic.py gpurun_out/pmc/p1 gpurun_out/pmc/p2 [size] [precision] [kernel]
 """
 import csv
 import json
@@ -32,12 +32,13 @@ def main():
     fetch_dir, write_dir = sys.argv[1], sys.argv[2]
     size = int(sys.argv[3]) if len(sys.argv) > 3 else 800
     precision = sys.argv[4] if len(sys.argv) > 4 else "fp16"
-    fetch_kib, n1 = counter(fetch_dir, "FETCH_SIZE")
-    write_kib, n2 = counter(write_dir, "WRITE_SIZE")
+    kernel = sys.argv[5] if len(sys.argv) > 5 else "k_march16"
+    fetch_kib, n1 = counter(fetch_dir, "FETCH_SIZE", kernel)
+    write_kib, n2 = counter(write_dir, "WRITE_SIZE", kernel)
     read_b = 2 * fetch_kib * 1024
     write_b = write_kib * 1024
     out = {
-        "kernel": "k_march16", "size": size, "precision": precision,
+        "kernel": kernel, "size": size, "precision": precision,
         "fetch_size_kib": fetch_kib, "write_size_kib": write_kib, "dispatches": [n1, n2],
         "hbm_read_bytes": read_b, "hbm_write_bytes": write_b,
         "hbm_bytes_per_launch": read_b + write_b,
@@ -45,7 +46,7 @@ def main():
                 "separate rocprofv3 --pmc passes of bench.py --size %d --steps 1 --warmup 0 "
                 "--no-extra-legs; the timed frame's launch (first dispatch)" % size,
     }
-    path = os.path.join(ROOT, "profiles", "pmc_k_march16.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))
 
