@@ -308,3 +308,68 @@ def direct_sample(it, active, bsdf, lights, lead, device, shapes=None, w_isect=F
     result = result.clone()
     result[ae] = result[ae] + f[ae] * le[ae]
     return result
+
+
+def path_sample(shapes, rays, bsdf, lights, max_depth, training, sampler, uniforms=None,
+                w_isect=False):
+    """Path.sample with autograd (integrators.py:275-354).  Per bounce the emitter term is
+    ``direct_sample`` on the current interaction (gradients through its normals and point, the
+    BSDF and the light) times the throughput, which the reference detaches after every BSDF
+    sample (:335-337).  The BSDF sample itself needs no gradient: ``nrt_path_bounce`` draws it on
+    the detached interaction with the same uniforms the no-grad Path uses, and updates the
+    (detached) throughput and the active mask.  The spawned rays are then rebuilt with autograd
+    -- origin p, direction from_local(wo) through the differentiable frame (:345,
+    interaction.py:57) -- so the secondary intersection's points and normals carry gradients as
+    in the reference."""
+    from .shapes.sdfs import sdf_handle
+    from .integrators.integrators import _bsdf_handle, _emitter_mode, _light_handle
+    dev = rays.device
+    lead = rays.shape[:-1]
+    it, active = shapes.intersect(rays, primary=training)
+    result = torch.zeros(*lead, 3, device=dev)
+    if not bool(active.any()):
+        return result, active, it
+    original_active = active.clone()
+    shadow, occ = _emitter_mode(w_isect)
+    P = active.numel()
+    nc = len(getattr(bsdf, "bsdfs", [bsdf]))
+    act = active.reshape(-1).to(torch.uint8).contiguous()
+    thr = torch.ones(P, 3, device=dev)      # detached throughput, updated by the bounce
+    scratch = torch.zeros(P, 3, device=dev)  # the bounce's own (gradient-free) emitter sum
+    rays_out = torch.empty(P, 6, device=dev)
+    lib = _lib.load(require_device=True)
+    ws = torch.empty(lib.nrt_path_workspace_bytes(P), dtype=torch.uint8, device=dev)
+    sh = sdf_handle(shapes.sdf)
+    curr = it
+    for depth in range(max_depth):
+        cur = act.bool().reshape(lead)
+        term = direct_sample(curr, cur, bsdf, lights, lead, dev, shapes, w_isect)
+        # a snapshot: autograd keeps this factor for the backward, and the bounce below updates
+        # `thr` in place through a raw pointer (no version bump for autograd to catch)
+        result = result + thr.clone().reshape(*lead, 3) * term
+        if uniforms is not None:
+            u_comp, u_sel = (u.to(dev).float().reshape(P, -1).contiguous() for u in uniforms[depth])
+        else:
+            draws = [sampler.sample(tuple(lead) + (2,), device=dev).reshape(P, 1, 2)
+                     for _ in range(nc)]
+            u_comp = torch.cat(draws, dim=1).contiguous()
+            u_sel = sampler.sample((P,), device=dev).contiguous()
+        with torch.no_grad():
+            cp = curr.p.detach().reshape(P, 3).contiguous()
+            cn = curr.n.detach().reshape(P, 3).contiguous()
+            cw = curr.wi.detach().reshape(P, 3).contiguous()
+            _lib.call("nrt_path_bounce", _bsdf_handle(bsdf), _light_handle(lights), sh, shadow,
+                      occ, int(shapes.max_steps), float(shapes.epsilon), _lib.ptr(cp), _lib.ptr(cn),
+                      _lib.ptr(cw), P, _lib.ptr(act), _lib.ptr(thr), _lib.ptr(scratch),
+                      _lib.ptr(u_comp), _lib.ptr(u_sel), _lib.ptr(rays_out), _lib.ptr(ws),
+                      _lib.precision_code(), _lib.stream())
+        if depth + 1 == max_depth or not bool(act.any()):
+            break  # the reference's last spawn is never shaded (:309, :342)
+        with torch.no_grad():
+            wo = curr.to_local(rays_out[:, 3:].reshape(*lead, 3))
+        d = curr.from_local(wo.detach())
+        curr, hits = shapes.intersect(curr.spawn_rays(d), primary=False)
+        act &= hits.reshape(-1).to(torch.uint8)
+        if not bool(act.any()):
+            break
+    return result, original_active, it

@@ -299,9 +299,12 @@ class Path(Integrator):
         lights = kwargs.get("lights", self.lights)
         shadow, occ = _emitter_mode(kwargs.get("w_isect", False))
         uniforms = kwargs.get("uniforms")
-        if needs_grad(shapes, bsdf, lights):
-            raise _lib.NrtError("Path is not on the HIP training path: render it under "
-                                "torch.no_grad()")
+        if needs_grad(shapes, bsdf, lights, kwargs.get("w_isect")):
+            # training: the emitter terms with autograd, the BSDF samples on
+            # the HIP bounce kernel, the spawned rays rebuilt differentiably
+            from ..differentiable import path_sample
+            return path_sample(shapes, rays, bsdf, lights, self.max_depth, self.training, sampler,
+                               uniforms, kwargs.get("w_isect", False))
         dev = rays.device
         lead = rays.shape[:-1]
         it, active = shapes.intersect(rays, primary=self.training)

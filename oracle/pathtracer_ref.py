@@ -703,6 +703,7 @@ class PathRef:
             u_comp, u_sel = uniforms[depth]
             wo_l, spec = bsdf_sample_ref(bsdf, curr, u_comp, u_sel, active)
             throughput = spec.clamp(min=1e-10) * throughput
+            throughput = throughput.detach()  # "detach to save memory" (integrators.py:336-337)
             active = active & (throughput > 0).any(-1)
             if not active.any():
                 break

@@ -15,7 +15,9 @@ import torch
 import torch.nn.functional as F
 
 from oracle import pathtracer_ref as R
+from oracle import recipes
 from tests.helpers import copy_mlp, seeded
+from tests.report import report
 
 SHAPES = {
     "sdf_8x256_softplus_F16": dict(num_layers=8, hidden_size=256, in_size=3, out=1, freqs=16,
@@ -322,20 +324,122 @@ def test_nerfle_training_gradients_match_oracle():
 
 
 @pytest.mark.gpu
-def test_path_and_envmap_refuse_autograd():
-    """Integrators without a HIP training path fail loudly instead of dropping gradients."""
-    import neural_raytracing_amd.pathtracer as pt
+def test_envmap_refuses_a_light_field():
+    """NeRFLE's envmap needs a PointLights: a LightField fails loudly instead of dropping the
+    light encoding."""
     from neural_raytracing_amd import NrtError
-    from neural_raytracing_amd.pathtracer.integrators import Path
-    from neural_raytracing_amd.pathtracer.lights import PointLights
     from neural_raytracing_amd.pathtracer.shapes import NeRFLE
     _, mine = _perturbed_scene()
     rays = mine["camera"].rays_tile(120, 120, 4, 4, 256)
-    with pytest.raises(NrtError):
-        Path().sample(mine["shape"], rays, mine["bsdf"], lights=mine["lights"])
     nerf = NeRFLE(envmap=True, device="cuda")
     with pytest.raises(NrtError):
-        nerf(rays, mine["lights"])  # envmap needs a PointLights
+        nerf(rays, mine["lights"])
+
+
+def _path_grad_pair():
+    """tests/test_gpu_parity.py's path_nerv-like scene with smooth (softplus) shading MLPs (the
+    leaky_relu kink: see _perturbed_scene) and a non-zero SDF shift."""
+    import tests.test_gpu_parity as P
+    ref, mine = P._path_pair()
+    pairs = [(ref["bsdf"].sp_var_fn, mine["bsdf"].sp_var_fn)]
+    pairs += [(a.mlp, b.mlp) for a, b in zip(ref["bsdf"].bsdfs[:2], mine["bsdf"].bsdfs[:2])]
+    for a, b in pairs:
+        a.act_name = "softplus"
+        b.activation = F.softplus
+    seeded(33)
+    with torch.no_grad():
+        sh = ref["shape"].sdf.shift
+        for a in [sh.init, *sh.layers]:
+            a.weight.normal_(0.0, 0.02)
+            a.bias.zero_()
+        sh.out.weight.normal_(0.0, 0.002)
+        sh.out.bias.zero_()
+    copy_mlp(mine["shape"].sdf.shift, sh)
+    ref["shape"].create_graph = True
+    return ref, mine
+
+
+def _path_params(scene):
+    out = {}
+    sdf = scene["shape"].sdf
+    out["centers"], out["radii"], out["tfs"] = sdf.centers, sdf.radii, sdf.tfs
+    for name, m in [("shift", sdf.shift), ("sp", scene["bsdf"].sp_var_fn),
+                    ("bsdf0", scene["bsdf"].bsdfs[0].mlp), ("bsdf1", scene["bsdf"].bsdfs[1].mlp)]:
+        for i, a in enumerate([m.init, *m.layers, m.out]):
+            out[f"{name}.W{i}"], out[f"{name}.b{i}"] = a.weight, a.bias
+    return out
+
+
+def _oracle_path_grads(ref, dtype, rays, uniforms, w):
+    r = {k: copy.deepcopy(v) for k, v in ref.items()}
+    for m in (r["shape"].sdf, r["bsdf"]):
+        m.to(dtype)
+        for sub in m.modules():
+            if hasattr(sub, "basis_p"):
+                sub.basis_p = sub.basis_p.to(dtype)
+            for k, v in list(vars(sub).items()):
+                if isinstance(v, torch.Tensor) and not isinstance(v, torch.nn.Parameter):
+                    setattr(sub, k, v.to(dtype))
+    for k, v in list(vars(r["lights"]).items()):
+        if isinstance(v, torch.Tensor):
+            setattr(r["lights"], k, v.to(dtype))
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dtype)
+    try:
+        uni = [(a.to(dtype), b.to(dtype)) for a, b in uniforms]
+        img, mask, _ = R.PathRef().sample(r["shape"], rays.to(dtype), r["bsdf"], r["lights"],
+                                          uniforms=uni)
+        (img * w.to(dtype)).sum().backward()
+    finally:
+        torch.set_default_dtype(old)
+    grads = {k: (a.grad if a.grad is not None else torch.zeros_like(a)).detach().double()
+             for k, a in _path_params(r).items()}
+    return img.detach(), grads
+
+
+@pytest.mark.gpu
+def test_path_gradients_match_oracle():
+    """Path (integrators.py:275-354) under autograd, two bounces with injected BSDF-sampling
+    uniforms: loss = <img, w>; the gradient of every parameter -- SphereSDF spheres and shift
+    (both bounces' normals, the secondary hit points through the differentiable spawned rays),
+    the spatial-weights MLP, the NeuralBSDFs -- against float64 oracle autograd, with the
+    reference's detached throughput (:336-337).  Bar per tensor as for pathtrace_sample."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    set_precision("fp32")
+    ref, mine = _path_grad_pair()
+    c2w = recipes.look_at_c2w((0.1, 0.5, 0.9)).unsqueeze(0)
+    ocam = R.NeRFCameraRef(c2w, recipes.nerf_focal(32))
+    rays = ocam.sample_positions(R._tile_positions(0, 0, 32), 32)
+    g = torch.Generator().manual_seed(9)
+    lead = rays.shape[:-1]
+    uniforms = [(torch.rand(*lead, 3, 2, generator=g), torch.rand(*lead, generator=g))
+                for _ in range(2)]
+    w = torch.randn(*lead, 3, generator=g)
+    img64, want = _oracle_path_grads(ref, torch.float64, rays, uniforms, w)
+    img32, ref32 = _oracle_path_grads(ref, torch.float32, rays, uniforms, w)
+    img, mask, _ = Path().sample(mine["shape"], rays.cuda(), mine["bsdf"], lights=mine["lights"],
+                                 uniforms=uniforms)
+    assert img.requires_grad
+    diff = (img.detach().cpu() - img32).abs().amax(-1)
+    # a bounce ray's hit / step flip moves that pixel's whole second-bounce term
+    assert (diff <= 1e-4).float().mean() >= 0.99, diff.max()
+    (img * w.cuda()).sum().backward()
+    got = _path_params(mine)
+    bad, worst = [], 0.0
+    for k, g64 in want.items():
+        gb = got[k].grad
+        gb = torch.zeros_like(g64) if gb is None else gb.detach().cpu().double()
+        scale = g64.abs().max().item()
+        err = (gb - g64).abs().max().item()
+        e32 = (ref32[k] - g64).abs().max().item()
+        worst = max(worst, err / max(scale, 1e-12))
+        if err > max(2e-3 * scale, 4 * e32) + 1e-9:
+            bad.append(f"{k}: err {err:.3g} scale {scale:.3g} fp32-oracle err {e32:.3g}")
+    report("path_gradients_vs_f64", params=len(want), worst_rel=worst,
+           pixels_over_1e4=int((diff > 1e-4).sum()))
+    assert not bad, "\n".join(bad)
+    assert want["shift.W0"].abs().max() > 0 and want["sp.W0"].abs().max() > 0
 
 
 @pytest.mark.gpu
