@@ -652,6 +652,28 @@ __device__ __forceinline__ float sp2(float x) {
   return __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(x));
 }
 
+// Sphere blob part of a SphereSDF (sdfs.py:37-43, utils.py:386-387) for a 32-ray tile: the two
+// lanes of a ray (l, l + 32) sum exp(-k d_i) over the even / odd spheres from the LDS table and
+// add the halves (commutative: both lanes get the same bits) -- half the VALU of every lane
+// walking the whole table.  FP16-path math: fast exp, as spheres_value<true>.
+__device__ __forceinline__ float spheres_value_halves(const SdfDev& s, const float4* sp, int lane,
+                                                      float x, float y, float z) {
+  float acc = 0.f;
+  const float nk = -s.k;
+  for (int i = lane >> 5; i < s.n_spheres; i += 2) {
+    const float4 r0 = sp[4 * i], r1 = sp[4 * i + 1], r2 = sp[4 * i + 2];
+    const float r = sp[4 * i + 3].x;
+    // row-major (I+T): r0 = (m00 m01 m02 m10), r1 = (m11 m12 m20 m21), r2 = (m22 cx cy cz)
+    const float qx = fmaf(r0.z, z, fmaf(r0.y, y, r0.x * x)) - r2.y;
+    const float qy = fmaf(r1.y, z, fmaf(r1.x, y, r0.w * x)) - r2.z;
+    const float qz = fmaf(r2.x, z, fmaf(r1.w, y, r1.z * x)) - r2.w;
+    const float d = sqrtf(qx * qx + qy * qy + qz * qz) - r;
+    acc += __expf(nk * d);
+  }
+  acc += __shfl_xor(acc, 32);
+  return -logf(fmaxf(acc, 1e-4f)) / s.k;
+}
+
 // Chunk schedule of one 8-layer (L hidden, skip period SK) evaluation, fixed at compile time:
 // chunk 0 = the whole init layer (NB row blocks x NE encoding k-steps), chunk 1 + NB i + ib =
 // row block ib of hidden layer i (2NB hidden k-steps, + NE encoding k-steps on skip layers),
@@ -742,6 +764,7 @@ struct Engine {
   uint32_t ring_lds;        // LDS byte address of the ring
   const float* lbias;       // LDS copy of bias16
   const float4* lbasis;     // LDS copy of the Fourier basis, one float4 per frequency
+  const float4* lspheres;   // LDS copy of the SphereSDF table (k_march16) or nullptr
   const void* sbase;        // FP16 weight stream (buffer base and range)
   int sbytes;
   int slot;                 // ring slot of the current chunk

@@ -259,6 +259,9 @@ struct MarchArgs {
   // r / group_rays (one random.random() draw per tile, sdfs.py:236); nullptr = `step` for all
   const double* groups = nullptr;
   int64_t group_rays = 1;
+  // FP16 ring march: byte offset of an LDS copy of the SphereSDF table (0 = read it from the
+  // constant cache); set by ring_march when the table fits beside the weight ring
+  int lds_spheres = 0;
 };
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
@@ -422,9 +425,23 @@ template <int NB, int NE, int WV, bool FOLD>
 struct RingPol16 {
   static constexpr int RPW = 32, WAVES = WV;
   using Eng = ring::Engine<NB, NE, WV>;
-  __device__ __forceinline__ static void init(Eng& E, const SdfDev&, const MlpDev& m, char* lds) { E.init(m, lds); }
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds,
+                                              const MarchArgs& a) {
+    E.init(m, lds);
+    E.lspheres = nullptr;
+    if (s.kind == 2 && a.lds_spheres > 0) {
+      float4* ls = reinterpret_cast<float4*>(lds + a.lds_spheres);
+      for (int i = threadIdx.x; i < s.n_spheres * 4; i += blockDim.x)
+        ls[i] = reinterpret_cast<const float4*>(s.spheres)[i];
+      __syncthreads();
+      E.lspheres = ls;
+    }
+  }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
-    const float d = (s.kind == 2) ? spheres_value<true>(s, x, y, z) : 0.f;
+    float d = 0.f;
+    if (s.kind == 2)
+      d = E.lspheres ? ring::spheres_value_halves(s, E.lspheres, E.lane, x, y, z)
+                     : spheres_value<true>(s, x, y, z);
     return d + ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, x, y, z);
   }
   __device__ __forceinline__ static void finish(Eng&) {}
@@ -433,7 +450,8 @@ template <int KH, int KE, int WV, int ACT>
 struct RingPol32 {
   static constexpr int RPW = 16, WAVES = WV;
   using Eng = ring32::Engine<KH, KE, WV>;
-  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds) {
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds,
+                                              const MarchArgs&) {
     E.init(m, s, lds, 2 * Eng::QE);
   }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
@@ -453,7 +471,8 @@ template <int KH, int KQ, int WV, int ACT>
 struct RingPol3 {
   static constexpr int RPW = 16, WAVES = WV;
   using Eng = ring3::Engine<KH, KQ, WV>;
-  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds) {
+  __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds,
+                                              const MarchArgs&) {
     E.init(m, s, lds, 4 * KQ, 4 * KQ);  // chunks 0 and 1: the init layer's
   }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
@@ -488,7 +507,7 @@ __device__ __forceinline__ void march_body(
   const int64_t J = mode == 0 ? (scan ? R + (R - T) + T * kScanSegs : R) : R;
   const uint32_t lt = (1u << r) - 1u;
   typename Pol::Eng E;
-  Pol::init(E, s, m, smem_c);
+  Pol::init(E, s, m, smem_c, a);
   // lane state: kind -1 = wants a job, -2 = list exhausted, 0 march, 1 scan segment, 2 sdf(best)
   int kind = -1;
   int64_t ray = 0;
@@ -689,7 +708,7 @@ __global__ void __launch_bounds__(64 * Pol::WAVES, 1) k_normal_r(
   const int64_t per_block = 4 * WV;
   if ((int64_t)blockIdx.x * per_block >= total) return;  // whole block, before the ring starts
   typename Pol::Eng E;
-  Pol::init(E, s, m, smem_c);
+  Pol::init(E, s, m, smem_c, MarchArgs{});
   const int lane = E.lane, comp = lane & 3;
   for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < total; b0 += (int64_t)gridDim.x * per_block) {
     const int64_t i = b0 + 4 * E.wv + ((lane & 15) >> 2);

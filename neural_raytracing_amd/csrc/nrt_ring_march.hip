@@ -17,8 +17,18 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
   const bool best32 = scan && option(OPT_SCAN_BEST32) != 0 && ring32_supported(s);
   if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   int rc = ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
+    // the SphereSDF table goes into LDS behind the ring when it fits and costs no resident block
+    // (spheres_value_halves: the two lanes of a ray split the spheres; colocate's 64 spheres:
+    // k_march16 51.3 -> 43.8 ms); a table of a few spheres stays on scalar loads
+    constexpr int kLdsSpheresMin = 8;
+    const size_t base = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
+    const size_t ring_lds = (base + 15) & ~size_t(15);
+    const size_t sph = ring32_sphere_bytes(s);
+    MarchArgs a = ma;
+    a.lds_spheres = (sph > 0 && s->host_dev.n_spheres >= kLdsSpheresMin && ring_lds + sph <= (size_t)kLdsBytes &&
+                     kLdsBytes / (ring_lds + sph) == kLdsBytes / base) ? (int)ring_lds : 0;
+    const size_t lds = a.lds_spheres ? ring_lds + sph : base;
     auto launch = [&](auto kern, const char* name) -> int {
-      const size_t lds = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
       if (int rc = set_lds(kern, lds)) return rc;
       int per_cu = 0;
       NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kRingWaves, lds));
@@ -29,7 +39,7 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, ma, t, hit, p, n, raw_n, thr, keys);
+          s->host_dev, s->mlp->host_dev, rays, P, a, t, hit, p, n, raw_n, thr, keys);
       return check_launch(name);
     };
     if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
