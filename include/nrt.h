@@ -176,6 +176,31 @@ int nrt_sdf_occlusion(const nrt_sdf* sdf, const float* rays, int64_t P, const fl
                       int32_t max_steps, float epsilon, uint8_t* visible, int precision,
                       void* stream);
 
+/* SDF callables the library cannot pack (SDF(sdf=f) with f any function of p: a warp or a
+ * displacement around a packed SDF, edit_dtu.py:86-100).  The caller evaluates f on the query
+ * points q[P,3] between steps; these do the rest of sdfs.py:111-181, elementwise in ray order.
+ *
+ * March (sdfs.py:118-133): first call dists = NULL (t = 0, remaining = 1, hit = 0); every later
+ * call consumes dists = f(q) of the step just taken (hit |= remaining & d <= eps, remaining &=
+ * !hit-now, t += d where still remaining).  prep = 1 then applies the next step's remaining &=
+ * t < max_t; every call writes q = r_o + t r_d (after the last step: the march's p).
+ * Replaces the loop at sdfs.py:118-131 (reference: torch ops around self.sdf). */
+int nrt_march_callable_step(const float* rays, int64_t P, const float* dists, float epsilon,
+                            float max_t, int prep, float* t, uint8_t* remaining, uint8_t* hit,
+                            float* q, void* stream);
+/* Coarse scan (SDF.throughput, sdfs.py:232-249): sd = f(scan point j) for j = 0 .. 128 (point 0
+ * = r_o); keeps the first strict minimum (curr_min, idx).  prep = 1 writes scan point j + 1
+ * (r_o + (float)(step (j+1)) r_d), prep = 2 writes best_pos = r_o + ((float)idx (float)step) r_d. */
+int nrt_scan_callable_step(const float* rays, int64_t P, const float* sd, int32_t j, double step,
+                           int prep, float* curr_min, int32_t* idx, float* q, void* stream);
+/* Shadow march (SDF.intersect_test, sdfs.py:162-181): phase 0 sets depth = t0 (= 1e2 eps,
+ * rounded to f32 by the caller), remaining = 1 and q; phase 1 consumes dists (depth += d where
+ * remaining, then remaining &= d >= eps) and writes q; phase 2 consumes the last step and writes
+ * visible = depth >= max_t[i] | remaining. */
+int nrt_occlusion_callable_step(const float* rays, int64_t P, const float* dists, float epsilon,
+                                float t0, const float* max_t, int phase, float* depth,
+                                uint8_t* remaining, float* q, uint8_t* visible, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Lights (lights/lights.py) and BSDFs (bsdf/bsdfs.py)
  * ------------------------------------------------------------------------------------- */

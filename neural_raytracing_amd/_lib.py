@@ -76,6 +76,9 @@ _SIGNATURES = {
     "nrt_sdf_intersect": (_I32, [_P, _P, _I64, ctypes.POINTER(MarchParams), _P, _P, _P, _P, _P,
                                  _P, _P, _P, _P, _P, _P]),
     "nrt_sdf_occlusion": (_I32, [_P, _P, _I64, _P, _I32, _F, _P, _I32, _P]),
+    "nrt_march_callable_step": (_I32, [_P, _I64, _P, _F, _F, _I32, _P, _P, _P, _P, _P]),
+    "nrt_scan_callable_step": (_I32, [_P, _I64, _P, _I32, ctypes.c_double, _I32, _P, _P, _P, _P]),
+    "nrt_occlusion_callable_step": (_I32, [_P, _I64, _P, _F, _F, _P, _I32, _P, _P, _P, _P, _P]),
     "nrt_light_create_field": (_I32, [_P, _P, ctypes.POINTER(_P)]),
     "nrt_light_create_point": (_I32, [_P, _P, _F, _F, _F, _F, ctypes.POINTER(_P)]),
     "nrt_light_destroy": (_I32, [_P]),

@@ -213,7 +213,13 @@ class Direct(Integrator):
         if self.emitter_samples != 1 or self.bsdf_samples != 0:
             raise _lib.NrtError("Direct on the HIP path supports emitter_samples=1, bsdf_samples=0")
         it, active = shapes.intersect(rays, primary=self.training)
-        if getattr(it, "_nrt_train", False) or needs_grad(bsdf, lights, kwargs.get("w_isect")):
+        from ..shapes.sdfs import is_hip_sdf
+        callable_shadow = bool(shadow) and not is_hip_sdf(getattr(shapes, "sdf", None))
+        if getattr(it, "_nrt_train", False) or needs_grad(bsdf, lights, kwargs.get("w_isect")) \
+                or callable_shadow:
+            # (an SDF callable with shadow rays: the shading kernel cannot march the callable, so
+            # the composed path shades -- HIP MLPs, the shadow march by intersect_test's
+            # nrt_occlusion_callable_step)
             # training: shading with autograd through the HIP MLPs
             return direct_sample(it, active, bsdf, lights, rays.shape[:-1], rays.device, shapes,
                                  kwargs.get("w_isect", False)), active, it

@@ -154,6 +154,13 @@ class _MlpFn(torch.autograd.Function):
     def backward(ctx, dy):
         import ctypes
         _check_versions(ctx)
+        if torch.is_grad_enabled():
+            # create_graph=True through SkipConnMLP.forward (e.g. autograd normals of an SDF
+            # callable that wraps the MLP, under training): the HIP backward has no graph, and a
+            # silently non-differentiable gradient would drop the eikonal term's contribution
+            raise _lib.NrtError("second derivatives through SkipConnMLP.forward are not on the HIP "
+                                "path (the SDF normal of a packed SDF uses nrt_mlp_grad_backward; "
+                                "an SDF callable wrapping an MLP trains without create_graph)")
         x, lat = ctx.saved_tensors
         lat = lat if ctx.has_lat else None
         mlp = ctx.mlp

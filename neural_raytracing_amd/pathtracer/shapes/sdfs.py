@@ -1,6 +1,8 @@
 """SDF shapes (shapes/sdfs.py): the sphere-tracing march, the 128-step coarse scan and the
 normals run in ``nrt_sdf_intersect``; ``SphereSDF`` / ``SkipConnMLP`` SDFs evaluate in
-``nrt_sdf_eval``.  SDF callables the library does not recognise raise ``NrtError``."""
+``nrt_sdf_eval``.  Any other SDF callable (a warp or displacement around a packed SDF,
+edit_dtu.py:86-100) is evaluated by the caller between the HIP march / scan / shadow steps
+(``nrt_*_callable_step``), with autograd normals through the callable as sdfs.py:184-197."""
 import ctypes
 import random
 
@@ -39,6 +41,10 @@ class SphereSDF(nn.Module):
         return torch.einsum("ijk,ibk->ibj", tfs, p.expand(tfs.shape[0], -1, -1))
 
     def forward(self, p):
+        if torch.is_grad_enabled() and (p.requires_grad or needs_grad(self)):
+            # inside an SDF callable (a warp) under autograd: the normals of the callable march
+            # differentiate through it (sphere part in torch, shift MLP on the HIP backward)
+            return sdf_value(self, p)
         return sdf_eval(self, p)
 
 
@@ -132,6 +138,17 @@ def march_handle(sdf):
     return train_sdf_handle(sdf) if needs_grad(sdf) else sdf_handle(sdf)
 
 
+def is_hip_sdf(sdf):
+    """True for the SDFs nrt_sdf packs (SPHERE_SDF, SphereSDF, SkipConnMLP and their TorchScript
+    modules); anything else is a callable the march evaluates between its HIP steps."""
+    from ..script_modules import resolve
+    try:
+        s = resolve(sdf)
+    except _lib.NrtError:
+        return False
+    return s is SPHERE_SDF or isinstance(s, SkipConnMLP) or _is_sphere_sdf(s)
+
+
 def _looks_like_sphere_sdf(m):
     return all(hasattr(m, a) for a in ("centers", "radii", "tfs", "shift"))
 
@@ -221,6 +238,8 @@ class SDF:
     def intersect(self, rays, max_t=10, active=True, primary: bool = True):
         """sdfs.py:111-160 on the HIP path.  ``primary`` draws ``random.random()`` for the
         coarse-scan jitter exactly like SDF.throughput (sdfs.py:236)."""
+        if not is_hip_sdf(self.sdf):
+            return self._intersect_callable(rays, max_t, primary)
         dev = rays.device
         lead = rays.shape[:-1]
         flat = rays.reshape(-1, 6).float().contiguous()
@@ -301,22 +320,148 @@ class SDF:
         return si
 
     def intersect_test(self, rays, max_t=10, active=True):
-        """sdfs.py:162-181 via nrt_sdf_occlusion."""
+        """sdfs.py:162-181 via nrt_sdf_occlusion (a callable SDF: nrt_occlusion_callable_step)."""
         lead = rays.shape[:-1]
         flat = rays.reshape(-1, 6).float().contiguous()
         P = flat.shape[0]
         mt = torch.as_tensor(max_t, dtype=torch.float32, device=rays.device)
         mt = mt.expand(lead + (1,)).reshape(P).contiguous() if mt.dim() > 0 else mt.expand(P).contiguous()
         vis = torch.empty(P, dtype=torch.uint8, device=rays.device)
+        if not is_hip_sdf(self.sdf):
+            self._occlusion_callable(flat, lead, mt, vis)
+            return vis.bool().reshape(lead)
         _lib.call("nrt_sdf_occlusion", march_handle(self.sdf), _lib.ptr(flat), P, _lib.ptr(mt),
                   int(self.max_steps), float(self.epsilon), _lib.ptr(vis), _lib.precision_code(),
                   _lib.stream())
         return vis.bool().reshape(lead)
 
+    # ---- SDF callables: the callable between HIP steps ------------------------------------------
+
+    def _eval_callable(self, q, lead):
+        """self.sdf on the query points in the rays' shape (what the reference passes), flattened
+        to one f32 distance per ray."""
+        P = q.shape[0]
+        d = self.sdf(q.reshape(lead + (3,)))
+        if not torch.is_tensor(d) or d.numel() != P:
+            raise _lib.NrtError(f"SDF callable returned {tuple(getattr(d, 'shape', ()))} for "
+                                f"{tuple(lead)} points (one distance per point expected)")
+        return d.detach().reshape(P).float().contiguous()
+
+    def _intersect_callable(self, rays, max_t, primary):
+        """sdfs.py:111-160 for an SDF callable: max_steps evaluations of the callable on every
+        ray (as the reference) with the depth / remaining / hit update and the next points in
+        nrt_march_callable_step; the 129-point coarse scan with nrt_scan_callable_step; then
+        throughput = -1000 sdf(best_pos) and the autograd normals through the callable."""
+        dev = rays.device
+        lead = rays.shape[:-1]
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        t = torch.empty(P, device=dev)
+        rem = torch.empty(P, dtype=torch.uint8, device=dev)
+        hit = torch.empty(P, dtype=torch.uint8, device=dev)
+        q = torch.empty(P, 3, device=dev)
+        steps, eps = int(self.max_steps), float(self.epsilon)
+
+        def march(d, prep):
+            _lib.call("nrt_march_callable_step", _lib.ptr(flat), P, _lib.ptr(d), eps, float(max_t),
+                      prep, _lib.ptr(t), _lib.ptr(rem), _lib.ptr(hit), _lib.ptr(q), _lib.stream())
+        with torch.no_grad():
+            march(None, 1 if steps > 0 else 0)
+            for i in range(steps):
+                march(self._eval_callable(q, lead), 1 if i + 1 < steps else 0)
+        p0 = q  # r_o + depth r_d (sdfs.py:133)
+        throughput = 0
+        if primary:
+            dist = getattr(self, "dist", 2.2)
+            step = (dist + random.random() * (2 / 128)) / 128
+            best = flat[:, :3].contiguous()
+            cmin = torch.empty(P, device=dev)
+            idx = torch.empty(P, dtype=torch.int32, device=dev)
+            with torch.no_grad():
+                for j in range(129):
+                    sd = self._eval_callable(best, lead)
+                    _lib.call("nrt_scan_callable_step", _lib.ptr(flat), P, _lib.ptr(sd), j, step,
+                              1 if j < 128 else 2, _lib.ptr(cmin), _lib.ptr(idx), _lib.ptr(best),
+                              _lib.stream())
+            # sdf(best_pos) outside no_grad (sdfs.py:249): differentiable through the callable
+            throughput = -1000 * self.sdf(best.reshape(lead + (3,)))
+        hit_b = hit.bool()
+        n = torch.zeros(P, 3, device=dev)
+        p = p0.clone()
+        raw = None
+        graph = torch.is_grad_enabled()  # under no_grad the render keeps no graph of the normals
+        if bool(hit_b.any()):
+            raw = self._callable_normals(p0[hit_b], create_graph=graph)
+            nh = F.normalize(raw, eps=1e-6, dim=-1)
+            n = n.index_put((hit_b,), nh)
+            p = p.index_put((hit_b,), p0[hit_b] + nh * self.epsilon * 5)
+        si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead).squeeze(), obj=self,
+                            throughput=throughput)
+        si.n = n.reshape(lead + (3,))
+        if raw is not None and raw.requires_grad:
+            # normals with a graph: frame and wi differentiable as in _differentiable
+            si.frame = coordinate_system(n).reshape(lead + (3, 3))
+            si.wi = si.to_local(-flat[:, 3:].reshape(lead + (3,)))
+        else:
+            frame = torch.empty(P, 9, device=dev)
+            wi = torch.empty(P, 3, device=dev)
+            _lib.call("nrt_frames", _lib.ptr(flat), _lib.ptr(n.contiguous()), P, _lib.ptr(frame),
+                      _lib.ptr(wi), _lib.stream())
+            si.frame = frame.reshape(lead + (3, 3))
+            si.wi = wi.reshape(lead + (3,))
+        hit_idx = torch.nonzero(hit_b).reshape(-1).to(torch.int32)
+        hit_count = torch.tensor([hit_idx.numel()], dtype=torch.int32, device=dev)
+        si._nrt_hits = (hit_idx if hit_idx.numel() else torch.zeros(1, dtype=torch.int32, device=dev),
+                        hit_count, flat)
+        raw_full = torch.zeros(P, 3, device=dev)
+        if raw is not None:
+            raw_full[hit_b] = raw.detach()
+        si._nrt_raw = raw_full
+        si._nrt_hit_mask = hit_b.reshape(lead)
+        if raw is not None and raw.requires_grad:
+            si._nrt_train = True  # raw_normals keeps its graph (the eikonal term)
+            si._nrt_raw_train = raw
+        return si, hit_b.reshape(lead)
+
+    def _callable_normals(self, p, create_graph=True):
+        """SDF.autograd_diff (sdfs.py:184-197) through the callable: create_graph, so the normal
+        carries gradients for whatever parameters the callable closes over (a render under
+        no_grad takes the same values without the graph)."""
+        with torch.enable_grad():
+            q = p.detach().requires_grad_(True)
+            out = self.sdf(q)
+            (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=create_graph)
+        return g if create_graph else g.detach()
+
+    def _occlusion_callable(self, flat, lead, mt, vis):
+        P = flat.shape[0]
+        dev = flat.device
+        depth = torch.empty(P, device=dev)
+        rem = torch.empty(P, dtype=torch.uint8, device=dev)
+        q = torch.empty(P, 3, device=dev)
+        steps, eps = int(self.max_steps), float(self.epsilon)
+        t0 = 1e2 * self.epsilon  # zeros(...) + 1e2 * epsilon (sdfs.py:165-166)
+
+        def step(d, phase):
+            _lib.call("nrt_occlusion_callable_step", _lib.ptr(flat), P, _lib.ptr(d), eps, t0,
+                      _lib.ptr(mt), phase, _lib.ptr(depth), _lib.ptr(rem), _lib.ptr(q),
+                      _lib.ptr(vis), _lib.stream())
+        with torch.no_grad():
+            step(None, 0)
+            if steps == 0:
+                # no step taken: visible = depth >= max_t | remaining (all remaining)
+                vis.fill_(1)
+                return
+            for i in range(steps):
+                step(self._eval_callable(q, lead), 2 if i + 1 == steps else 1)
+
     def autograd_diff(self, p):
         """Normal direction d sdf / dp (sdfs.py:184-197) from the f32 backward kernel; with
         autograd on and trainable SDF parameters the result is differentiable
-        (create_graph=True, nrt_mlp_grad_backward)."""
+        (create_graph=True, nrt_mlp_grad_backward).  A callable SDF: autograd through it."""
+        if not is_hip_sdf(self.sdf):
+            return self._callable_normals(p.reshape(-1, 3),
+                                          create_graph=torch.is_grad_enabled()).reshape(p.shape)
         if needs_grad(self.sdf):
             return sdf_gradient(self.sdf, p)
         flat = p.reshape(-1, 3).float().contiguous()
