@@ -404,9 +404,11 @@ __device__ __forceinline__ void write_enc_slab(const MlpDev& m, const EncIn& e, 
 // One FP32 GEMM over `nks` k-steps of the slab starting at column kcol; accumulates into acc.
 // act_in >= 0 applies the activation to B on the fly (skip-concat of the encoding).
 // The A fragments are read through a global-address-space pointer (generic "flat" loads also
-// count in lgkmcnt, so the slab's ds_read waits drained them) and prefetched one k-step ahead:
-// the wait before a k-step's MFMAs covers only the previous step's loads.
-template <int NB>
+// count in lgkmcnt, so the slab's ds_read waits drained them) and prefetched PF - 1 k-steps
+// ahead through PF rotating buffers: a k-step's wait covers only loads issued PF - 1 steps
+// earlier.  PF = 2 is the ping-pong of the occupancy-rich kernels; the training kernels run one
+// wave per SIMD and hide the L2 latency with PF = 4.
+template <int NB, int PF = 2>
 __device__ __forceinline__ void gemm32(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
                                        int rb0, int nks, const float* X, int RS, int kcol,
                                        int act_in) {
@@ -421,34 +423,38 @@ __device__ __forceinline__ void gemm32(f16v (&acc)[NB], const float* __restrict_
   int off[NB];
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) off[ib] = (rb0 + ib < nrb ? ib : nrb - 1 - rb0) * 64;
-  // ping-pong fragment buffers (no register copies, which would wait for the prefetch)
-  float a0[NB], a1[NB];
+  // rotating fragment buffers (no register copies, which would wait for the prefetch)
+  float a[PF][NB];
 #pragma unroll
-  for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[off[ib]];
-  auto step = [&](const float (&a)[NB], int s) {
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)(p < nks ? p : nks - 1) * stride + off[ib]];
+  auto step = [&](const float (&av)[NB], int s) {
     float b = xr[2 * s];
     if (act_in >= 0) b = act_fwd<false>(b, act_in);
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib)
-      if (rb0 + ib < nrb) acc[ib] = mfma32(a[ib], b, acc[ib]);
+      if (rb0 + ib < nrb) acc[ib] = mfma32(av[ib], b, acc[ib]);
   };
   int s = 0;
-  for (; s + 1 < nks; s += 2) {
+  for (; s + PF <= nks; s += PF) {
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) a1[ib] = Ag[(size_t)(s + 1) * stride + off[ib]];
-    step(a0, s);
-    const int s2 = s + 2 < nks ? s + 2 : nks - 1;
+    for (int p = 0; p < PF; ++p) {
+      step(a[p], s + p);
+      const int sn = s + p + PF < nks ? s + p + PF : nks - 1;
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[(size_t)s2 * stride + off[ib]];
-    step(a1, s + 1);
+      for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)sn * stride + off[ib]];
+    }
   }
-  if (s < nks) step(a0, s);
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (s + p < nks) step(a[p], s + p);
 }
 
 // gemm32 with B from a per-wave global tile T[slot][32 rows] (coalesced: a k-step reads two
-// 128-byte rows) instead of the LDS slab; B is prefetched one k-step ahead like the A fragments.
+// 128-byte rows) instead of the LDS slab; B is prefetched with the A fragments.
 // Used by k_mlp_backward32 to keep the encoding out of LDS.
-template <int NB>
+template <int NB, int PF = 2>
 __device__ __forceinline__ void gemm32_tile(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
                                             int rb0, int nks, const float* T, int act_in) {
   using gptr = const __attribute__((address_space(1))) float*;
@@ -461,29 +467,34 @@ __device__ __forceinline__ void gemm32_tile(f16v (&acc)[NB], const float* __rest
   int off[NB];
 #pragma unroll
   for (int ib = 0; ib < NB; ++ib) off[ib] = (rb0 + ib < nrb ? ib : nrb - 1 - rb0) * 64;
-  float a0[NB], a1[NB], b0, b1;
+  float a[PF][NB], bb[PF];
 #pragma unroll
-  for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[off[ib]];
-  b0 = Bg[0];
-  auto step = [&](const float (&a)[NB], float b) {
+  for (int p = 0; p < PF; ++p) {
+    const int sp = p < nks ? p : nks - 1;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)sp * stride + off[ib]];
+    bb[p] = Bg[sp * 64];
+  }
+  auto step = [&](const float (&av)[NB], float b) {
     if (act_in >= 0) b = act_fwd<false>(b, act_in);
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib)
-      if (rb0 + ib < nrb) acc[ib] = mfma32(a[ib], b, acc[ib]);
+      if (rb0 + ib < nrb) acc[ib] = mfma32(av[ib], b, acc[ib]);
   };
   int s = 0;
-  for (; s + 1 < nks; s += 2) {
+  for (; s + PF <= nks; s += PF) {
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) a1[ib] = Ag[(size_t)(s + 1) * stride + off[ib]];
-    b1 = Bg[(s + 1) * 64];
-    step(a0, b0);
-    const int s2 = s + 2 < nks ? s + 2 : nks - 1;
+    for (int p = 0; p < PF; ++p) {
+      step(a[p], bb[p]);
+      const int sn = s + p + PF < nks ? s + p + PF : nks - 1;
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) a0[ib] = Ag[(size_t)s2 * stride + off[ib]];
-    b0 = Bg[s2 * 64];
-    step(a1, b1);
+      for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)sn * stride + off[ib]];
+      bb[p] = Bg[sn * 64];
+    }
   }
-  if (s < nks) step(a0, b0);
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (s + p < nks) step(a[p], bb[p]);
 }
 
 template <int NB>
