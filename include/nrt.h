@@ -104,6 +104,18 @@ int nrt_mlp_backward(const nrt_mlp* mlp, const float* x, const float* latent, in
                      const float* dy, float* dx, float* dlatent, float* const* dweights,
                      float* const* dbiases, void* workspace, void* stream);
 
+/* nrt_mlp_backward for n MLPs of one shape (no latent) on the same input x [M, in] -- the
+ * NeuralBSDFs of a ComposeSpatialVarying mixture, which all read param_rusin(wi, wo)
+ * (bsdfs.py:634-637) -- in one backward launch and one weight-gradient launch.  dy[i] [M, out],
+ * dx[i] [M, in] (the array or entries may be NULL); dweights / dbiases are flat host arrays of
+ * n x (num_layers + 2) device pointers, MLP-major.  Per MLP the same results as nrt_mlp_backward
+ * up to the split-K summation order of the weight gradients.
+ * workspace: nrt_mlp_backward_multi_workspace_bytes(mlps, n, M) bytes. */
+size_t nrt_mlp_backward_multi_workspace_bytes(const nrt_mlp* const* mlps, int n, int64_t M);
+int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                           const float* const* dy, float* const* dx, float* const* dweights,
+                           float* const* dbiases, void* workspace, void* stream);
+
 /* Double backward of the input gradient (SDF.autograd_diff with
  * create_graph=True, sdfs.py:184-197, differentiated again by loss.backward()): for
  * g(x) = d(sum_o y_o)/dx [M, in] (torch.autograd.grad with grad_outputs = ones) and v [M, in] =

@@ -102,6 +102,8 @@ _SIGNATURES = {
     "nrt_plain_nerf_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _I64, _P, _P, _P, _I32, _P]),
     "nrt_mlp_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_mlp_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "nrt_mlp_backward_multi_workspace_bytes": (ctypes.c_size_t, [_P, _I32, _I64]),
+    "nrt_mlp_backward_multi": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "nrt_mlp_grad_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_mlp_grad_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "nrt_frames": (_I32, [_P, _P, _I64, _P, _P, _P]),

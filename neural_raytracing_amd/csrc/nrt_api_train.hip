@@ -33,7 +33,7 @@ __device__ __forceinline__ int enc_col(const MlpDev& m, int s) {
 // at two waves (the 16x256 F=128 spatial-weights MLP: 68 KB a wave -> 33 KB).  Otherwise the slab
 // row is [hidden | encoding], and the encoding slots take the encoding gradient in the backward.
 template <int NB, bool TILE>
-__global__ void __launch_bounds__(256) k_mlp_backward32(
+__device__ __forceinline__ void mlp_backward32(
     const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
     int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
     float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
@@ -100,18 +100,26 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
       }
     }
     wave_lds_fence();
+    // registers 4g..4g+3 of a row block are 4 consecutive columns of the lane's row: one 16-byte
+    // store each for Z and A (H is a multiple of 32, the arrays 256-byte aligned)
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
-      for (int reg = 0; reg < 16; ++reg) {
-        const int k = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-        const float z = acc[ib][reg];
-        const float a = act_fwd<false>(z, m.act);
-        if (valid) {
-          Zg[((int64_t)l * M + row) * H + k] = z;
-          Ag[((int64_t)l * M + row) * H + k] = a;
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = 32 * ib + 8 * g + 4 * h;
+        float4 zv, av;
+        float* zp = &zv.x;
+        float* ap = &av.x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          zp[j] = acc[ib][4 * g + j];
+          ap[j] = act_fwd<false>(zp[j], m.act);
+          rowp[k0 + j] = ap[j];
         }
-        rowp[k] = a;
+        if (valid) {
+          *reinterpret_cast<float4*>(Zg + ((int64_t)l * M + row) * H + k0) = zv;
+          *reinterpret_cast<float4*>(Ag + ((int64_t)l * M + row) * H + k0) = av;
+        }
       }
     wave_lds_fence();
   }
@@ -139,7 +147,9 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
   wave_lds_fence();
   for (int l = L; l >= 0; --l) {
     if (valid)
-      for (int k = h; k < H; k += 2) dZg[((int64_t)l * M + row) * H + k] = rowp[k];
+      for (int k = 4 * h; k < H; k += 8)
+        *reinterpret_cast<float4*>(dZg + ((int64_t)l * M + row) * H + k) =
+            make_float4(rowp[k], rowp[k + 1], rowp[k + 2], rowp[k + 3]);
     const float* At = m.wt32[l];
     const int nrb = m.nbt[l];
     const bool has_hidden_in = (l != 0);
@@ -179,9 +189,12 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int pos = 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          rowp[pos] = acc[ib][reg] * act_bwd(Zg[((int64_t)(l - 1) * M + rr) * H + pos], m.act);
+        for (int g = 0; g < 4; ++g) {
+          const int k0 = 32 * ib + 8 * g + 4 * h;
+          const float4 zv = *reinterpret_cast<const float4*>(Zg + ((int64_t)(l - 1) * M + rr) * H + k0);
+          const float* zp = &zv.x;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rowp[k0 + j] = acc[ib][4 * g + j] * act_bwd(zp[j], m.act);
         }
       wave_lds_fence();
     }
@@ -207,6 +220,33 @@ __global__ void __launch_bounds__(256) k_mlp_backward32(
   }
   if (dLat && valid)
     for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[es * (2 * F + in + j)];
+}
+
+template <int NB, bool TILE>
+__global__ void __launch_bounds__(256) k_mlp_backward32(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
+    float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
+    float* __restrict__ Eact, float* __restrict__ dZg, float* __restrict__ Et,
+    float* __restrict__ Gt, int RS, int per_wave) {
+  mlp_backward32<NB, TILE>(mp, x, lat, M, dY, dX, dLat, Zg, Ag, Eraw, Eact, dZg, Et, Gt, RS, per_wave);
+}
+
+// n same-shape MLPs on one input (the NeuralBSDFs of a spatially varying mixture all read the
+// same Rusinkiewicz features): one launch, blockIdx.y = MLP.  Each MLP alone is 1,200 32-row waves
+// on 1,024 SIMDs for a 38,400-ray training batch; together they fill the machine.
+struct BwdJob {
+  const MlpDev* mp;
+  const float* dY;
+  float *dX, *Z, *A, *Eraw, *Eact, *dZ, *Et, *Gt;
+};
+
+template <int NB, bool TILE>
+__global__ void __launch_bounds__(256) k_mlp_backward32_multi(
+    const BwdJob* __restrict__ jobs, const float* __restrict__ x, int64_t M, int RS, int per_wave) {
+  const BwdJob j = jobs[blockIdx.y];
+  mlp_backward32<NB, TILE>(j.mp, x, nullptr, M, j.dY, j.dX, nullptr, j.Z, j.A, j.Eraw, j.Eact,
+                           j.dZ, j.Et, j.Gt, RS, per_wave);
 }
 
 // second derivative of act at pre-activation x (torch double-backward formulas:
@@ -568,6 +608,7 @@ int batch_slices(int64_t total_tiles, int64_t M) {
 
 struct WgradBatch {
   std::vector<WgradJob> jobs;
+  int max_jobs = kMaxWgradJobs;  // the device table's capacity
   void weight(const float* dZ, int R, const float* In, int C, int64_t M, float* dW, int ldw, int c0) {
     WgradJob j{};
     j.dZ = dZ; j.In = In; j.dW = dW; j.M = M; j.R = R; j.C = C; j.ldi = C; j.ldw = ldw; j.c0 = c0;
@@ -604,7 +645,7 @@ struct WgradBatch {
   // table: kMaxWgradJobs * sizeof(WgradJob) bytes of device memory; part: the plan's floats
   int run(void* table, float* part, hipStream_t st) {
     if (jobs.empty()) return NRT_OK;
-    if ((int)jobs.size() > kMaxWgradJobs) { set_error("weight gradients: too many jobs"); return NRT_EINVAL; }
+    if ((int)jobs.size() > max_jobs) { set_error("weight gradients: too many jobs"); return NRT_EINVAL; }
     int S = 1;
     plan(S);
     int64_t blocks = 0, total = 0;
@@ -652,6 +693,46 @@ size_t batch_part_floats(const MlpDev& d, int64_t M, bool grad_bwd) {
   int S = 1;
   return b.plan(S);
 }
+// k_mlp_backward32's LDS plan: slab row [hidden | encoding] (H + ke floats), or [hidden] with the
+// encoding in global tiles when that at least doubles the waves per CU (TILE)
+LdsPlan backward_plan(const MlpDev& d, bool& tile) {
+  auto plan = [&](bool t) {
+    LdsPlan p;
+    p.RS = (std::max(d.hidden, 32) + (t ? 0 : d.ke)) | 1;
+    p.per_wave = wave_lds_floats(p.RS, 1, false);
+    p.waves = std::max(1, std::min(4, kLdsBytes / (p.per_wave * 4)));
+    p.bytes = (size_t)p.waves * p.per_wave * 4;
+    spread_waves(p);
+    return p;
+  };
+  const LdsPlan slab = plan(false), tiled = plan(true);
+  const auto per_cu = [](const LdsPlan& p) { return std::min(8, kLdsBytes / (p.per_wave * 4)); };
+  tile = per_cu(tiled) >= 2 * per_cu(slab);
+  return tile ? tiled : slab;
+}
+
+// one MLP's activations / gradients region of the multi-MLP workspace (carve's first seven arrays)
+size_t region_bytes(const MlpDev& d, int64_t M) {
+  const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
+  const size_t enc = (size_t)M * d.dp * 4;
+  return 3 * a256(lay) + 2 * a256(enc) + 2 * a256(enc_tile_bytes(d, M));
+}
+
+bool same_shape(const nrt_mlp* a, const nrt_mlp* b) {
+  const MlpDev &x = a->host_dev, &y = b->host_dev;
+  return x.hidden == y.hidden && x.n_hidden == y.n_hidden && x.ke == y.ke && x.dp == y.dp &&
+         x.in_size == y.in_size && x.out == y.out && x.skip == y.skip && x.freqs == y.freqs &&
+         x.latent == y.latent && x.nb == y.nb && a->desc.activation == b->desc.activation;
+}
+
+// the combined weight-gradient batch of n same-shape MLPs (pointers filled by the caller's f)
+template <class F>
+void multi_jobs(const MlpDev& d, int n, int64_t M, WgradBatch& b, F&& f) {
+  b.max_jobs = n * kMaxWgradJobs;
+  for (int i = 0; i < n; ++i)
+    backward_jobs(d, false, [&](int l, int R, int kind, int C, int ldw, int c0) { f(i, l, R, kind, C, ldw, c0); });
+  (void)M;
+}
 }  // namespace
 
 
@@ -693,21 +774,8 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     return NRT_OK;
   }
   TrainWs w = carve(m, M, workspace);
-  // LDS slab row [hidden | encoding] (H + ke floats), or [hidden] with the encoding in global
-  // tiles when that at least doubles the waves per CU (k_mlp_backward32's TILE)
-  auto plan = [&](bool tile) {
-    LdsPlan p;
-    p.RS = (std::max(H, 32) + (tile ? 0 : d.ke)) | 1;
-    p.per_wave = wave_lds_floats(p.RS, 1, false);
-    p.waves = std::max(1, std::min(4, kLdsBytes / (p.per_wave * 4)));
-    p.bytes = (size_t)p.waves * p.per_wave * 4;
-    spread_waves(p);
-    return p;
-  };
-  const LdsPlan slab = plan(false), tiled = plan(true);
-  const auto per_cu = [](const LdsPlan& p) { return std::min(8, kLdsBytes / (p.per_wave * 4)); };
-  const bool tile = per_cu(tiled) >= 2 * per_cu(slab);
-  const LdsPlan lp = tile ? tiled : slab;
+  bool tile = false;
+  const LdsPlan lp = backward_plan(d, tile);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
@@ -744,6 +812,98 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     batch.weight(dZ, R, In, C, M, dweights[l], ldw, c0);
   });
   return batch.run(w.part, w.kpart, st);
+}
+
+size_t nrt_mlp_backward_multi_workspace_bytes(const nrt_mlp* const* mlps, int n, int64_t M) {
+  if (!mlps || n <= 0 || !mlps[0]) return 0;
+  M = std::max<int64_t>(M, 1);
+  const MlpDev& d = mlps[0]->host_dev;
+  WgradBatch b;
+  multi_jobs(d, n, M, b, [&](int, int, int R, int kind, int C, int, int) {
+    if (kind == 3) b.bias(nullptr, R, M, nullptr);
+    else b.weight(nullptr, R, nullptr, C, M, nullptr, 0, 0);
+  });
+  int S = 1;
+  const size_t part = b.plan(S);
+  return (size_t)n * region_bytes(d, M) + a256((size_t)n * sizeof(BwdJob)) +
+         a256((size_t)n * kWgradTableBytes) + a256(part * 4);
+}
+
+int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                           const float* const* dy, float* const* dx, float* const* dweights,
+                           float* const* dbiases, void* workspace, void* stream) {
+  if (!mlps || n <= 0 || M < 0 || !dy || (M > 0 && (!x || !workspace))) {
+    set_error("nrt_mlp_backward_multi: bad argument");
+    return NRT_EINVAL;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (!mlps[i] || !same_shape(mlps[0], mlps[i])) {
+      set_error("nrt_mlp_backward_multi: the MLPs must share one shape");
+      return NRT_EINVAL;
+    }
+  }
+  const MlpDev& d = mlps[0]->host_dev;
+  if (d.latent > 0) { set_error("nrt_mlp_backward_multi: latent MLPs are not supported"); return NRT_EINVAL; }
+  if (M > INT32_MAX) { set_error("nrt_mlp_backward_multi: at most 2^31-1 rows per call"); return NRT_EINVAL; }
+  const int L = d.n_hidden, H = d.hidden, NL = L + 2;
+  if (M == 0) {
+    for (int i = 0; i < n; ++i)
+      if (int rc = nrt_mlp_backward(mlps[i], x, nullptr, 0, dy[i], nullptr, nullptr,
+                                    dweights ? dweights + (size_t)i * NL : nullptr,
+                                    dbiases ? dbiases + (size_t)i * NL : nullptr, workspace, stream))
+        return rc;
+    return NRT_OK;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  char* p = (char*)workspace;
+  std::vector<TrainWs> ws(n);
+  std::vector<BwdJob> jobs(n);
+  for (int i = 0; i < n; ++i) {
+    ws[i] = carve(mlps[i], M, p);  // its first seven arrays; part / kpart are not used
+    p += region_bytes(d, M);
+    jobs[i] = BwdJob{mlps[i]->dev, dy[i], dx ? dx[i] : nullptr, ws[i].Z, ws[i].A, ws[i].Eraw,
+                     ws[i].Eact, ws[i].dZ, ws[i].Et, ws[i].Gt};
+  }
+  BwdJob* tj = (BwdJob*)p;
+  p += a256((size_t)n * sizeof(BwdJob));
+  void* table = p;
+  p += a256((size_t)n * kWgradTableBytes);
+  float* part = (float*)p;
+  NRT_HIP(hipMemcpyAsync(tj, jobs.data(), (size_t)n * sizeof(BwdJob), hipMemcpyHostToDevice, st));
+  bool tile = false;
+  const LdsPlan lp = backward_plan(d, tile);
+  const int waves = ceil_div64(M, 32);
+  dim3 grid(ceil_div64(waves, lp.waves), n), block(64 * lp.waves);
+  int rc = NRT_OK;
+  {
+    ProfScope prof("k_mlp_backward32", st);
+    NRT_NB_SWITCH(d.nb, {
+      if (tile) {
+        if (!(rc = set_lds(k_mlp_backward32_multi<NB, true>, lp.bytes)))
+          k_mlp_backward32_multi<NB, true><<<grid, block, lp.bytes, st>>>(tj, x, M, lp.RS, lp.per_wave);
+      } else {
+        if (!(rc = set_lds(k_mlp_backward32_multi<NB, false>, lp.bytes)))
+          k_mlp_backward32_multi<NB, false><<<grid, block, lp.bytes, st>>>(tj, x, M, lp.RS, lp.per_wave);
+      }
+    });
+    if (rc) return rc;
+    if ((rc = check_launch("k_mlp_backward32_multi"))) return rc;
+  }
+  if (!dweights && !dbiases) return NRT_OK;
+  const size_t lay = (size_t)M * H;
+  WgradBatch batch;
+  multi_jobs(d, n, M, batch, [&](int i, int l, int R, int kind, int C, int ldw, int c0) {
+    const TrainWs& w = ws[i];
+    const float* dZ = l == L + 1 ? dy[i] : w.dZ + (size_t)l * lay;
+    if (kind == 3) {
+      if (dbiases && dbiases[(size_t)i * NL + l]) batch.bias(dZ, R, M, dbiases[(size_t)i * NL + l]);
+      return;
+    }
+    if (!dweights || !dweights[(size_t)i * NL + l]) return;
+    const float* In = kind == 0 ? w.Eraw : kind == 1 ? w.A + (size_t)(l - 1) * lay : w.Eact;
+    batch.weight(dZ, R, In, C, M, dweights[(size_t)i * NL + l], ldw, c0);
+  });
+  return batch.run(table, part, st);
 }
 
 static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {

@@ -246,6 +246,7 @@ def bsdf_eval(bsdf, it, wo, active, feat=None):
     """eval_and_pdf of the supported BSDFs (bsdfs.py:108-118, 364-388, 515-536, 634-637).
     `feat`: param_rusin2(it.wi, wo) when the caller already has it."""
     from .bsdf.bsdfs import ComposeSpatialVarying, Conductor, Diffuse, NeuralBSDF, identity_div_pi
+    from .neural_blocks import mlp_multi, same_shape
     if isinstance(bsdf, ComposeSpatialVarying):
         k = bsdf.sp_var_fn(bsdf.preprocess(it.p)).reshape(it.p.shape[:-1] + (len(bsdf.bsdfs),))
         setattr(it, "nonnormalized_weights", k)
@@ -254,11 +255,21 @@ def bsdf_eval(bsdf, it, wo, active, feat=None):
         # reference recomputes them per component (bsdfs.py:634-637); computing them once gives
         # the same values and the same gradient (autograd sums the components' contributions),
         # with ~40 forward and ~80 backward launches per component fewer
-        if sum(isinstance(b, NeuralBSDF) for b in bsdf.bsdfs) > 1:
+        neural = [b for b in bsdf.bsdfs if isinstance(b, NeuralBSDF)]
+        pre = {}
+        if len(neural) > 1:
             feat = param_rusin2(it.wi, wo)
+            mlps = [b.mlp for b in neural]
+            if same_shape(mlps) and not any(m.latent_size for m in mlps):
+                # the components' MLPs on the shared features: one batched HIP backward
+                pre = {id(b): y for b, y in zip(neural, mlp_multi(mlps, feat))}
         parts = []
         for b in bsdf.bsdfs:
-            f, pdf = bsdf_eval(b, it, wo, active, feat)
+            if id(b) in pre:
+                f = b.act(pre[id(b)])
+                pdf = torch.ones(f.shape[:-1], device=f.device)
+            else:
+                f, pdf = bsdf_eval(b, it, wo, active, feat)
             parts.append(torch.cat([f, pdf.reshape(f.shape[:-1] + (1,))], dim=-1))
         spec_pdf = torch.stack(parts, dim=-1)
         setattr(it, "normalized_weights", k)

@@ -183,6 +183,80 @@ class _MlpFn(torch.autograd.Function):
         return (None, dx, dlat, *grads)
 
 
+def _shape_key(m):
+    return (m.in_size, m.init.out_features, len(m.layers), m.out.out_features, m.skip,
+            m.latent_size, m.activation_code(), tuple(m.basis_p.shape))
+
+
+def same_shape(mlps):
+    """True when the SkipConnMLPs share one architecture (nrt_mlp_backward_multi's condition)."""
+    k = _shape_key(mlps[0])
+    return all(_shape_key(m) == k for m in mlps[1:])
+
+
+def mlp_multi(mlps, x):
+    """[mlp(x) for mlp in mlps] for same-shape SkipConnMLPs (no latent) on one input -- the
+    NeuralBSDFs of a spatially varying mixture on the shared Rusinkiewicz features
+    (bsdfs.py:634-637).  Under autograd the backward of all of them is one
+    nrt_mlp_backward_multi call (one backward launch, one weight-gradient launch)."""
+    flat = x.reshape(-1, mlps[0].in_size).float().contiguous()
+    params = [t for m in mlps for lin in m._linears() for t in (lin.weight, lin.bias)]
+    if not (torch.is_grad_enabled() and (flat.requires_grad or any(q.requires_grad for q in params))):
+        return [m(x) for m in mlps]
+    if any(t.device != x.device for t in params):
+        raise _lib.NrtError("SkipConnMLP parameters and inputs are on different devices: "
+                            "move the module to the GPU (.to(device)) to train it")
+    ys = _MultiMlpFn.apply(tuple(mlps), flat, *params)
+    return [y.reshape(x.shape[:-1] + (m.out.out_features,)) for y, m in zip(ys, mlps)]
+
+
+class _MultiMlpFn(torch.autograd.Function):
+    """ys[i] = mlps[i](x): the forwards on the HIP MLP kernels; the backward (dL/dx summed over
+    the MLPs, every nn.Linear weight and bias) in one nrt_mlp_backward_multi call."""
+
+    @staticmethod
+    def forward(ctx, mlps, x, *params):
+        handles = [train_handle(m) for m in mlps]
+        with torch.no_grad():
+            ys = [_mlp_forward(m, x.detach(), None, h) for m, h in zip(mlps, handles)]
+        ctx.mlps = mlps
+        ctx.handles = handles
+        _save_versions(ctx, params)
+        ctx.save_for_backward(x)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        import ctypes
+        _check_versions(ctx)
+        if torch.is_grad_enabled():
+            raise _lib.NrtError("second derivatives through SkipConnMLP.forward are not on the HIP "
+                                "path")
+        (x,) = ctx.saved_tensors
+        mlps, n, M = ctx.mlps, len(ctx.mlps), x.shape[0]
+        lib = _lib.load(require_device=True)
+        dys = [dy.float().contiguous() for dy in dys]
+        dx = torch.empty(n, M, x.shape[1], device=x.device) if ctx.needs_input_grad[1] else None
+        grads, wptr, bptr = [], [], []
+        for m in mlps:
+            for lin in m._linears():
+                dw = torch.empty_like(lin.weight) if lin.weight.requires_grad else None
+                db = torch.empty_like(lin.bias) if lin.bias.requires_grad else None
+                grads += [dw, db]
+                wptr.append(0 if dw is None else dw.data_ptr())
+                bptr.append(0 if db is None else db.data_ptr())
+        P = ctypes.c_void_p
+        hs = (P * n)(*[h.value for h in ctx.handles])
+        dyp = (P * n)(*[d.data_ptr() for d in dys])
+        dxp = None if dx is None else (P * n)(*[dx[i].data_ptr() for i in range(n)])
+        wp, bp = (P * len(wptr))(*wptr), (P * len(bptr))(*bptr)
+        ws = torch.empty(lib.nrt_mlp_backward_multi_workspace_bytes(hs, n, M), dtype=torch.uint8,
+                         device=x.device)
+        _lib.call("nrt_mlp_backward_multi", hs, n, _lib.ptr(x), M, dyp, dxp, wp, bp,
+                  _lib.ptr(ws), _lib.stream())
+        return (None, None if dx is None else dx.sum(0), *grads)
+
+
 def input_gradient(mlp, x):
     """d(sum_o mlp(x)_o)/dx -- torch.autograd.grad(mlp(x), x, ones, create_graph=True), the SDF
     normal of SDF.autograd_diff (sdfs.py:184-197) -- on the HIP path: nrt_mlp_backward for the

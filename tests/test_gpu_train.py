@@ -167,3 +167,30 @@ def test_refreshed_handle_matches_a_fresh_pack(prec):
     (mlp(x) * dy.cuda()).sum().backward()
     for i, a in enumerate(mlp._linears()):
         _close(a.weight.grad, want[f"dW[{i}]"], ref32[f"dW[{i}]"], f"dW[{i}]")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 77, 5000])
+@pytest.mark.parametrize("name", ["neural_bsdf_6x96_F64", "sp_var_16x256_F128"])
+def test_mlp_backward_multi_matches_single(name, M):
+    """nrt_mlp_backward_multi (n same-shape MLPs on one input: the mixture's NeuralBSDFs, one
+    batched launch) against each MLP's own nrt_mlp_backward through autograd: dL/dx summed over
+    the MLPs and every weight / bias gradient, relative 1e-5 (only the split-K slice count of the
+    weight gradients differs)."""
+    from neural_raytracing_amd.pathtracer.neural_blocks import mlp_multi
+    kw = SHAPES[name]
+    mlps = [_pair(kw, seed)[1] for seed in (1, 2, 3)]
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, kw["in_size"], generator=g) * 2 - 1).cuda()
+    dys = [torch.randn(M, kw["out"], generator=g).cuda() for _ in mlps]
+    params = [q for m in mlps for q in m.parameters()]
+
+    def grads(batched):
+        xx = x.clone().requires_grad_(True)
+        ys = mlp_multi(mlps, xx) if batched else [m(xx) for m in mlps]
+        loss = sum((y * dy).sum() for y, dy in zip(ys, dys))
+        return torch.autograd.grad(loss, [xx] + params)
+    got, want = grads(True), grads(False)
+    for a, b in zip(got, want):
+        scale = b.abs().max().clamp_min(1e-6)
+        assert ((a - b).abs().max() / scale) < 1e-5, (name, M, (a - b).abs().max(), scale)
