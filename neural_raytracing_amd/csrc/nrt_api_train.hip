@@ -16,8 +16,10 @@
 
 namespace nrt {
 
-// A-fragment prefetch depth of the training kernels' slab GEMMs (gemm32): one wave per SIMD
-constexpr int kTrainPF = 4;
+// A-fragment prefetch depth of the training kernels' slab GEMMs (gemm32): they run one wave per
+// SIMD from 4 row blocks up (accumulators + slab), where 8 buffers fit; at 3 row blocks and
+// below 4, which keeps two waves per SIMD
+constexpr int train_pf(int nb) { return nb >= 4 ? 8 : 4; }
 
 // reference encoding column of slot s ([x, sin(xB), cos(xB), latent], utils.py:37-40); -1 = pad
 __device__ __forceinline__ int enc_col(const MlpDev& m, int s) {
@@ -88,15 +90,15 @@ __device__ __forceinline__ void mlp_backward32(
   for (int l = 0; l <= L; ++l) {
     bias32<NB>(acc, m.bias[l], 0, NB, h);
     if (l == 0) {
-      if (TILE) gemm32_tile<NB, kTrainPF>(acc, m.w32[0], NB, 0, ke >> 1, et - r, -1);
-      else gemm32<NB, kTrainPF>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, H, -1);
+      if (TILE) gemm32_tile<NB, train_pf(NB)>(acc, m.w32[0], NB, 0, ke >> 1, et - r, -1);
+      else gemm32<NB, train_pf(NB)>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, H, -1);
     } else {
       const int i = l - 1;
-      gemm32<NB, kTrainPF>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
+      gemm32<NB, train_pf(NB)>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
       if (i != L - 1 && (i % m.skip) == 0) {
         const float* Ws = m.w32[l] + (H >> 1) * NB * 64;
-        if (TILE) gemm32_tile<NB, kTrainPF>(acc, Ws, NB, 0, ke >> 1, et - r, m.act);
-        else gemm32<NB, kTrainPF>(acc, Ws, NB, 0, ke >> 1, X, RS, H, m.act);
+        if (TILE) gemm32_tile<NB, train_pf(NB)>(acc, Ws, NB, 0, ke >> 1, et - r, m.act);
+        else gemm32<NB, train_pf(NB)>(acc, Ws, NB, 0, ke >> 1, X, RS, H, m.act);
       }
     }
     wave_lds_fence();
@@ -160,7 +162,7 @@ __device__ __forceinline__ void mlp_backward32(
       for (int rb0 = hid_rb; rb0 < nrb; rb0 += NB) {
 #pragma unroll
         for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
-        gemm32<NB, kTrainPF>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+        gemm32<NB, train_pf(NB)>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
 #pragma unroll
         for (int ib = 0; ib < NB; ++ib) {
           if (rb0 + ib >= nrb) continue;
@@ -184,7 +186,7 @@ __device__ __forceinline__ void mlp_backward32(
     if (has_hidden_in) {
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
-      gemm32<NB, kTrainPF>(acc, At, nrb, 0, H >> 1, X, RS, 0, -1);
+      gemm32<NB, train_pf(NB)>(acc, At, nrb, 0, H >> 1, X, RS, 0, -1);
       wave_lds_fence();
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib)
@@ -336,10 +338,10 @@ __global__ void __launch_bounds__(256) k_mlp_grad_backward32(
     const bool skip = l > 0 && (l - 1) != L - 1 && ((l - 1) % m.skip) == 0;
     bias32<NB>(acc, m.bias[l], 0, NB, h);
     if (l == 0) {
-      gemm32<NB, kTrainPF>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, EE, -1);
+      gemm32<NB, train_pf(NB)>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, EE, -1);
     } else {
-      gemm32<NB, kTrainPF>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
-      if (skip) gemm32<NB, kTrainPF>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, EE, m.act);
+      gemm32<NB, train_pf(NB)>(acc, m.w32[l], NB, 0, H >> 1, X, RS, 0, -1);
+      if (skip) gemm32<NB, train_pf(NB)>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, EE, m.act);
     }
     wave_lds_fence();
 #pragma unroll
@@ -359,10 +361,10 @@ __global__ void __launch_bounds__(256) k_mlp_grad_backward32(
 #pragma unroll
     for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
     if (l == 0) {
-      gemm32<NB, kTrainPF>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, ET, -1);
+      gemm32<NB, train_pf(NB)>(acc, m.w32[0], NB, 0, ke >> 1, X, RS, ET, -1);
     } else {
-      gemm32<NB, kTrainPF>(acc, m.w32[l], NB, 0, H >> 1, X, RS, PT, -1);
-      if (skip) gemm32<NB, kTrainPF>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, ET, -1);
+      gemm32<NB, train_pf(NB)>(acc, m.w32[l], NB, 0, H >> 1, X, RS, PT, -1);
+      if (skip) gemm32<NB, train_pf(NB)>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, 0, ke >> 1, X, RS, ET, -1);
     }
     wave_lds_fence();
 #pragma unroll
@@ -415,7 +417,7 @@ __global__ void __launch_bounds__(256) k_mlp_grad_backward32(
       const int col = pass ? PT : 0;
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
-      gemm32<NB, kTrainPF>(acc, At, nrb, 0, H >> 1, X, RS, col, -1);
+      gemm32<NB, train_pf(NB)>(acc, At, nrb, 0, H >> 1, X, RS, col, -1);
       wave_lds_fence();
 #pragma unroll
       for (int ib = 0; ib < NB; ++ib)
