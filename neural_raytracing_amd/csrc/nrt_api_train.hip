@@ -523,32 +523,51 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
   // the A operand, clamped columns / rows feed only outputs that are never stored
   const int ia = std::min(r0 + i, R - 1), ib = std::min(r0 + 32 + i, R - 1);
   const int ja = std::min(c0 + i, C - 1), jbb = std::min(c0 + 32 + i, C - 1);
-  for (int64_t m = m0 + (int64_t)w * 2 * U; m < m1; m += (int64_t)kWgradWaves * 2 * U) {
-    float a0[U], a1[U], b0[U], b1[U];
-    int ok = 0;
+  // software-pipelined over groups of U k-steps: group g + 1's loads are in flight while group
+  // g's MFMAs run (two register sets, the loop unrolled by two)
+  struct Grp { float a0[U], a1[U], b0[U], b1[U]; int ok; };
+  auto load = [&](Grp& q, int64_t m) {
+    q.ok = 0;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t row = m + 2 * u + h;
-      ok |= row < m1 ? (1 << u) : 0;
+      q.ok |= row < m1 ? (1 << u) : 0;
       const int64_t rc = row < m1 ? row : m1 - 1;
       const float* zr = dZ + rc * R;
-      a0[u] = zr[ia]; a1[u] = zr[ib];
+      q.a0[u] = zr[ia]; q.a1[u] = zr[ib];
       if (In) {
         const float* ir = In + rc * ldi;
-        b0[u] = ir[ja]; b1[u] = ir[jbb];
+        q.b0[u] = ir[ja]; q.b1[u] = ir[jbb];
       } else {
-        b0[u] = 1.f; b1[u] = 1.f;
+        q.b0[u] = 1.f; q.b1[u] = 1.f;
       }
     }
+  };
+  auto mma = [&](const Grp& q) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool o = (ok >> u) & 1;
-      const float x0 = o ? a0[u] : 0.f, x1 = o ? a1[u] : 0.f;
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, b0[u], acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, b1[u], acc[1], 0, 0, 0);
-      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, b0[u], acc[2], 0, 0, 0);
-      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, b1[u], acc[3], 0, 0, 0);
+      const bool o = (q.ok >> u) & 1;
+      const float x0 = o ? q.a0[u] : 0.f, x1 = o ? q.a1[u] : 0.f;
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, q.b0[u], acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(x0, q.b1[u], acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, q.b0[u], acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(x1, q.b1[u], acc[3], 0, 0, 0);
     }
+  };
+  const int64_t gstep = (int64_t)kWgradWaves * 2 * U;
+  int64_t m = m0 + (int64_t)w * 2 * U;
+  Grp g0, g1;
+  if (m < m1) load(g0, m);
+  while (m < m1) {
+    const int64_t mn = m + gstep;
+    if (mn < m1) load(g1, mn);
+    mma(g0);
+    m = mn;
+    if (m >= m1) break;
+    const int64_t mn2 = m + gstep;
+    if (mn2 < m1) load(g0, mn2);
+    mma(g1);
+    m = mn2;
   }
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
