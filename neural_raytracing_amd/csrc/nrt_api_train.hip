@@ -163,9 +163,37 @@ __device__ __forceinline__ void mlp_backward32(
 #pragma unroll
         for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
         gemm32<NB, train_pf(NB)>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+        // per row block: every load first (clamped addresses, unconditional), then the
+        // activation's branches -- a load inside the act switch would wait on its own.  From
+        // four row blocks up (one wave per SIMD already); below, the registers keep two waves.
 #pragma unroll
         for (int ib = 0; ib < NB; ++ib) {
           if (rb0 + ib >= nrb) continue;
+          if constexpr (NB < 4) {
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+              const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+              const int slot = pos - enc_pos0;
+              if (slot >= 0 && slot < ke) {
+                float v = acc[ib][reg];
+                if (l != 0) {  // skip inputs are act(enc)
+                  const int c = enc_col(m, slot);
+                  v = c < 0 ? 0.f : v * act_bwd(eraw_row[c], m.act);
+                }
+                gt[slot * es] += v;
+              }
+            }
+            continue;
+          }
+          float ev[16], gv[16];
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int slot = min(max(pos - enc_pos0, 0), ke - 1);
+            const int c = l != 0 ? enc_col(m, slot) : -1;
+            ev[reg] = eraw_row[c < 0 ? 0 : c];
+            gv[reg] = gt[slot * es];
+          }
 #pragma unroll
           for (int reg = 0; reg < 16; ++reg) {
             const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
@@ -174,9 +202,9 @@ __device__ __forceinline__ void mlp_backward32(
               float v = acc[ib][reg];
               if (l != 0) {  // skip inputs are act(enc)
                 const int c = enc_col(m, slot);
-                v = c < 0 ? 0.f : v * act_bwd(eraw_row[c], m.act);
+                v = c < 0 ? 0.f : v * act_bwd(ev[reg], m.act);
               }
-              gt[slot * es] += v;
+              gt[slot * es] = gv[reg] + v;
             }
           }
         }
@@ -188,16 +216,26 @@ __device__ __forceinline__ void mlp_backward32(
       for (int ib = 0; ib < NB; ++ib) acc[ib] = f16v{};
       gemm32<NB, train_pf(NB)>(acc, At, nrb, 0, H >> 1, X, RS, 0, -1);
       wave_lds_fence();
+      // the row block's four Z loads issue together, ahead of the activation's branches (from
+      // four row blocks up, as above)
 #pragma unroll
-      for (int ib = 0; ib < NB; ++ib)
+      for (int ib = 0; ib < NB; ++ib) {
+        constexpr int Q = NB < 4 ? 1 : 4;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int k0 = 32 * ib + 8 * g + 4 * h;
-          const float4 zv = *reinterpret_cast<const float4*>(Zg + ((int64_t)(l - 1) * M + rr) * H + k0);
-          const float* zp = &zv.x;
+        for (int g0 = 0; g0 < 4; g0 += Q) {
+          float4 zq[Q];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) rowp[k0 + j] = acc[ib][4 * g + j] * act_bwd(zp[j], m.act);
+          for (int q = 0; q < Q; ++q)
+            zq[q] = *reinterpret_cast<const float4*>(Zg + ((int64_t)(l - 1) * M + rr) * H + 32 * ib + 8 * (g0 + q) + 4 * h);
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            const int k0 = 32 * ib + 8 * (g0 + q) + 4 * h;
+            const float* zp = &zq[q].x;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) rowp[k0 + j] = acc[ib][4 * (g0 + q) + j] * act_bwd(zp[j], m.act);
+          }
         }
+      }
       wave_lds_fence();
     }
   }
@@ -224,8 +262,9 @@ __device__ __forceinline__ void mlp_backward32(
     for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[es * (2 * F + in + j)];
 }
 
+// below four row blocks two waves per SIMD fit (registers and slab): ask the compiler for that
 template <int NB, bool TILE>
-__global__ void __launch_bounds__(256) k_mlp_backward32(
+__global__ void __launch_bounds__(256, NB < 4 ? 2 : 1) k_mlp_backward32(
     const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
     int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
     float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
@@ -244,7 +283,7 @@ struct BwdJob {
 };
 
 template <int NB, bool TILE>
-__global__ void __launch_bounds__(256) k_mlp_backward32_multi(
+__global__ void __launch_bounds__(256, NB < 4 ? 2 : 1) k_mlp_backward32_multi(
     const BwdJob* __restrict__ jobs, const float* __restrict__ x, int64_t M, int RS, int per_wave) {
   const BwdJob j = jobs[blockIdx.y];
   mlp_backward32<NB, TILE>(j.mp, x, nullptr, M, j.dY, j.dX, nullptr, j.Z, j.A, j.Eraw, j.Eact,
