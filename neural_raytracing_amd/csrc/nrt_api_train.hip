@@ -264,7 +264,7 @@ __device__ __forceinline__ void mlp_backward32(
 
 // below four row blocks two waves per SIMD fit (registers and slab): ask the compiler for that
 template <int NB, bool TILE>
-__global__ void __launch_bounds__(256, NB < 4 ? 2 : 1) k_mlp_backward32(
+__global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_backward32(
     const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
     int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
     float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
@@ -283,7 +283,7 @@ struct BwdJob {
 };
 
 template <int NB, bool TILE>
-__global__ void __launch_bounds__(256, NB < 4 ? 2 : 1) k_mlp_backward32_multi(
+__global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_backward32_multi(
     const BwdJob* __restrict__ jobs, const float* __restrict__ x, int64_t M, int RS, int per_wave) {
   const BwdJob j = jobs[blockIdx.y];
   mlp_backward32<NB, TILE>(j.mp, x, nullptr, M, j.dY, j.dX, nullptr, j.Z, j.A, j.Eraw, j.Eact,
@@ -316,7 +316,7 @@ __device__ __forceinline__ float act_bwd2(float x, int act) {
 // and dW_l = z_bar^T In_l + zt_bar^T InT_l, db_l = sum z_bar, done afterwards as one GEMM over the
 // stacked [primal; tangent] rows.  Slab row: [a | enc | enc tangent | a tangent].
 template <int NB>
-__global__ void __launch_bounds__(256) k_mlp_grad_backward32(
+__global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_grad_backward32(
     const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
     const float* __restrict__ v, int64_t M, float* __restrict__ Zg, float* __restrict__ Tg,
     float* __restrict__ Ag, float* __restrict__ E0, float* __restrict__ E1,
