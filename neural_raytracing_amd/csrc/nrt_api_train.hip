@@ -669,6 +669,10 @@ int batch_slices(int64_t total_tiles, int64_t M) {
 struct WgradBatch {
   std::vector<WgradJob> jobs;
   int max_jobs = kMaxWgradJobs;  // the device table's capacity
+  // the slice count the workspace was sized with (the full job plan's); 0 = plan it.  A batch
+  // with some gradients not requested has fewer tiles, so planning it anew would choose more
+  // slices than the partial-product region holds.
+  int slices = 0;
   void weight(const float* dZ, int R, const float* In, int C, int64_t M, float* dW, int ldw, int c0) {
     WgradJob j{};
     j.dZ = dZ; j.In = In; j.dW = dW; j.M = M; j.R = R; j.C = C; j.ldi = C; j.ldw = ldw; j.c0 = c0;
@@ -688,7 +692,7 @@ struct WgradBatch {
       tiles += j.n_tiles;
       Mmax = std::max(Mmax, j.M);
     }
-    S = batch_slices(std::max<int64_t>(tiles, 1), Mmax);
+    S = slices > 0 ? slices : batch_slices(std::max<int64_t>(tiles, 1), Mmax);
     int64_t block = 0, out = 0;
     size_t off = 0;
     for (auto& j : jobs) {
@@ -703,11 +707,12 @@ struct WgradBatch {
     return off;
   }
   // table: kMaxWgradJobs * sizeof(WgradJob) bytes of device memory; part: the plan's floats
-  int run(void* table, float* part, hipStream_t st) {
+  // part_cap: the floats the workspace's partial-product region holds
+  int run(void* table, float* part, size_t part_cap, hipStream_t st) {
     if (jobs.empty()) return NRT_OK;
     if ((int)jobs.size() > max_jobs) { set_error("weight gradients: too many jobs"); return NRT_EINVAL; }
     int S = 1;
-    plan(S);
+    if (plan(S) > part_cap) { set_error("weight gradients: partial products exceed the workspace"); return NRT_EINVAL; }
     int64_t blocks = 0, total = 0;
     for (auto& j : jobs) { blocks += (int64_t)j.n_tiles * S; total += (int64_t)j.R * j.C; }
     NRT_HIP(hipMemcpyAsync(table, jobs.data(), jobs.size() * sizeof(WgradJob), hipMemcpyHostToDevice, st));
@@ -744,14 +749,17 @@ void backward_jobs(const MlpDev& d, bool grad_bwd, F&& f) {
   }
 }
 
-size_t batch_part_floats(const MlpDev& d, int64_t M, bool grad_bwd) {
+// the partial floats and slice count of every job of one MLP's backward (the workspace's plan)
+size_t batch_part_floats(const MlpDev& d, int64_t M, bool grad_bwd, int* slices = nullptr) {
   WgradBatch b;
   backward_jobs(d, grad_bwd, [&](int, int R, int kind, int C, int ldw, int c0) {
     if (kind == 3) b.bias(nullptr, R, M, nullptr);
     else b.weight(nullptr, R, nullptr, C, grad_bwd ? 2 * M : M, nullptr, ldw, c0);
   });
   int S = 1;
-  return b.plan(S);
+  const size_t floats = b.plan(S);
+  if (slices) *slices = S;
+  return floats;
 }
 // k_mlp_backward32's LDS plan: slab row [hidden | encoding] (H + ke floats), or [hidden] with the
 // encoding in global tiles when that at least doubles the waves per CU (TILE)
@@ -792,6 +800,19 @@ void multi_jobs(const MlpDev& d, int n, int64_t M, WgradBatch& b, F&& f) {
   for (int i = 0; i < n; ++i)
     backward_jobs(d, false, [&](int l, int R, int kind, int C, int ldw, int c0) { f(i, l, R, kind, C, ldw, c0); });
   (void)M;
+}
+
+// the partial floats and slice count of every job of n same-shape MLPs' backward
+size_t multi_part_floats(const MlpDev& d, int n, int64_t M, int* slices = nullptr) {
+  WgradBatch b;
+  multi_jobs(d, n, M, b, [&](int, int, int R, int kind, int C, int, int) {
+    if (kind == 3) b.bias(nullptr, R, M, nullptr);
+    else b.weight(nullptr, R, nullptr, C, M, nullptr, 0, 0);
+  });
+  int S = 1;
+  const size_t floats = b.plan(S);
+  if (slices) *slices = S;
+  return floats;
 }
 }  // namespace
 
@@ -861,6 +882,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   // every weight and bias gradient in one batched split-K launch (+ its slice reduction)
   const size_t lay = (size_t)M * H;
   WgradBatch batch;
+  const size_t cap = batch_part_floats(d, M, false, &batch.slices);
   backward_jobs(d, false, [&](int l, int R, int kind, int C, int ldw, int c0) {
     const float* dZ = l == L + 1 ? dy : w.dZ + (size_t)l * lay;
     if (kind == 3) {
@@ -871,20 +893,14 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     const float* In = kind == 0 ? w.Eraw : kind == 1 ? w.A + (size_t)(l - 1) * lay : w.Eact;
     batch.weight(dZ, R, In, C, M, dweights[l], ldw, c0);
   });
-  return batch.run(w.part, w.kpart, st);
+  return batch.run(w.part, w.kpart, cap, st);
 }
 
 size_t nrt_mlp_backward_multi_workspace_bytes(const nrt_mlp* const* mlps, int n, int64_t M) {
   if (!mlps || n <= 0 || !mlps[0]) return 0;
   M = std::max<int64_t>(M, 1);
   const MlpDev& d = mlps[0]->host_dev;
-  WgradBatch b;
-  multi_jobs(d, n, M, b, [&](int, int, int R, int kind, int C, int, int) {
-    if (kind == 3) b.bias(nullptr, R, M, nullptr);
-    else b.weight(nullptr, R, nullptr, C, M, nullptr, 0, 0);
-  });
-  int S = 1;
-  const size_t part = b.plan(S);
+  const size_t part = multi_part_floats(d, n, M);
   return (size_t)n * region_bytes(d, M) + a256((size_t)n * sizeof(BwdJob)) +
          a256((size_t)n * kWgradTableBytes) + a256(part * 4);
 }
@@ -952,6 +968,7 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   if (!dweights && !dbiases) return NRT_OK;
   const size_t lay = (size_t)M * H;
   WgradBatch batch;
+  const size_t cap = multi_part_floats(d, n, M, &batch.slices);
   multi_jobs(d, n, M, batch, [&](int i, int l, int R, int kind, int C, int ldw, int c0) {
     const TrainWs& w = ws[i];
     const float* dZ = l == L + 1 ? dy[i] : w.dZ + (size_t)l * lay;
@@ -963,7 +980,7 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
     const float* In = kind == 0 ? w.Eraw : kind == 1 ? w.A + (size_t)(l - 1) * lay : w.Eact;
     batch.weight(dZ, R, In, C, M, dweights[(size_t)i * NL + l], ldw, c0);
   });
-  return batch.run(table, part, st);
+  return batch.run(table, part, cap, st);
 }
 
 static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {
@@ -1047,6 +1064,7 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   // the out layer's bias takes no gradient from J (its tangent rows carry no bias)
   if (dbiases && dbiases[L + 1]) NRT_HIP(hipMemsetAsync(dbiases[L + 1], 0, (size_t)d.out * 4, st));
   WgradBatch batch;
+  const size_t cap = batch_part_floats(d, M, true, &batch.slices);
   backward_jobs(d, true, [&](int l, int R, int kind, int C, int ldw, int c0) {
     const float* dZ = l == L + 1 ? seed : buf[3] + (size_t)l * lay2;
     if (kind == 3) {  // bias: the primal rows only
@@ -1057,7 +1075,7 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
     const float* In = kind == 0 ? buf[4] : kind == 1 ? buf[2] + (size_t)(l - 1) * lay2 : buf[5];
     batch.weight(dZ, R, In, C, M2, dweights[l], ldw, c0);
   });
-  return batch.run(part, buf[8], st);
+  return batch.run(part, buf[8], cap, st);
 }
 
 }  // extern "C"

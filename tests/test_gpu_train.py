@@ -194,3 +194,65 @@ def test_mlp_backward_multi_matches_single(name, M):
     for a, b in zip(got, want):
         scale = b.abs().max().clamp_min(1e-6)
         assert ((a - b).abs().max() / scale) < 1e-5, (name, M, (a - b).abs().max(), scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frozen", ["biases", "weights_of_odd_layers"])
+def test_mlp_backward_with_frozen_parameters(frozen):
+    """Some parameters frozen (requires_grad=False: a null gradient pointer at the boundary) at a
+    batch large enough that the weight-gradient batch has fewer tiles than the full plan the
+    workspace was sized for: the batch keeps the full plan's slice count (a re-plan
+    chose more slices and wrote past the workspace).  The requested gradients match float64
+    autograd; the frozen ones stay None."""
+    from neural_raytracing_amd import set_precision
+    kw = SHAPES["8x64_leaky"]
+    ref, mine = _pair(kw, 91)
+    set_precision("fp32")
+    lins = mine._linears()
+    for i, a in enumerate(lins):
+        if frozen == "biases":
+            a.bias.requires_grad_(False)
+        elif i % 2 == 1:
+            a.weight.requires_grad_(False)
+    M = 20000
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(M, 3, generator=g) - 0.5
+    dy = torch.randn(M, 3, generator=g)
+    want = _grads(ref, x, None, dy, torch.float64)
+    ref32 = _grads(ref, x, None, dy, torch.float32)
+    xm = x.cuda().requires_grad_(True)
+    (mine(xm) * dy.cuda()).sum().backward()
+    _close(xm.grad, want["dx"], ref32["dx"], "dx")
+    for i, a in enumerate(lins):
+        for nm, t in (("dW", a.weight), ("db", a.bias)):
+            if t.requires_grad:
+                _close(t.grad, want[f"{nm}[{i}]"], ref32[f"{nm}[{i}]"], f"{nm}[{i}]")
+            else:
+                assert t.grad is None
+
+
+@pytest.mark.gpu
+def test_mlp_backward_multi_with_frozen_biases():
+    """The batched mixture backward with frozen biases at a large batch matches the per-MLP
+    backward (same slice-count rule as the single-MLP batch)."""
+    from neural_raytracing_amd.pathtracer.neural_blocks import mlp_multi
+    kw = SHAPES["neural_bsdf_6x96_F64"]
+    mlps = [_pair(kw, seed)[1] for seed in (4, 5)]
+    for m in mlps:
+        for a in m._linears():
+            a.bias.requires_grad_(False)
+    M = 30000
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand(M, 3, generator=g) * 2 - 1).cuda()
+    dys = [torch.randn(M, 3, generator=g).cuda() for _ in mlps]
+    params = [q for m in mlps for q in m.parameters() if q.requires_grad]
+
+    def grads(batched):
+        xx = x.clone().requires_grad_(True)
+        ys = mlp_multi(mlps, xx) if batched else [m(xx) for m in mlps]
+        loss = sum((y * dy).sum() for y, dy in zip(ys, dys))
+        return torch.autograd.grad(loss, [xx] + params)
+    got, want = grads(True), grads(False)
+    for a, b in zip(got, want):
+        scale = b.abs().max().clamp_min(1e-6)
+        assert ((a - b).abs().max() / scale) < 1e-5, ((a - b).abs().max(), scale)
