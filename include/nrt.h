@@ -225,6 +225,11 @@ int nrt_light_create_field(const nrt_mlp* mlp, const float* host_color3, nrt_lig
 int nrt_light_create_point(const float* host_location3, const float* host_intensity3,
                            float constant, float linear, float square, float scale,
                            nrt_light** out);
+/* pytorch3d.renderer.PointLights as a pathtracer light (renderer/lighting.py:221-304, the light
+ * of utils.sphere_examples, utils.py:409-431): d = (loc - p) / (1e-7 + |loc - p|),
+ * Le = scale * intensity / (1e-7 + |loc - p|)^2, intensity = ambient_color; one light */
+int nrt_light_create_renderer_point(const float* host_location3, const float* host_intensity3,
+                                    float scale, nrt_light** out);
 int nrt_light_destroy(nrt_light* light);
 
 #define NRT_BSDF_NEURAL 0     /* NeuralBSDF (bsdfs.py:613-637): act(MLP(param_rusin2))     */
@@ -330,6 +335,14 @@ int nrt_raygen(const nrt_camera* host_cams, int32_t N, int32_t x0, int32_t y0, i
 /* SurfaceInteraction.set_normals + to_local(-d) (interaction.py:73-78, sdfs.py:158-159):
  * frame[P,9] = coordinate_system(n) as [s | t | n] columns (row-major 3x3, may be NULL) and
  * wi[P,3] = to_local(frame, -d) (may be NULL). */
+/* Sphere (shapes/shapes.py:31-97): the analytic ray / sphere hit in the reference's float32 op
+ * order (quad_solve :11-18; nearest root >= 1e-8; p = o + t d + 1e-5 n, n = normalize(p - c)).
+ * center: 3 host floats; radius: the python float (sqr_radius = radius^2 in double, then f32).  Optional outputs (NULL = skip): t, hit, p, n (needs p), upper = the far
+ * root (intersect_limits, :78-91), hit_idx + hit_count (compacted hit list, count zeroed here).
+ * intersect_test (:70-77) is the hit output alone. */
+int nrt_sphere_intersect(const float* center, double radius, const float* rays, int64_t P,
+                         float* t, uint8_t* hit, float* p, float* n, float* upper,
+                         int32_t* hit_idx, int32_t* hit_count, void* stream);
 int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi,
                void* stream);
 

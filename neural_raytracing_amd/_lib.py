@@ -81,7 +81,9 @@ _SIGNATURES = {
     "nrt_occlusion_callable_step": (_I32, [_P, _I64, _P, _F, _F, _P, _I32, _P, _P, _P, _P, _P]),
     "nrt_light_create_field": (_I32, [_P, _P, ctypes.POINTER(_P)]),
     "nrt_light_create_point": (_I32, [_P, _P, _F, _F, _F, _F, ctypes.POINTER(_P)]),
+    "nrt_light_create_renderer_point": (_I32, [_P, _P, _F, ctypes.POINTER(_P)]),
     "nrt_light_destroy": (_I32, [_P]),
+    "nrt_sphere_intersect": (_I32, [_P, ctypes.c_double, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "nrt_bsdf_create": (_I32, [_I32, _P, _P, ctypes.POINTER(_P)]),
     "nrt_bsdf_destroy": (_I32, [_P]),
     "nrt_shade_direct": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I32, _P]),

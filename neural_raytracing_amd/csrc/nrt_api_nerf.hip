@@ -647,8 +647,9 @@ size_t nrt_nerfle_workspace_bytes_for(const nrt_mlp* first, const nrt_mlp* secon
 
 int nrt_light_envmap(const nrt_light* l, int32_t bins, float* out, void* stream) {
   if (!l || bins < 1 || !out) { set_error("nrt_light_envmap: bad argument"); return NRT_EINVAL; }
-  if (l->host_dev.kind != 1) {
-    set_error("nrt_light_envmap: envmap is defined for PointLights only (lights.py:81-88)");
+  if (l->host_dev.kind != 1 || l->host_dev.falloff != 0) {
+    set_error("nrt_light_envmap: envmap is defined for the pathtracer's PointLights only "
+              "(lights.py:81-88; the renderer's PointLights has none)");
     return NRT_EUNSUPPORTED;
   }
   k_light_envmap<><<<dim3(ceil_div64(bins * bins, 64)), dim3(64), 0, (hipStream_t)stream>>>(l->dev, bins, out);

@@ -43,6 +43,26 @@ int nrt_light_create_point(const float* loc, const float* inten, float c, float 
   return NRT_OK;
 }
 
+int nrt_light_create_renderer_point(const float* loc, const float* inten, float scale,
+                                    nrt_light** out) {
+  if (!loc || !inten || !out || !std::isfinite(scale)) {
+    set_error("nrt_light_create_renderer_point: bad argument");
+    return NRT_EINVAL;
+  }
+  std::unique_ptr<nrt_light> l(new nrt_light());
+  std::memset(&l->host_dev, 0, sizeof(LightDev));
+  l->host_dev.kind = 1;
+  l->host_dev.falloff = 1;
+  for (int i = 0; i < 3; ++i) {
+    l->host_dev.loc[i] = loc[i];
+    l->host_dev.scaled_dir[i] = scale * inten[i];  // self.scale * self.intensity, in f32
+  }
+  NRT_HIP(hipMalloc(&l->dev, sizeof(LightDev)));
+  NRT_HIP(hipMemcpy(l->dev, &l->host_dev, sizeof(LightDev), hipMemcpyHostToDevice));
+  *out = l.release();
+  return NRT_OK;
+}
+
 int nrt_light_destroy(nrt_light* l) {
   if (!l) return NRT_OK;
   if (l->dev) (void)hipFree(l->dev);

@@ -77,8 +77,10 @@ struct LightDev {
   const MlpDev* mlp;
   float color_sig[3];       // sigmoid(color)
   float loc[3];
-  float scaled_dir[3];      // scale * normalize(intensity)
+  float scaled_dir[3];      // scale * normalize(intensity) (falloff 0), scale * intensity (1)
   float c, l, q;            // clamped falloff coefficients
+  int falloff;              // point lights: 0 the pathtracer's (lights.py:89-110), 1 the
+                            // renderer's inverse square (renderer/lighting.py:283-304)
 };
 
 constexpr int kMaxComponents = 32;

@@ -445,6 +445,8 @@ struct RingPol16 {
     return d + ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, x, y, z);
   }
   __device__ __forceinline__ static void finish(Eng&) {}
+  static constexpr bool kGuard = false;
+  __device__ __forceinline__ static bool retry(Eng&, bool, float) { return false; }
 };
 template <int KH, int KE, int WV, int ACT>
 struct RingPol32 {
@@ -463,6 +465,8 @@ struct RingPol32 {
     return ring32::eval<KH, KE, WV, ACT, true>(E, m, x, y, z);
   }
   __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
+  static constexpr bool kGuard = false;
+  __device__ __forceinline__ static bool retry(Eng&, bool, float) { return false; }
 };
 
 // FP32-accurate evaluation on FP16 matrix cores (nrt_ring3.h, the "fp32-split" precision):
@@ -475,14 +479,24 @@ struct RingPol3 {
                                               const MarchArgs&) {
     E.init(m, s, lds, 4 * KQ, 4 * KQ);  // chunks 0 and 1: the init layer's
   }
+  // the f16 range guard (nrt_ring3.h): the wave's guarded flag picks the variant (a scalar
+  // branch: both variants pass the same block barriers)
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
+    if (__builtin_amdgcn_readfirstlane((int)E.guarded))
+      return d + ring3::eval<KH, KQ, WV, ACT, false, true>(E, m, x, y, z);
     return d + ring3::eval<KH, KQ, WV, ACT>(E, m, x, y, z);
   }
   __device__ __forceinline__ static float tan(Eng& E, const MlpDev& m, float x, float y, float z) {
+    if (__builtin_amdgcn_readfirstlane((int)E.guarded))
+      return ring3::eval<KH, KQ, WV, ACT, true, true>(E, m, x, y, z);
     return ring3::eval<KH, KQ, WV, ACT, true>(E, m, x, y, z);
   }
   __device__ __forceinline__ static void finish(Eng& E) { E.drain(); }
+  static constexpr bool kGuard = true;
+  __device__ __forceinline__ static bool retry(Eng& E, bool active, float v) {
+    return ring3::retry(E, active, v);
+  }
 };
 
 template <class Pol, int MODE>
@@ -625,6 +639,10 @@ __device__ __forceinline__ void march_body(
       const uint32_t busy = (uint32_t)__ballot(kind >= 0) & kRayMask;
       if (lane == 0) atomicAdd(a.evals, (unsigned long long)__popc(busy));
     }
+    // fp32-split range guard: an evaluation whose activations left f16's range runs again,
+    // guarded, with every lane's job state unchanged (each wave still makes one evaluation per
+    // iteration, so the block's ring barriers stay matched)
+    if (Pol::retry(E, kind >= 0, d)) continue;
     if (kind == 0) {
       if (d <= a.eps) { hit = true; ended = true; }
       else t = t + d;
@@ -716,7 +734,10 @@ __global__ void __launch_bounds__(64 * Pol::WAVES, 1) k_normal_r(
     const int64_t ii = valid ? i : total - 1;
     const int64_t idx = index ? (int64_t)index[ii] : ii;
     const float x = p_io[idx * 3], y = p_io[idx * 3 + 1], z = p_io[idx * 3 + 2];
-    const float v = Pol::tan(E, m, x, y, z);
+    float v = Pol::tan(E, m, x, y, z);
+    if constexpr (Pol::kGuard) {  // range guard: the whole block repeats the tile (one barrier)
+      while (__syncthreads_or(Pol::retry(E, true, v) ? 1 : 0)) v = Pol::tan(E, m, x, y, z);
+    }
     const float gx = __shfl(v, lane + 1), gy = __shfl(v, lane + 2), gz = __shfl(v, lane + 3);
     if (valid && lane < 16 && comp == 0) {
       float g[3] = {0.f, 0.f, 0.f};
@@ -877,6 +898,28 @@ __global__ void __launch_bounds__(256, F16 ? 2 : 1) k_occlusion(const SdfDev* __
   if (valid && lane < 32) visible[ray] = ((t >= max_t[ray]) || live) ? 1 : 0;
 }
 
+// PointLights.sample_direction at p: the unit-ish direction to the light, Le and the distance.
+// falloff 0, the pathtracer's light (lights.py:89-110): d = normalize(loc - p) (eps 1e-6),
+// Le = scale normalize(I) / max(c + l dist + q dist^2, 1e-6).  falloff 1, the renderer's
+// PointLights (renderer/lighting.py:283-304, utils.sphere_examples' light): d = (loc - p) inv,
+// Le = ((scale I) inv) inv with inv = 1 / (1e-7 + dist).
+__device__ __forceinline__ void point_light(const LightDev& lt, float px, float py, float pz,
+                                            float& lx, float& ly, float& lz, float le[3],
+                                            float& dist) {
+  const float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
+  dist = sqrtf(vx * vx + vy * vy + vz * vz);
+  if (lt.falloff == 1) {
+    const float inv = 1.f / (1e-7f + dist);
+    lx = vx * inv; ly = vy * inv; lz = vz * inv;
+    for (int k = 0; k < 3; ++k) le[k] = (lt.scaled_dir[k] * inv) * inv;
+  } else {
+    lx = vx; ly = vy; lz = vz;
+    normalize3(lx, ly, lz, 1e-6f);
+    const float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
+    for (int k = 0; k < 3; ++k) le[k] = lt.scaled_dir[k] / fall;
+  }
+}
+
 // shadow rays toward a point light for each hit-list position i (sample_emitter_dir_w_isect,
 // scene.py:290-298 with PointLights.sample_direction, lights.py:89-110): [p, normalize(loc - p)],
 // max_t = |loc - p|
@@ -891,9 +934,8 @@ __global__ void k_point_shadow_rays(const LightDev* __restrict__ lp, const float
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t idx = hit_idx[i];
     const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
-    float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
-    const float dist = sqrtf(vx * vx + vy * vy + vz * vz);
-    normalize3(vx, vy, vz, 1e-6f);
+    float vx, vy, vz, le[3], dist;
+    point_light(lt, px, py, pz, vx, vy, vz, le, dist);
     float* o = rays + i * 6;
     o[0] = px; o[1] = py; o[2] = pz; o[3] = vx; o[4] = vy; o[5] = vz;
     max_t[i] = dist;
@@ -1021,13 +1063,9 @@ __global__ void __launch_bounds__(256) k_shade_direct(
     float feat[3] = {0.f, 0.f, 0.f};
     float f[3] = {0.f, 0.f, 0.f};
     if (lt.kind == 1) {
-      // PointLights.sample_direction (lights.py:89-110)
-      float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
-      float dist = sqrtf(vx * vx + vy * vy + vz * vz);
-      ldx = vx; ldy = vy; ldz = vz;
-      normalize3(ldx, ldy, ldz, 1e-6f);
-      float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
-      le[0] = lt.scaled_dir[0] / fall; le[1] = lt.scaled_dir[1] / fall; le[2] = lt.scaled_dir[2] / fall;
+      // PointLights.sample_direction (lights.py:89-110 / renderer/lighting.py:283-304)
+      float dist;
+      point_light(lt, px, py, pz, ldx, ldy, ldz, le, dist);
       to_local(fr, ldx, ldy, ldz, wo);
       rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
     }
@@ -1155,13 +1193,9 @@ __global__ void __launch_bounds__(64 * WV, 1) k_light16(
       light_from_field(ring::tile_row(o, 0, lane), ring::tile_row(o, 1, lane),
                        ring::tile_row(o, 2, lane), lt, fr, wix, wiy, wiz, le, wo, feat);
     } else {
-      // PointLights.sample_direction (lights.py:89-110)
-      float vx = lt.loc[0] - px, vy = lt.loc[1] - py, vz = lt.loc[2] - pz;
-      float dist = sqrtf(vx * vx + vy * vy + vz * vz);
-      float ldx = vx, ldy = vy, ldz = vz;
-      normalize3(ldx, ldy, ldz, 1e-6f);
-      float fall = fmaxf((lt.c + lt.l * dist) + lt.q * (dist * dist), 1e-6f);
-      le[0] = lt.scaled_dir[0] / fall; le[1] = lt.scaled_dir[1] / fall; le[2] = lt.scaled_dir[2] / fall;
+      // PointLights.sample_direction (lights.py:89-110 / renderer/lighting.py:283-304)
+      float ldx, ldy, ldz, dist;
+      point_light(lt, px, py, pz, ldx, ldy, ldz, le, dist);
       to_local(fr, ldx, ldy, ldz, wo);
       rusin2(wix, wiy, wiz, wo[0], wo[1], wo[2], feat);
     }

@@ -20,6 +20,19 @@
 // the hi halves and as many for the lo halves (32 + 32 VGPRs at H = 256).  The weight stream
 // moves through a 2-slot LDS ring by LDS-DMA exactly as in ring32 (chunk = 32 output rows =
 // one k-step of the next layer: 2 sub-blocks x 2 halves x 1 KiB per k-step).
+//
+// Range guard.  An f16 half holds |a| < 65520; the weights are scaled per layer by the packer
+// (scale3), activations are data-dependent.  An activation past f16's range makes its hi half
+// +-inf and its lo half the opposite infinity, so the next layer's Wh ah + Wh al is inf - inf =
+// NaN in every row (0 x inf is NaN too) and the evaluation's output is NaN: a non-finite output
+// is the overflow signal, at no cost per element.  The caller (RingPol3::retry, the normal and
+// shading kernels) then re-runs the evaluation in the guarded variant (GUARD): the inputs of
+// linear layer l are scaled by 2^-e_l before the split (and its bias with them), its accumulator
+// by 2^e_l after -- powers of two, exact -- and each layer's largest scaled input is checked;
+// the first layer whose inputs still leave the range gets e_l raised by 12, and the evaluation
+// runs again, until no layer overflows (a few retries per layer at most).
+// The exponents stay with the wave (or block) for its later evaluations.  Small inputs of a
+// scaled layer keep an absolute resolution of 2^(e_l - 25), i.e. ~2^-35 of the layer's largest.
 #pragma once
 #include "nrt_device.h"
 
@@ -93,6 +106,10 @@ struct Engine {
   int sbytes, bstride;
   int slot;
   int lane, wv;
+  // range guard (see the header): lane l holds e_l, the exponent of linear layer l's inputs;
+  // `guarded` selects eval<..., GUARD>; `changed` = the last guarded evaluation raised an e_l
+  int gexp = 0;
+  bool guarded = false, changed = false;
 
   __device__ __forceinline__ void issue(int qoff, int nq, int s) {
     const int w = __builtin_amdgcn_readfirstlane(wv);
@@ -189,9 +206,28 @@ struct Engine {
 // One segment of a two-sub-block chunk: NU k-steps at ring pieces P0 + 4u + {hi b0, lo b0, hi b1,
 // lo b1}; chains a0 / a1 alternate so consecutive MFMAs are independent.  Each k-step's four LDS
 // reads are issued one k-step ahead.  side(u) runs before k-step u + 1's reads in program order.
-template <int NU, int P0, int NBV, class Side>
+struct NoSide {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+// PF = false (the guarded variant): each k-step's pieces are read in place, not a k-step ahead
+// (fewer live registers on the rare path, so the fast path keeps its allocation).
+template <int NU, int P0, int NBV, class Side, bool PF = true>
 __device__ __forceinline__ void seg(const float4* A, const u4v (&Bh)[NBV], const u4v (&Bl)[NBV],
                                     f4v& a0, f4v& a1, Side&& side) {
+  if constexpr (!PF) {
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      side(u);
+      const u4v h0 = __builtin_bit_cast(u4v, A[(P0 + 4 * u) * 64]);
+      const u4v l0 = __builtin_bit_cast(u4v, A[(P0 + 4 * u + 1) * 64]);
+      const u4v h1 = __builtin_bit_cast(u4v, A[(P0 + 4 * u + 2) * 64]);
+      const u4v l1 = __builtin_bit_cast(u4v, A[(P0 + 4 * u + 3) * 64]);
+      a0 = mfma(h0, Bh[u], a0); a1 = mfma(h1, Bh[u], a1);
+      a0 = mfma(h0, Bl[u], a0); a1 = mfma(h1, Bl[u], a1);
+      a0 = mfma(l0, Bh[u], a0); a1 = mfma(l1, Bh[u], a1);
+    }
+    return;
+  }
   float4 w0 = A[P0 * 64], w1 = A[(P0 + 1) * 64], w2 = A[(P0 + 2) * 64], w3 = A[(P0 + 3) * 64];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
@@ -236,7 +272,7 @@ __device__ __forceinline__ float act_enc_tan(float v, float t) {
 // One SkipConnMLP evaluation (output row 0) for the wave's 16 columns; every lane of a column gets
 // the value.  Columns are rays, or (TAN) 4 rays x (value, d/dx, d/dy, d/dz) as ring32::eval.
 // Every wave of the block must call it the same number of times.
-template <int KH, int KQ, int WV, int ACT, bool TAN = false>
+template <int KH, int KQ, int WV, int ACT, bool TAN = false, bool GUARD = false>
 __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, float x0, float x1,
                                       float x2) {
   constexpr int NC = KH;  // 32-row chunks per hidden layer (= k-steps of the next layer)
@@ -245,54 +281,101 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   const int comp = TAN ? (E.lane & 3) : 0;
   const bool value = comp == 0;
   const int F = m.freqs, L = m.n_hidden, SK = m.skip;
-  // encoding: element e of k-step v in lane group g is slot 32 v + 8 g + e -- sin / cos of
-  // projection slot / 2 (utils.py:37-40, same fma order and accurate sincosf as the FP32 ring),
-  // then x, zeros.  Pairs (e, e + 1) share a projection.
-  u4v erh[KQ], erl[KQ], eah[KQ], eal[KQ];
+  // range guard: 2^-e_l scales linear layer l's inputs (dn), 2^e_l its accumulator (up); gm =
+  // this lane's largest scaled input of the layer being checked; fail = a layer overflowed in
+  // this pass (later layers are NaN: only the first one is rescaled per pass)
+  auto ex = [&](int l) -> int { return GUARD ? __builtin_amdgcn_readlane(E.gexp, l) : 0; };
+  // 2^-e / 2^e from the exponent bits (scalar ALU: e is wave-uniform, |e| <= 100)
+  auto dn = [&](int l) -> float { return GUARD ? __int_as_float((127 - ex(l)) << 23) : 1.f; };
+  auto up = [&](int l) -> float { return GUARD ? __int_as_float((127 + ex(l)) << 23) : 1.f; };
+  float gm = 0.f;
+  bool fail = false;
+  auto note = [&](float a) { if (GUARD) gm = fmaxf(gm, fabsf(a)); };
+  auto guard = [&](int l) {
+    if constexpr (GUARD) {
+      // first overflowing layer of the pass: its inputs' scale 2^-e_l drops by 2^-12 (a wave
+      // max reduction here costs the fast variant registers); inputs up to 2^27 then fit, a
+      // larger range takes another pass.  e_l stops at 100 (an f32 overflow, +-inf activations,
+      // is the reference's too: nothing to rescale), so every retry loop ends.
+      // branch-free (selects on wave-uniform conditions)
+      const bool over = wave_any(gm >= 65504.f) && !fail;
+      const bool raise = over && __builtin_amdgcn_readlane(E.gexp, l) < 100;
+      E.gexp += (raise && E.lane == l) ? 12 : 0;
+      E.changed = E.changed || raise;
+      fail = fail || over;
+      gm = 0.f;
+    }
+  };
+  // values r (and, TAN, tangents tr) of the encoding pair q of k-step v of this lane
+  auto enc_vals = [&](int v, int q, float (&r)[2], float (&tr)[2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int slot = 32 * v + 8 * g + 2 * q + t;
+      float val = 0.f, tv = 0.f;
+      if (slot < 2 * F) {
+        const float4 b = E.lbasis[slot >> 1];
+        float pr = x0 * b.x;
+        pr = fmaf(x1, b.y, pr);
+        pr = fmaf(x2, b.z, pr);
+        float sn, cs;
+        sincosf(pr, &sn, &cs);
+        val = t ? cs : sn;
+        if (TAN) {
+          const float bk = comp == 1 ? b.x : comp == 2 ? b.y : b.z;
+          tv = t ? -sn * bk : cs * bk;
+        }
+      } else if (slot == 2 * F) {
+        val = x0;
+        tv = comp == 1 ? 1.f : 0.f;
+      } else if (slot == 2 * F + 1) {
+        val = x1;
+        tv = comp == 2 ? 1.f : 0.f;
+      } else if (slot == 2 * F + 2) {
+        val = x2;
+        tv = comp == 3 ? 1.f : 0.f;
+      }
+      r[t] = val;
+      tr[t] = tv;
+    }
+  };
+  // act(enc) (skip-layer inputs) of pair q of k-step v, times d: value columns act_enc(r),
+  // tangent columns its tangent
+  auto enc_act = [&](int v, int q, float d, uint32_t& hi, uint32_t& lo) {
+    float r[2], tr[2];
+    enc_vals(v, q, r, tr);
+    float a0, a1;
+    if (TAN && !value) {
+      a0 = act_enc_tan<ACT>(r[0], tr[0]); a1 = act_enc_tan<ACT>(r[1], tr[1]);
+    } else {
+      a0 = act_enc<ACT>(r[0]); a1 = act_enc<ACT>(r[1]);
+    }
+    if (GUARD) {
+      a0 *= d; a1 *= d;
+      note(a0); note(a1);
+    }
+    split2(a0, a1, hi, lo);
+  };
+  // the raw encoding (init-layer inputs) and, unguarded, act(enc) for the skip layers (the
+  // guarded variant recomputes act(enc) per skip layer at that layer's scale instead of holding
+  // it: fewer live registers on the rare path)
+  u4v erh[KQ], erl[KQ], eah[GUARD ? 1 : KQ], eal[GUARD ? 1 : KQ];
 #pragma unroll
   for (int v = 0; v < KQ; ++v) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       float r[2], tr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int slot = 32 * v + 8 * g + 2 * q + t;
-        float val = 0.f, tv = 0.f;
-        if (slot < 2 * F) {
-          const float4 b = E.lbasis[slot >> 1];
-          float pr = x0 * b.x;
-          pr = fmaf(x1, b.y, pr);
-          pr = fmaf(x2, b.z, pr);
-          float sn, cs;
-          sincosf(pr, &sn, &cs);
-          val = t ? cs : sn;
-          if (TAN) {
-            const float bk = comp == 1 ? b.x : comp == 2 ? b.y : b.z;
-            tv = t ? -sn * bk : cs * bk;
-          }
-        } else if (slot == 2 * F) {
-          val = x0;
-          tv = comp == 1 ? 1.f : 0.f;
-        } else if (slot == 2 * F + 1) {
-          val = x1;
-          tv = comp == 2 ? 1.f : 0.f;
-        } else if (slot == 2 * F + 2) {
-          val = x2;
-          tv = comp == 3 ? 1.f : 0.f;
-        }
-        r[t] = val;
-        tr[t] = tv;
+      enc_vals(v, q, r, tr);
+      float e0 = (TAN && !value) ? tr[0] : r[0], e1 = (TAN && !value) ? tr[1] : r[1];
+      if (GUARD) {
+        const float d0 = dn(0);
+        e0 *= d0; e1 *= d0;
+        note(e0); note(e1);
       }
       uint32_t hi, lo;
-      if (TAN && !value) {
-        split2(tr[0], tr[1], hi, lo);
-        erh[v][q] = hi; erl[v][q] = lo;
-        split2(act_enc_tan<ACT>(r[0], tr[0]), act_enc_tan<ACT>(r[1], tr[1]), hi, lo);
-        eah[v][q] = hi; eal[v][q] = lo;
-      } else {
-        split2(r[0], r[1], hi, lo);
-        erh[v][q] = hi; erl[v][q] = lo;
-        split2(act_enc<ACT>(r[0]), act_enc<ACT>(r[1]), hi, lo);
+      split2(e0, e1, hi, lo);
+      erh[v][q] = hi; erl[v][q] = lo;
+      if constexpr (!GUARD) {
+        enc_act(v, q, 1.f, hi, lo);
         eah[v][q] = hi; eal[v][q] = lo;
       }
     }
@@ -318,12 +401,18 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   // sub-block 2 ib for q < 2, of sub-block 2 ib + 1 after).  The empty asm pins each result inside
   // the chunk that computes it (dst is read only by the next layer).
   auto retire2 = [&](int layer, int ib, int q) {
-    const float sc = m.scale3[layer];
+    const float sc = GUARD ? m.scale3[layer] * up(layer) : m.scale3[layer];
     const float z0 = (q < 2 ? pend0[2 * q] : pend1[2 * q - 4]) * sc;
     const float z1 = (q < 2 ? pend0[2 * q + 1] : pend1[2 * q - 3]) * sc;
     uint32_t hi, lo;
-    if (TAN) split2(act_tan<ACT>(z0, value), act_tan<ACT>(z1, value), hi, lo);
-    else split2(act<ACT>(z0), act<ACT>(z1), hi, lo);
+    float a0 = TAN ? act_tan<ACT>(z0, value) : act<ACT>(z0);
+    float a1 = TAN ? act_tan<ACT>(z1, value) : act<ACT>(z1);
+    if (GUARD) {
+      const float d = dn(layer + 1);
+      a0 *= d; a1 *= d;
+      note(a0); note(a1);
+    }
+    split2(a0, a1, hi, lo);
     asm volatile("" : "+v"(hi), "+v"(lo));
     dh[ib][q] = hi; dl[ib][q] = lo;
   };
@@ -331,19 +420,21 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
   auto bias = [&](int layer, int sb) {
     f4v b = E.bias_at(layer, sb);
     if (TAN) b *= bmask;
+    if (GUARD) b *= dn(layer);
     return b;
   };
   auto retire = [&](int layer, int ib) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) retire2(layer, ib, q);
   };
+  guard(0);
   // init layer (neural_blocks.py:80): raw encoding in
 #pragma unroll
   for (int ib = 0; ib < NC; ++ib) {
     const float4* A = E.begin(size_at(ib + AH));
     f4v a0 = bias(0, 2 * ib), a1 = bias(0, 2 * ib + 1);
     if (ib > 0) retire(0, ib - 1);
-    seg<KQ, 0>(A, erh, erl, a0, a1, [](int) {});
+    seg<KQ, 0, KQ, NoSide, !GUARD>(A, erh, erl, a0, a1, NoSide{});
     pend0 = a0; pend1 = a1;
     E.end();
   }
@@ -353,21 +444,40 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
 #pragma unroll
     for (int k = 0; k < KH; ++k) { sh[k] = dh[k]; sl[k] = dl[k]; }
     const bool skip = i != L - 1 && i % SK == 0;
-    const int nq = chunk_q(i);
+    u4v gah[GUARD ? KQ : 1], gal[GUARD ? KQ : 1];
+    if constexpr (GUARD) {
+      if (skip) {
+        const float d = dn(1 + i);
+#pragma unroll
+        for (int v = 0; v < KQ; ++v)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            uint32_t hi, lo;
+            enc_act(v, q, d, hi, lo);
+            gah[v][q] = hi; gal[v][q] = lo;
+          }
+      }
+    }
+    guard(1 + i);
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
       const float4* A = E.begin(size_at(NC + i * NC + ib + AH));
       f4v a0 = bias(1 + i, 2 * ib), a1 = bias(1 + i, 2 * ib + 1);
       // the previous chunk's four activation pairs, spread over the chunk's k-steps
-      seg<KH, 0>(A, sh, sl, a0, a1, [&](int u) {
+      auto side = [&](int u) {
         if (ib > 0 && (KH == 4 || (u & 1) == 0)) retire2(1 + i, ib - 1, KH == 4 ? u : u >> 1);
-      });
-      if (skip) seg<KQ, 4 * KH>(A, eah, eal, a0, a1, [](int) {});
+      };
+      seg<KH, 0, KH, decltype(side)&, !GUARD>(A, sh, sl, a0, a1, side);
+      if (skip) {
+        if constexpr (GUARD) seg<KQ, 4 * KH, KQ, NoSide, false>(A, gah, gal, a0, a1, NoSide{});
+        else seg<KQ, 4 * KH>(A, eah, eal, a0, a1, NoSide{});
+      }
       pend0 = a0; pend1 = a1;
       E.end();
     }
     retire(1 + i, NC - 1);
   }
+  guard(L + 1);
   // out layer (neural_blocks.py:86): one 16-row sub-block, pieces [k-step][hi, lo]; two chains
   // (even / odd k-steps); row 0 of ray j sits in register 0 of lane j
   const float4* A = E.begin(size_at(NCH - 1 + AH));
@@ -390,8 +500,26 @@ __device__ __forceinline__ float eval(Engine<KH, KQ, WV>& E, const MlpDev& m, fl
     }
   }
   E.end();
-  const float o = (o0[0] + o1[0]) * m.scale3[L + 1];
+  const float o = (o0[0] + o1[0]) * (GUARD ? m.scale3[L + 1] * up(L + 1) : m.scale3[L + 1]);
   return __shfl(o, E.lane & 15);
+}
+
+// After an evaluation of the wave (output v of this lane, `active` = the lane's result is used):
+// true if it must run again -- an unguarded evaluation whose output is not finite somewhere
+// switches the wave to the guarded variant; a guarded one repeats while it raised an exponent.
+// The result is wave-uniform.
+template <class Eng>
+__device__ __forceinline__ bool retry(Eng& E, bool active, float v) {
+  if (!__builtin_amdgcn_readfirstlane((int)E.guarded)) {
+    if (!wave_any(active && !__builtin_isfinite(v))) return false;
+    E.guarded = true;
+    E.gexp = 0;
+    E.changed = false;
+    return true;
+  }
+  const bool ch = __builtin_amdgcn_readfirstlane((int)E.changed) != 0;
+  E.changed = false;
+  return ch;
 }
 
 }  // namespace ring3

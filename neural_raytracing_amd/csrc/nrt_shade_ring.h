@@ -63,7 +63,8 @@ struct Engine {
   static constexpr int RING_BYTES = D * SLOTQ * 1024;
   static constexpr int kOutOfRange = 0x40000000;
   __host__ __device__ static size_t lds_bytes(const RProgDev& p) {
-    return RING_BYTES + (size_t)p.basis_q * 16 + (size_t)p.table_floats * 4;
+    return RING_BYTES + (size_t)p.basis_q * 16 + (size_t)p.table_floats * 4 +
+           (size_t)p.n_mlp * kMaxLin * 4;
   }
   const float4* ring;
   uint32_t ring_lds;
@@ -73,6 +74,11 @@ struct Engine {
   int sbytes;
   const NRT_CONST int* chunks;  // [2 n]: (KiB offset, KiB count)
   int nch, ahead, slot, lane, wv;
+  // fp32-split range guard (nrt_ring3.h), per block: lexp[mlp][l] = e_l of that MLP's linear
+  // layer l (LDS, zero at start); `guarded` (block-uniform) selects eval3<..., GUARD>;
+  // `changed` = this wave's last guarded evaluation raised an exponent
+  int* lexp;
+  bool guarded, changed;
 
   __device__ __forceinline__ void issue(int qoff, int nq, int s) {
     const int w = __builtin_amdgcn_readfirstlane(wv);
@@ -108,6 +114,10 @@ struct Engine {
     float* lt = reinterpret_cast<float*>(lds + RING_BYTES + (size_t)p.basis_q * 16);
     for (int i = threadIdx.x; i < p.table_floats; i += blockDim.x) lt[i] = p.tables[i];
     ltab = lt;
+    lexp = reinterpret_cast<int*>(lt + p.table_floats);
+    for (int i = threadIdx.x; i < p.n_mlp * kMaxLin; i += blockDim.x) lexp[i] = 0;
+    guarded = false;
+    changed = false;
     sbase = p.stream;
     sbytes = p.stream_bytes;
     chunks = (const NRT_CONST int*)p.chunks;
@@ -135,6 +145,22 @@ struct Engine {
   __device__ __forceinline__ void end() { slot = slot + 1 == D ? 0 : slot + 1; }
   // the DMA issued by the last begin() must land before the block's LDS is released
   __device__ __forceinline__ void drain() { __builtin_amdgcn_s_waitcnt(ring::waitcnt_vm_lgkm0(0)); }
+  // After a tile's split evaluations (ok = this lane's outputs are finite): true if the whole
+  // block runs them again -- the first non-finite output switches the block to the guarded
+  // variant, a guarded pass repeats while some wave raised an exponent.  Block-uniform (one
+  // barrier per tile).
+  __device__ __forceinline__ bool retry(bool ok) {
+    int want;
+    if (!guarded) {
+      want = wave_any(!ok) ? 1 : 0;
+    } else {
+      want = changed ? 1 : 0;
+      changed = false;
+    }
+    if (!__syncthreads_or(want)) return false;
+    guarded = true;
+    return true;
+  }
   // acc[reg] = bias[layer][16 sb + 4 g + reg] of MLP m
   __device__ __forceinline__ f4v bias_at(const RProgMlp& m, int layer, int sb) const {
     const float4 q = *reinterpret_cast<const float4*>(ltab + m.bias_off + layer * m.bstride + 16 * sb +
@@ -294,9 +320,11 @@ __device__ __forceinline__ f4v eval32(En& E, const RProgMlp& m, float x0, float 
 // fp32-split (f16 hi/lo halves, three f16 MFMA products, f32 accumulation)
 // ---------------------------------------------------------------------------------------------
 // k-outer encoding part: pieces [k-step][sub-block][hi, lo]
-template <class S, int ACT, class En>
+// (GUARD: every input times d, its magnitude noted for the range check)
+template <class S, int ACT, bool GUARD = false, class En, class Note>
 __device__ __forceinline__ void enc_part3(En& E, const RProgMlp& m, const float4* basis, bool actv,
-                                          float x0, float x1, float x2, f4v (&acc)[S::NSB]) {
+                                          float x0, float x1, float x2, f4v (&acc)[S::NSB],
+                                          float d, Note&& note) {
   const int g = E.lane >> 4;
 #pragma unroll 1
   for (int cc = 0; cc < S::CE3; ++cc) {
@@ -313,6 +341,10 @@ __device__ __forceinline__ void enc_part3(En& E, const RProgMlp& m, const float4
           float sn, cs;
           enc_pair(basis, m.F, 16 * v + 4 * g + q, x0, x1, x2, sn, cs);
           if (actv) { sn = ring3::act<ACT>(sn); cs = ring3::act<ACT>(cs); }
+          if (GUARD) {
+            sn *= d; cs *= d;
+            note(sn); note(cs);
+          }
           uint32_t hi, lo;
           ring3::split2(sn, cs, hi, lo);
           bh[q] = hi; bl[q] = lo;
@@ -332,8 +364,9 @@ __device__ __forceinline__ void enc_part3(En& E, const RProgMlp& m, const float4
   }
 }
 
-template <class S, int ACT, class En>
-__device__ __forceinline__ f4v eval3(En& E, const RProgMlp& m, float x0, float x1, float x2) {
+// GUARD: the range-guarded variant (nrt_ring3.h header), exponents lexp[mi][l] of this MLP
+template <class S, int ACT, bool GUARD = false, class En>
+__device__ __forceinline__ f4v eval3(En& E, const RProgMlp& m, int mi, float x0, float x1, float x2) {
   constexpr int NSB = S::NSB, NC = S::NC, KH = S::KH;
   const float4* basis = E.lbasis + m.basis_off;
   const float* scl = E.ltab + m.scale_off;  // 2^-s per layer
@@ -341,64 +374,101 @@ __device__ __forceinline__ f4v eval3(En& E, const RProgMlp& m, float x0, float x
   u4v sh[KH], sl[KH], dh[KH], dl[KH];
   f4v acc[NSB];
   f4v pend0, pend1;
+  // range guard: inputs of linear layer l scaled by dn(l) = 2^-e_l, its accumulator by up(l)
+  const int* lx = E.lexp + mi * kMaxLin;
+  auto ex = [&](int l) -> int { return GUARD ? __builtin_amdgcn_readfirstlane(lx[l]) : 0; };
+  auto dn = [&](int l) -> float { return GUARD ? __int_as_float((127 - ex(l)) << 23) : 1.f; };
+  auto up = [&](int l) -> float { return GUARD ? __int_as_float((127 + ex(l)) << 23) : 1.f; };
+  float gm = 0.f;
+  bool fail = false;
+  auto note = [&](float a) { if (GUARD) gm = fmaxf(gm, fabsf(a)); };
+  auto guard = [&](int l) {  // as ring3::eval's, the exponent raised in LDS for the block
+    if constexpr (GUARD) {
+      const bool over = wave_any(gm >= 65504.f) && !fail;
+      const int e = ex(l);
+      if (over && e < 100) {
+        if (E.lane == 0) atomicMax(E.lexp + mi * kMaxLin + l, e + 12);
+        E.changed = true;
+      }
+      fail = fail || over;
+      gm = 0.f;
+    }
+  };
   // activation pair q (< 4) of a chunk's accumulators into k-step ib of dst (B element pair 2q,
-  // 2q + 1 = registers 2q, 2q + 1 of sub-block 2 ib for q < 2, of sub-block 2 ib + 1 after)
-  auto retire2 = [&](float sc, int ib, int q) {
+  // 2q + 1 = registers 2q, 2q + 1 of sub-block 2 ib for q < 2, of sub-block 2 ib + 1 after);
+  // sc = the layer's scale (x up under GUARD), d = the next layer's input scale
+  auto retire2 = [&](float sc, float d, int ib, int q) {
     const float z0 = (q < 2 ? pend0[2 * (q & 1)] : pend1[2 * (q & 1)]) * sc;
     const float z1 = (q < 2 ? pend0[2 * (q & 1) + 1] : pend1[2 * (q & 1) + 1]) * sc;
+    float a0 = ring3::act<ACT>(z0), a1 = ring3::act<ACT>(z1);
+    if (GUARD) {
+      a0 *= d; a1 *= d;
+      note(a0); note(a1);
+    }
     uint32_t hi, lo;
-    ring3::split2(ring3::act<ACT>(z0), ring3::act<ACT>(z1), hi, lo);
+    ring3::split2(a0, a1, hi, lo);
     asm volatile("" : "+v"(hi), "+v"(lo));
     dh[ib][q] = hi; dl[ib][q] = lo;
   };
-  auto act_all = [&](float sc) {
+  auto act_all = [&](float sc, float d) {
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
       pend0 = acc[2 * ib]; pend1 = acc[2 * ib + 1];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) retire2(sc, ib, q);
+      for (int q = 0; q < 4; ++q) retire2(sc, d, ib, q);
     }
+  };
+  auto bias = [&](int layer, int sb) {
+    f4v b = E.bias_at(m, layer, sb);
+    if (GUARD) b *= dn(layer);
+    return b;
   };
   // init layer: the raw encoding, k-outer
 #pragma unroll
-  for (int sb = 0; sb < NSB; ++sb) acc[sb] = E.bias_at(m, 0, sb);
-  enc_part3<S, ACT>(E, m, basis, false, x0, x1, x2, acc);
-  act_all(scl[0]);
+  for (int sb = 0; sb < NSB; ++sb) acc[sb] = bias(0, sb);
+  enc_part3<S, ACT, GUARD>(E, m, basis, false, x0, x1, x2, acc, dn(0), note);
+  guard(0);
+  act_all(GUARD ? scl[0] * up(0) : scl[0], dn(1));
   // hidden part of layer i (as eval32: RAW keeps the accumulators for the encoding part)
-  auto hidden = [&](int i, float sc, auto raw_c) {
+  auto hidden = [&](int i, float sc, float d, auto raw_c) {
     constexpr bool RAW = decltype(raw_c)::value;
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
       const float4* A = E.begin();
-      f4v a0 = E.bias_at(m, 1 + i, 2 * ib), a1 = E.bias_at(m, 1 + i, 2 * ib + 1);
-      ring3::seg<KH, 0>(A, sh, sl, a0, a1, [&](int u) {
+      f4v a0 = bias(1 + i, 2 * ib), a1 = bias(1 + i, 2 * ib + 1);
+      auto side = [&](int u) {
         if (!RAW && ib > 0)
 #pragma unroll
-          for (int q = (u * 4) / KH; q < ((u + 1) * 4) / KH; ++q) retire2(sc, ib - 1, q);
-      });
+          for (int q = (u * 4) / KH; q < ((u + 1) * 4) / KH; ++q) retire2(sc, d, ib - 1, q);
+      };
+      ring3::seg<KH, 0, KH, decltype(side)&, !GUARD>(A, sh, sl, a0, a1, side);
       if (RAW) { acc[2 * ib] = a0; acc[2 * ib + 1] = a1; }
       else { pend0 = a0; pend1 = a1; }
       E.end();
     }
     if (!RAW)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) retire2(sc, NC - 1, q);
+      for (int q = 0; q < 4; ++q) retire2(sc, d, NC - 1, q);
   };
   for (int i = 0; i < L; ++i) {
 #pragma unroll
     for (int k = 0; k < KH; ++k) { sh[k] = dh[k]; sl[k] = dl[k]; }
-    const float sc = scl[1 + i];
+    const float sc = GUARD ? scl[1 + i] * up(1 + i) : scl[1 + i];
+    const float d = dn(2 + i);
     if (i != L - 1 && i % SK == 0) {
-      hidden(i, sc, std::true_type{});
-      enc_part3<S, ACT>(E, m, basis, true, x0, x1, x2, acc);
-      act_all(sc);
+      hidden(i, sc, d, std::true_type{});
+      enc_part3<S, ACT, GUARD>(E, m, basis, true, x0, x1, x2, acc, dn(1 + i), note);
+      guard(1 + i);
+      act_all(sc, d);
     } else {
-      hidden(i, sc, std::false_type{});
+      guard(1 + i);
+      hidden(i, sc, d, std::false_type{});
     }
   }
+  guard(L + 1);
   // out layer: pieces [k-step][hi, lo] of one sub-block; three chains (hi.hi, hi.lo, lo.hi)
   const float4* A = E.begin();
-  f4v o0 = E.bias_at(m, L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f}, o2 = o1;
+  f4v o0 = bias(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f}, o2 = o1;
   {
     float4 w0 = A[0], w1 = A[64];
 #pragma unroll
@@ -413,13 +483,23 @@ __device__ __forceinline__ f4v eval3(En& E, const RProgMlp& m, float x0, float x
     }
   }
   E.end();
-  return (o0 + (o1 + o2)) * scl[L + 1];
+  return (o0 + (o1 + o2)) * (GUARD ? scl[L + 1] * up(L + 1) : scl[L + 1]);
 }
 
+// MLP mi of the program; the split path takes the block's guarded variant once it is on
 template <int PREC, class S, int ACT, class En>
-__device__ __forceinline__ f4v eval(En& E, const RProgMlp& m, float x0, float x1, float x2) {
-  if constexpr (PREC == 2) return eval3<S, ACT>(E, m, x0, x1, x2);
-  else return eval32<S, ACT>(E, m, x0, x1, x2);
+__device__ __forceinline__ f4v eval(En& E, const RProgMlp& m, int mi, float x0, float x1, float x2) {
+  if constexpr (PREC == 2) {
+    if (__builtin_amdgcn_readfirstlane((int)E.guarded)) return eval3<S, ACT, true>(E, m, mi, x0, x1, x2);
+    return eval3<S, ACT>(E, m, mi, x0, x1, x2);
+  } else {
+    return eval32<S, ACT>(E, m, x0, x1, x2);
+  }
+}
+
+__device__ __forceinline__ bool finite4(const f4v& o) {
+  return __builtin_isfinite(o[0]) && __builtin_isfinite(o[1]) && __builtin_isfinite(o[2]) &&
+         __builtin_isfinite(o[3]);
 }
 
 // row q (< 16) of ray lane & 15 from an eval tile
@@ -449,7 +529,10 @@ __global__ void __launch_bounds__(64 * WV, 1) k_light_r(
     const bool valid = i < total;
     const int64_t idx = hit_idx[valid ? i : total - 1];
     const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
-    const f4v o = eval<PREC, LightShape, ACT_LEAKY>(E, prog.mlp[0], px, py, pz);
+    f4v o = eval<PREC, LightShape, ACT_LEAKY>(E, prog.mlp[0], 0, px, py, pz);
+    if constexpr (PREC == 2) {  // range guard (nrt_ring3.h)
+      while (E.retry(finite4(o))) o = eval<PREC, LightShape, ACT_LEAKY>(E, prog.mlp[0], 0, px, py, pz);
+    }
     float fr[9];
     make_frame(N_[idx * 3], N_[idx * 3 + 1], N_[idx * 3 + 2], fr);
     const float wix = WI[idx * 3], wiy = WI[idx * 3 + 1], wiz = WI[idx * 3 + 2];
@@ -490,11 +573,20 @@ __global__ void __launch_bounds__(64 * WV, 1) k_bsdf_r(
     const bool valid = i < total;
     const int64_t ii = valid ? i : total - 1;
     const int64_t idx = hit_idx[ii];
+    const float* ls = LS + ii * kLsStride;
+    const float le0 = ls[0], le1 = ls[1], le2 = ls[2];
+    const float ft0 = ls[3], ft1 = ls[4], ft2 = ls[5];
+    const float wo0 = ls[6], wo1 = ls[7], wo2 = ls[8];
     float K[16];
+    float f0, f1, f2;
+    // the tile's evaluations; the split path repeats them while the range guard asks
+    for (;;) {
+    bool ok = true;
     int k = 0;
     if (SPATIAL) {
       const float px = P_[idx * 3], py = P_[idx * 3 + 1], pz = P_[idx * 3 + 2];
-      const f4v o = eval<PREC, SpatialShape, ACT_LEAKY>(E, prog.mlp[0], px, py, pz);
+      const f4v o = eval<PREC, SpatialShape, ACT_LEAKY>(E, prog.mlp[0], 0, px, py, pz);
+      ok = ok && finite4(o);
       k = 1;
 #pragma unroll
       for (int q = 0; q < 16; ++q) K[q] = sigmoidf_(out_row(o, q, lane));
@@ -502,16 +594,13 @@ __global__ void __launch_bounds__(64 * WV, 1) k_bsdf_r(
 #pragma unroll
       for (int q = 0; q < 16; ++q) K[q] = 1.f;
     }
-    const float* ls = LS + ii * kLsStride;
-    const float le0 = ls[0], le1 = ls[1], le2 = ls[2];
-    const float ft0 = ls[3], ft1 = ls[4], ft2 = ls[5];
-    const float wo0 = ls[6], wo1 = ls[7], wo2 = ls[8];
-    float f0 = 0.f, f1 = 0.f, f2 = 0.f;
+    f0 = 0.f; f1 = 0.f; f2 = 0.f;
     for (int c = 0; c < nc; ++c) {
       const BsdfCompDev& cp = bs.comp[c];
       float v[3];
       if (cp.kind == 0) {
-        const f4v o = eval<PREC, BsdfShape, ACT_LEAKY>(E, prog.mlp[k], ft0, ft1, ft2);
+        const f4v o = eval<PREC, BsdfShape, ACT_LEAKY>(E, prog.mlp[k], k, ft0, ft1, ft2);
+        ok = ok && finite4(o);
         ++k;
 #pragma unroll
         for (int q = 0; q < 3; ++q) v[q] = act_fwd<false>(out_row(o, q, lane), cp.act);
@@ -533,6 +622,8 @@ __global__ void __launch_bounds__(64 * WV, 1) k_bsdf_r(
 #pragma unroll
       for (int q = 1; q < 16; ++q) kj = c == q ? K[q] : kj;
       f0 += v[0] * kj; f1 += v[1] * kj; f2 += v[2] * kj;
+    }
+    if (PREC != 2 || !E.retry(ok)) break;
     }
     if (valid && lane < 16) {
       // integrators.py:186-189: mis(=1) * bsdf_val * emitter_val, / emitter_samples(=1)
@@ -562,7 +653,11 @@ __global__ void __launch_bounds__(64 * WV, 1) k_mlp_ring(const RProgDev prog, co
     const int64_t i = b0 + 16 * E.wv + j;
     const bool valid = i < M;
     const int64_t ii = valid ? i : M - 1;
-    const f4v o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
+    f4v o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], 0, x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
+    if constexpr (PREC == 2) {  // range guard (nrt_ring3.h)
+      while (E.retry(finite4(o)))
+        o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], 0, x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
+    }
     if (valid)
 #pragma unroll
       for (int r = 0; r < 4; ++r)

@@ -190,7 +190,7 @@ def _per_camera(t, p):
 def light_sample(lights, it, active):
     """lights.sample_direction + sample_emitter_dir_wo_isect (scene.py:321-324)
     -> (d, Le, pdf, dist); dist is None for a LightField (lights.py:181-183)."""
-    from .lights.lights import LightField, PointLights
+    from .lights.lights import LightField, PointLights, RendererPointLights
     p = it.p
     if isinstance(lights, LightField):
         # lights.py:175-195
@@ -213,6 +213,15 @@ def light_sample(lights, it, active):
             lights.square.clamp(min=1e-6).to(p.device) * dist.square()
         color = _per_camera(lights.intensity, p)
         le = lights.scale.to(p.device) * F.normalize(color, dim=-1) / fall.clamp(min=1e-6)
+        pdf = torch.ones(p.shape[:-1], device=p.device)
+    elif isinstance(lights, RendererPointLights):
+        # renderer/lighting.py:285-304 (one light): d (loc - p) / (1e-7 + dist), scale I / (..)^2
+        lights.single()
+        d = lights.location.reshape(-1, 3)[0].to(p.device) - p
+        dist = (d * d).sum(dim=-1, keepdim=True).sqrt()
+        inv = (1e-7 + dist).reciprocal()
+        d = d * inv
+        le = lights.scale * lights.intensity.reshape(-1, 3)[0].to(p.device) * inv * inv
         pdf = torch.ones(p.shape[:-1], device=p.device)
     else:
         raise _lib.NrtError(f"light {type(lights).__name__} has no HIP training path")

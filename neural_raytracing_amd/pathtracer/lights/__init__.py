@@ -1,1 +1,2 @@
-from .lights import Constant, Light, LightField, PointLights  # noqa: F401
+from .lights import (Constant, Light, LightField, PointLights,  # noqa: F401
+                     RendererPointLights)

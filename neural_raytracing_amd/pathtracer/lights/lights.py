@@ -110,6 +110,83 @@ class PointLights(Light):
         return self.scale * F.normalize(self.intensity, dim=-1) / spectrum.clamp(min=1e-6)
 
 
+class RendererPointLights(Light):
+    """``pytorch3d.renderer.PointLights`` of the reference's PyTorch3D fork (renderer/lighting.py:
+    221-304) as a pathtracer light -- the light of utils.sphere_examples / sphere_render_bsdf
+    (utils.py:389-431): intensity = ambient_color, sample_direction gives d = (loc - p) inv and
+    Le = scale * intensity * inv^2 with inv = 1 / (1e-7 + |loc - p|) (no normalised intensity,
+    no constant / linear terms: not the pathtracer's PointLights).  The mesh shader's diffuse /
+    specular terms belong to the rasteriser (out of scope).  One light (the reference broadcasts
+    a [N, 3] location against the ray bundle axis, so only N = 1 is meaningful there)."""
+
+    def __init__(self, ambient_color=((0.5, 0.5, 0.5),), diffuse_color=((0.3, 0.3, 0.3),),
+                 specular_color=((0.2, 0.2, 0.2),), location=((0, 1, 0),), device="cpu",
+                 scale=1e-2):
+        super().__init__()
+        self.device = torch.device(device)
+
+        def t(v):
+            v = v.to(self.device) if isinstance(v, torch.Tensor) else \
+                torch.tensor(v, device=self.device, dtype=torch.float)
+            return v.reshape(-1, 3) if v.dim() < 2 else v
+        self.ambient_color = t(ambient_color)
+        self.diffuse_color = t(diffuse_color)
+        self.specular_color = t(specular_color)
+        self.location = t(location)
+        if self.location.shape[-1] != 3:
+            raise ValueError(f"Expected location to have shape (N, 3); got {tuple(self.location.shape)}")
+        self.intensity = torch.tensor(ambient_color, device=self.device) \
+            if not isinstance(ambient_color, torch.Tensor) else ambient_color.to(self.device)
+        self.scale = scale
+
+    def per_camera(self):
+        return None
+
+    def single(self):
+        if self.location.reshape(-1, 3).shape[0] != 1 or self.intensity.reshape(-1, 3).shape[0] != 1:
+            raise _lib.NrtError("pytorch3d.renderer.PointLights on the pathtracer path: one "
+                                "location and one ambient colour")
+        return self
+
+    def sample_towards(self, points):
+        return F.normalize(self.location - points, dim=-1)
+
+    def sample_direction(self, it, sampler=None, active=True):
+        """renderer/lighting.py:285-304 (torch; the HIP kernels do the same in-kernel)."""
+        ds = DirectionSample()
+        ds.p = self.location
+        ds.n = 0
+        ds.uv = 0
+        ds.obj = self
+        ds.delta = torch.tensor(True, device=self.device)
+        ds.d = ds.p - it.p
+        ds.dist = (ds.d * ds.d).sum(dim=-1, keepdim=True).sqrt()
+        inv_dist = (1e-7 + ds.dist).reciprocal()
+        ds.d = ds.d * inv_dist
+        spectrum = self.scale * self.intensity * inv_dist * inv_dist
+        return ds, spectrum
+
+    def nrt(self):
+        self.single()
+        loc = _host(self.location.reshape(-1, 3)[0])
+        inten = _host(self.intensity.reshape(-1, 3)[0].float())
+        out = ctypes.c_void_p()
+        _lib.check(_lib.load().nrt_light_create_renderer_point(
+            loc.data_ptr(), inten.data_ptr(), float(self.scale), ctypes.byref(out)),
+            "nrt_light_create_renderer_point")
+        h = _Handle(out, "nrt_light_destroy")
+        object.__setattr__(self, "_nrt_light", h)
+        return h.value
+
+    def diffuse(self, normals, points):
+        raise NotImplementedError("PointLights.diffuse belongs to the mesh shader (pytorch3d._C "
+                                  "rasteriser, out of scope)")
+
+    def specular(self, normals, points, camera_position, shininess):
+        raise NotImplementedError("PointLights.specular belongs to the mesh shader (pytorch3d._C "
+                                  "rasteriser, out of scope)")
+
+
 class LightField(nn.Module):
     """Learned light f(p) -> direction * magnitude, colour sigmoid(c) (lights.py:155-195)."""
 

@@ -10,7 +10,7 @@ import torch
 
 from .differentiable import needs_grad
 from .render import fused_integrator, render_tiles
-from .shapes.sdfs import SPHERE_SDF, is_hip_sdf
+from .shapes.sdfs import is_hip_sdf
 from .samplers import Sampler
 
 
@@ -78,8 +78,10 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     fused = _fused(integrator, cameras, w_isect, addition) if trim == 0 else None
     if needs_grad(shapes, bsdf, lights):
         fused = None  # training: integrator.sample carries the gradients
-    if not is_hip_sdf(getattr(shapes, "sdf", SPHERE_SDF)):
-        fused = None  # an SDF callable: SDF.intersect evaluates it between the HIP march steps
+    if not hasattr(shapes, "sdf") or not is_hip_sdf(shapes.sdf):
+        # an SDF callable (SDF.intersect evaluates it between the HIP march steps) or another
+        # shape (the analytic Sphere): integrator.sample on its own intersect, tile by tile
+        fused = None
     if getattr(lights, "per_camera", lambda: None)() is not None:
         fused = None  # one light per camera: Direct.sample shades camera by camera
     if fused is not None:

@@ -149,22 +149,38 @@ def heightmap(warp, size=256, device="cuda"):
     return warp.pdf(torch.stack([u, v], dim=-1))
 
 
-def sphere_examples(bsdf, device="cuda", size=256, chunk_size=128, scale=100):
-    """utils.py:409-431 renders each component of a ComposeSpatialVarying on an analytic unit
-    Sphere (shapes/shapes.py:31-97) lit by pytorch3d.renderer.PointLights -- a mesh-renderer class
-    with no sample_direction and no ``scale`` argument, so the reference call fails as written.
-    Here: the same camera (look_at_view_transform(dist=2, elev=0, azim=0)) and light
-    (location (0, 1, 4), scale) with the pathtracer's PointLights, Direct(), and the unit sphere
-    as SPHERE_SDF marched on the HIP path."""
-    from . import pathtrace
+def _sphere_scene(device, scale):
+    """utils.py:390-399 / 417-420: the unit Sphere at the origin, look_at_view_transform(dist=2,
+    elev=0, azim=0) through OpenGLPerspectiveCameras, the renderer's PointLights at (0, 1, 4)."""
     from .cameras import OpenGLPerspectiveCameras, look_at_view_transform
-    from .integrators import Direct
-    from .lights import PointLights
-    from .shapes import SDF, SPHERE_SDF
-    sphere = SDF(sdf=SPHERE_SDF, device=device)
+    from .lights import RendererPointLights
+    from .shapes import Sphere
+    sphere = Sphere([0, 0, 0], 1, device=device)
     R, T = look_at_view_transform(dist=2., elev=0, azim=0)
     cameras = OpenGLPerspectiveCameras(device=device, R=R, T=T)
-    lights = PointLights(device=device, location=[[0., 1., 4.]], scale=scale)
+    lights = RendererPointLights(device=device, location=[[0., 1., 4.]], scale=scale)
+    return sphere, cameras, lights
+
+
+def sphere_render_bsdf(bsdf, integrator=None, device="cuda", size=256, chunk_size=128, scale=100):
+    """utils.py:389-407: one BSDF on the analytic unit Sphere (Direct by default), on the HIP
+    path (nrt_sphere_intersect + the fused shading kernels)."""
+    from . import pathtrace
+    from .integrators import Direct
+    sphere, cameras, lights = _sphere_scene(device, scale)
+    if integrator is None:
+        integrator = Direct()
+    return pathtrace(sphere, cameras=cameras, lights=lights, chunk_size=chunk_size, size=size,
+                     bsdf=bsdf, integrator=integrator, device=device, silent=True)[0]
+
+
+def sphere_examples(bsdf, device="cuda", size=256, chunk_size=128, scale=100):
+    """utils.py:409-431: every component of a ComposeSpatialVarying rendered on the analytic unit
+    Sphere (shapes/shapes.py:31-97, HIP intersect) lit by the renderer's PointLights
+    (renderer/lighting.py:221-304) with Direct()."""
+    from . import pathtrace
+    from .integrators import Direct
+    sphere, cameras, lights = _sphere_scene(device, scale)
     out = []
     for basis in bsdf.bsdfs:
         out.append(pathtrace(sphere, cameras=cameras, lights=lights, chunk_size=chunk_size,

@@ -242,6 +242,69 @@ class MarchedSDF:
 
 
 # ---------------------------------------------------------------------------------------------
+# The analytic Sphere  (shapes/shapes.py:9-97)
+# ---------------------------------------------------------------------------------------------
+
+SPHERE_EPS = 1e-8  # shapes.py:9
+
+
+def quad_solve(a, b, c):
+    """shapes.py:11-18: roots [..., 2] of a t^2 + b t + c (sqrt only where the discriminant is
+    positive; elsewhere the discriminant itself stands in) and the validity mask."""
+    d = b * b - 4 * a * c
+    valid = d > 0
+    d[valid] = d[valid].sqrt()
+    s = torch.stack([d, -d], dim=-1)
+    return (-b[..., None] + s) / (2 * a[..., None]), valid
+
+
+class SphereRef:
+    """Sphere, shapes.py:31-97 (one sphere)."""
+
+    def __init__(self, center=(0.0, 0.0, 0.0), radius=1.0):
+        self.center = torch.tensor(list(center), dtype=torch.float)
+        self.radius = float(radius)
+        self.sqr_radius = self.radius * self.radius
+
+    def __len__(self):
+        return 1
+
+    def _roots(self, rays):
+        r_o, r_d = torch.split(rays, 3, dim=-1)
+        fs = r_o - self.center
+        a = torch.sum(r_d * r_d, dim=-1)
+        b = 2 * torch.sum(r_d * fs, dim=-1)
+        c = torch.sum(fs * fs, dim=-1) - self.sqr_radius
+        return r_o, r_d, quad_solve(a, b, c)
+
+    def intersect(self, rays, max_t=None, active=True, primary=True, jitter=None):
+        """shapes.py:47-69 (no scan, no throughput: a SurfaceInteraction)."""
+        r_o, r_d, (ts, mask) = self._roots(rays)
+        mask = mask & (ts >= SPHERE_EPS).any(-1)
+        ts[ts < SPHERE_EPS] = math.inf
+        t, _ = ts.min(dim=-1)
+        p = r_o + t[..., None] * r_d
+        n = F.normalize(p - self.center, dim=-1)
+        p = p + n * 1e-5
+        it = Interaction(p=p, t=t)
+        it.set_normals(n)
+        it.wi = it.to_local(-r_d)
+        return it, mask
+
+    def intersect_test(self, rays, max_t=None, active=True):
+        """shapes.py:70-77."""
+        _, _, (ts, mask) = self._roots(rays)
+        return mask & (ts >= SPHERE_EPS).any(-1)
+
+    def intersect_limits(self, rays, max_t=None, active=True):
+        """shapes.py:78-91."""
+        _, _, (ts, mask) = self._roots(rays)
+        mask = mask & (ts >= SPHERE_EPS).any(-1)
+        ts[ts < SPHERE_EPS] = math.inf
+        return ts.min(dim=-1)[0], ts.max(dim=-1)[0], mask
+
+
+# ---------------------------------------------------------------------------------------------
 # Interaction frames  (interaction.py:9-119)
 # ---------------------------------------------------------------------------------------------
 
@@ -503,6 +566,28 @@ class PointLightRef(nn.Module):
         color = self.intensity.reshape(shape)
         le = self.scale * F.normalize(color, dim=-1) / fall.clamp(min=1e-6)
         le = le.expand_as(it.p).clone() if le.shape != it.p.shape else le
+        le[~active] = 0
+        return LightSample(d, 1, dist), le
+
+
+class RendererPointLightRef(nn.Module):
+    """pytorch3d.renderer.PointLights of the reference's fork (renderer/lighting.py:221-304):
+    intensity = ambient_color, sample_direction d = (loc - p) inv, Le = scale I inv inv with
+    inv = 1 / (1e-7 + |loc - p|)."""
+
+    def __init__(self, ambient_color=((0.5, 0.5, 0.5),), location=((0.0, 1.0, 0.0),), scale=1e-2):
+        super().__init__()
+        self.location = torch.tensor(location, dtype=torch.float).reshape(-1, 3)
+        self.intensity = torch.tensor(ambient_color)
+        self.scale = scale
+
+    def sample_direction(self, it, active):
+        d = self.location - it.p
+        dist = (d * d).sum(dim=-1, keepdim=True).sqrt()
+        inv_dist = (1e-7 + dist).reciprocal()
+        d = d * inv_dist
+        spectrum = self.scale * self.intensity * inv_dist * inv_dist
+        le = spectrum.expand_as(it.p).clone() if spectrum.shape != it.p.shape else spectrum
         le[~active] = 0
         return LightSample(d, 1, dist), le
 

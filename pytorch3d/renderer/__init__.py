@@ -1,6 +1,7 @@
 """``pytorch3d.renderer`` for the pathtracer drivers: the camera math they use (host float32, the
 reference's op order; renderer/cameras.py:280-575, 1275-1422) and import-only stand-ins for the
-mesh-renderer classes they import (out of scope: the rasterisers need pytorch3d._C)."""
+mesh-renderer classes they import (out of scope: the rasterisers need pytorch3d._C).  PointLights
+is the fork's light with its pathtracer sample_direction (renderer/lighting.py:221-304)."""
 from neural_raytracing_amd.pathtracer.cameras import (FoVPerspectiveCameras,  # noqa: F401
                                                       OpenGLPerspectiveCameras, look_at_rotation,
                                                       look_at_view_transform)
@@ -35,6 +36,6 @@ class SoftPhongShader(_MeshRendererPart):
     pass
 
 
-class PointLights(_MeshRendererPart):
-    """The mesh shader's lights (renderer/lighting.py); the pathtracer's point light is
-    pytorch3d.pathtracer.lights.PointLights."""
+# the fork's PointLights (renderer/lighting.py:221-304) with its sample_direction: the light the
+# pathtracer's sphere_examples / sphere_render_bsdf use
+from neural_raytracing_amd.pathtracer.lights import RendererPointLights as PointLights  # noqa: E402,F401

@@ -228,7 +228,7 @@ def _dtu_oracle(sc):
                 integrator=R.NeRFIntegratorRef(R.DirectRef()))
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
 def test_dtu_like_render_matches_oracle(prec):
     """cfg4 (dtu.py:91-113 with a synthetic DTU pinhole): DTUCamera (fx = fy = 2890, cx = 800,
     cy = 600 on the 1600x1200 sensor) + 8x256 MLP SDF + ComposeSpatialVarying([NeuralBSDF(
@@ -261,7 +261,7 @@ def test_dtu_like_render_matches_oracle(prec):
            step_flips=steps, maxabs_agreeing=err[agree].max().item(),
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.9, rh.float().mean()
-    if prec == "fp32":
+    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar
         assert int((~agree).sum()) <= 0.005 * crop * crop
         assert err[agree].max().item() <= 1e-4
     else:
@@ -470,7 +470,8 @@ def test_point_light_per_camera_matches_oracle(mode):
     err = (got - want).abs().amax(-1)
     report(f"point_light_per_camera[{mode}]", pixels=err.numel(),
            over_1e4=int((err > 1e-4).sum()), maxabs=err.max().item())
-    assert (err <= 1e-4).float().mean() >= 0.995
+    # no march flips on this scene (reported 0 since round 3): every pixel at the FP32 bar
+    assert int((err > 1e-4).sum()) == 0, int((err > 1e-4).sum())
     # the second camera is lit by its own light: rendering it with the first light differs
     random.seed(17)
     with torch.no_grad():

@@ -551,7 +551,7 @@ def _shadow_scene():
     return oracle, prod
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
 def test_direct_shadow_rays_match_oracle(prec):
     """Direct with w_isect=True (sample_emitter_dir_w_isect, scene.py:290-298 + intersect_test,
     sdfs.py:162-181): HIP shadow march + masked shading vs the oracle.  FP32 within 1e-4 except
@@ -580,8 +580,11 @@ def test_direct_shadow_rays_match_oracle(prec):
     got = got.cpu()
     want = imgs[True]
     assert got.shape == want.shape
-    if prec == "fp32":
-        close = (got - want).abs().amax(-1) <= 1e-4
+    err = (got - want).abs().amax(-1)
+    report(f"direct_shadow_rays[{prec}]", pixels=err.numel(), shadowed=int(shadowed.sum()),
+           over_1e4=int((err > 1e-4).sum()), maxabs=err.max().item())
+    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar (flips at a shadow boundary aside)
+        close = err <= 1e-4
         assert close.float().mean() >= 0.995, (got - want).abs().max()
     else:
         mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
@@ -728,7 +731,7 @@ def _colocate_pair():
     return ref, mine
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
 def test_colocate_fov_render_matches_oracle(prec):
     """Full-frame pathtrace of the colocate-like scene (FoV camera, point light, 4-component
     spatially varying BSDF incl. Diffuse and Conductor) on the fused tile path vs the oracle."""
@@ -761,9 +764,9 @@ def test_colocate_fov_render_matches_oracle(prec):
     report(f"colocate_fov_render[{prec}]", pixels=err.numel(), hits=int(rh.sum()), flips=flips,
            step_flips=steps, over_1e4=int((err > 1e-4).sum()),
            over_1e4_on_agreeing=int((err[agree] > 1e-4).sum()), maxabs=err.max().item())
-    if prec == "fp32":
-        close = err <= 1e-4
-        assert close.float().mean() >= 0.995, (got - want).abs().max()
+    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar on every ray whose march agrees
+        assert int((~agree).sum()) <= 0.005 * err.numel()
+        assert int((err[agree] > 1e-4).sum()) == 0, err[agree].max()
     else:
         mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
         assert -10 * math.log10(max(mse, 1e-12)) > 40
@@ -930,7 +933,8 @@ def _path_pair(seed=31):
 
 
 @pytest.mark.parametrize("prec,w_isect", [("fp32", False), ("fp32", True), ("fp16", True),
-                                          ("fp32", "occ")])
+                                          ("fp32", "occ"), ("fp32-split", False),
+                                          ("fp32-split", True)])
 def test_path_integrator_matches_oracle(prec, w_isect):
     """Path (integrators.py:275-354), two bounces, with injected BSDF-sampling uniforms: the
     emitter term per bounce (optionally shadowed), ComposeSpatialVarying.sample, throughput
@@ -967,8 +971,8 @@ def test_path_integrator_matches_oracle(prec, w_isect):
     report(f"path_integrator[{prec},{w_isect}]", pixels=err.numel(), hits=int(wmask.sum()),
            over_1e4=int((err > 1e-4).sum()), over_1e2=int((err > 1e-2).sum()),
            maxabs=err.max().item())
-    if prec == "fp32":
-        assert (err <= 1e-4).float().mean() >= 0.99, err.max()
+    if prec != "fp16":  # fp32 and fp32-split: no bounce flips on this scene (reported 0)
+        assert int((err > 1e-4).sum()) == 0, err.max()
     else:
         mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
         assert -10 * math.log10(max(mse, 1e-12)) > 30

@@ -222,3 +222,36 @@ def test_shaped_mlp_sdf_level_set():
         q = p + 1e-2 * F.normalize(torch.randn(512, 3, generator=g), dim=-1)
         lip = (m(q) - m(p)).abs().squeeze(-1) / (q - p).norm(dim=-1)
         assert lip.max().item() <= 1.0 + 1e-3, lip.max()
+
+
+def test_sphere_ref_known_answers():
+    """SphereRef (shapes/shapes.py:31-97): a ray from (0, 0, 2) down -z hits the unit sphere at
+    t = 1, p = (0, 0, 1 + 1e-5), n = +z, wi = +z in the frame; a ray from inside takes the far
+    root; a ray passing by misses (t from the unsquared discriminant: 6 here); t is in units of
+    the unnormalised direction; intersect_limits gives both roots."""
+    s = R.SphereRef()
+    rays = torch.tensor([[0, 0, 2., 0, 0, -1], [0, 0, 2., 0, 1, 0], [0, 0, 0., 1, 0, 0],
+                         [0, 3, 0, 0, -2, 0]])
+    it, m = s.intersect(rays)
+    assert m.tolist() == [True, False, True, True]
+    assert torch.allclose(it.t, torch.tensor([1.0, 6.0, 1.0, 1.0]))  # |d| = 2 on the last
+    assert torch.allclose(it.p[0], torch.tensor([0.0, 0.0, 1.0 + 1e-5]))
+    assert torch.allclose(it.n[0], torch.tensor([0.0, 0.0, 1.0]))
+    assert torch.allclose(it.wi[0], torch.tensor([0.0, 0.0, 1.0]), atol=1e-6)
+    lo, hi, m2 = s.intersect_limits(rays)
+    assert m2.tolist() == m.tolist()
+    assert torch.allclose(lo[[0, 3]], torch.tensor([1.0, 1.0])) and torch.allclose(hi[[0, 3]], torch.tensor([3.0, 2.0]))
+    assert math.isinf(hi[2].item())  # the root behind the origin
+    assert s.intersect_test(rays).tolist() == m.tolist()
+
+
+def test_renderer_point_light_ref_known_answer():
+    """RendererPointLightRef (renderer/lighting.py:283-304): d = (loc - p) / (1e-7 + dist),
+    Le = scale * ambient / (1e-7 + dist)^2."""
+    light = R.RendererPointLightRef(location=[[0.0, 1.0, 4.0]], scale=100)
+    it = R.Interaction(p=torch.tensor([[0.0, 0.0, 1.0]]))
+    ds, le = light.sample_direction(it, torch.tensor([True]))
+    dist = math.sqrt(10.0)
+    assert torch.allclose(ds.d, torch.tensor([[0.0, 1.0, 3.0]]) / (1e-7 + dist))
+    assert torch.allclose(le, torch.full((1, 3), 100 * 0.5 / (1e-7 + dist) ** 2))
+    assert torch.allclose(ds.dist, torch.tensor([[dist]]))
