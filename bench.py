@@ -60,9 +60,17 @@ def parse():
                          "BASELINE.json configs[2..4] as one-GPU workloads")
     ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
     ap.add_argument("--crop", type=int, default=80, help="--scene train: crop side")
+    ap.add_argument("--nrt-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="nrt_set_option before the run (include/nrt.h runtime options), e.g. "
+                         "xcd_lines=0 for an A/B of a schedule switch; repeatable")
     ap.add_argument("--torch-profile", default=None,
                     help="--scene train: write a torch.profiler op table of one step here")
     args = ap.parse_args()
+    if args.nrt_option:
+        from neural_raytracing_amd import _lib
+        for kv in args.nrt_option:
+            k, _, v = kv.partition("=")
+            _lib.set_option(k, int(v))
     import sys
     args.precision_set = any(a.startswith("--precision") for a in sys.argv[1:])
     if args.scene == "train":

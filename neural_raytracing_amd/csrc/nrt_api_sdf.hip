@@ -210,6 +210,7 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   ma.eps = a->epsilon;
   ma.max_t = a->max_t;
   ma.primary = a->primary;
+  ma.xcd_lines = (int)option(OPT_XCD_LINES);
   ma.step = a->scan_max_t / 128.0;
   ma.scan_idx = a->primary ? a->scan_index : nullptr;
   ma.evals = profile_eval_counter();

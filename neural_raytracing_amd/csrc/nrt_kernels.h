@@ -262,6 +262,8 @@ struct MarchArgs {
   // FP16 ring march: byte offset of an LDS copy of the SphereSDF table (0 = read it from the
   // constant cache); set by ring_march when the table fits beside the weight ring
   int lds_spheres = 0;
+  // ring marches: deal rays to waves by XCD lines (OwnedRays; option "xcd_lines")
+  int xcd_lines = 0;
 };
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
@@ -394,25 +396,57 @@ __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
   return ((uint64_t)b << 32) | (uint32_t)idx;
 }
 
-// Rays owned by wave w of nw: whole rounds of kRayChunk consecutive rays (chunk c of round f is
-// chunk f*nw + w of the image), then the remainder dealt one ray at a time (w, w + nw, ...), so
-// every wave owns the same number of rays to within one.  A chunk's rays, their ray records,
-// outputs and scan keys are contiguous and touched by one wave only (one XCD's L2 assembles
-// whole lines); a wave's ~10 chunks are spread over the image, so its mix of short (hit) and
-// long (miss) marches stays near the frame's.  kRayChunk = 1 is the plain strided deal.
+// Rays owned by wave w of nw (the strided deal, kRayChunk = 1: ray w, w + nw, ...): every wave
+// owns the same number of rays to within one and a sample of the whole image, so its mix of
+// short (hit) and long (miss) marches stays near the frame's.  With kRayChunk > 1, whole rounds
+// of kRayChunk consecutive rays (measured 7 % slower: chunk-correlated march lengths unbalance
+// the waves).
+//
+// XCD lines (MarchArgs::xcd_lines): the same deal within each XCD.  The image is cut into lines
+// of kLineRays consecutive rays (128 B of t, a line of p / n / keys between them); line k belongs
+// to XCD group k % X, and a group's rays are dealt one at a time to the waves of its blocks
+// (workgroups are dispatched round-robin over the 8 XCDs: block b runs on XCD b % 8).  The 32
+// lane-scattered stores of a line then come from waves of one XCD and merge in its L2 instead of
+// reaching HBM as partial lines from up to 8 L2s; every wave still samples the whole image.
 #ifndef NRT_RAY_CHUNK
 #define NRT_RAY_CHUNK 1  // 32 measured 7 % slower (chunk-correlated march lengths unbalance the waves)
 #endif
 constexpr int64_t kRayChunk = NRT_RAY_CHUNK;
+constexpr int64_t kLineRays = 32;
+constexpr int kXcds = 8;  // MI355X: 8 XCDs, each with its own L2
 struct OwnedRays {
   int64_t nw, w, full, R;  // full = rays of this wave in whole chunk rounds
+  // XCD lines: group g of X, the group's rays Rg, its waves nwg, this wave's index v in it
+  bool lines = false;
+  int64_t X = 1, g = 0, Rg = 0, nwg = 1, v = 0;
   __device__ __forceinline__ OwnedRays(int64_t P, int64_t nw_, int64_t w_) : nw(nw_), w(w_) {
     const int64_t rounds = P / (nw * kRayChunk);
     full = rounds * kRayChunk;
     const int64_t rem = P - rounds * nw * kRayChunk;
     R = full + (w < rem ? (rem - 1 - w) / nw + 1 : 0);
   }
+  // wv waves per block; blocks = nw / wv
+  __device__ __forceinline__ OwnedRays(int64_t P, int64_t nw_, int64_t w_, int wv, bool xcd)
+      : OwnedRays(P, nw_, w_) {
+    if (!xcd) return;
+    lines = true;
+    const int64_t blocks = nw / wv, b = w / wv;
+    X = blocks < kXcds ? blocks : kXcds;
+    g = b % X;
+    const int64_t gb = (blocks - g + X - 1) / X;  // blocks of the group
+    nwg = gb * wv;
+    v = (b / X) * wv + (w % wv);
+    const int64_t NL = (P + kLineRays - 1) / kLineRays;  // lines
+    const int64_t ng = NL > g ? (NL - g + X - 1) / X : 0;  // lines of the group
+    Rg = ng * kLineRays;
+    if (ng > 0 && (NL - 1) % X == g) Rg -= NL * kLineRays - P;  // the short last line
+    R = v < Rg ? (Rg - 1 - v) / nwg + 1 : 0;
+  }
   __device__ __forceinline__ int64_t ray(int64_t k) const {
+    if (lines) {
+      const int64_t q = v + k * nwg;  // the group's q-th ray
+      return (g + X * (q / kLineRays)) * kLineRays + (q % kLineRays);
+    }
     if (k < full) return ((k / kRayChunk) * nw + w) * kRayChunk + (k % kRayChunk);
     return (full * nw) + w + (k - full) * nw;
   }
@@ -512,7 +546,7 @@ __device__ __forceinline__ void march_body(
   const int lane = lane_id(), r = lane & (RPW - 1);
   const int64_t nw = (int64_t)gridDim.x * WV;
   const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const OwnedRays own(P, nw, w);
+  const OwnedRays own(P, nw, w, WV, a.xcd_lines != 0);
   const int64_t R = own.R;  // rays owned by this wave
   const bool scan = mode == 0 && a.primary;
   // scan jobs: the whole 129-point scan of each of the first R - T rays (one plain key store),

@@ -26,6 +26,7 @@ enum Option {
   OPT_MAX_WAVES,       // "max_waves"
   OPT_SHADE_RING,      // "shade_ring"
   OPT_NORMALS_RING,    // "normals_ring"
+  OPT_XCD_LINES,       // "xcd_lines"
   OPT_COUNT
 };
 int64_t option(Option o);

@@ -385,6 +385,11 @@ def path_sample(shapes, rays, bsdf, lights, max_depth, training, sampler, unifor
                       _lib.precision_code(), _lib.stream())
         if depth + 1 == max_depth or not bool(act.any()):
             break  # the reference's last spawn is never shaded (:309, :342)
+        # the sampled local direction carries no gradient in the reference either: NeuralBSDF /
+        # Diffuse sample wo from the cosine hemisphere at the sampler's uniforms (bsdfs.py:90-106,
+        # 625-633), independent of the geometry; the Conductor's reflect(it.wi) (:396) would, but
+        # Conductor.sample fails in the reference and nrt_path_bounce refuses it.  The world
+        # direction is rebuilt through the differentiable frame, as spawn_rays(from_local(wo)).
         with torch.no_grad():
             wo = curr.to_local(rays_out[:, 3:].reshape(*lead, 3))
         d = curr.from_local(wo.detach())

@@ -389,8 +389,13 @@ class SDF:
         n = torch.zeros(P, 3, device=dev)
         p = p0.clone()
         raw = None
-        graph = torch.is_grad_enabled()  # under no_grad the render keeps no graph of the normals
+        graph = False
         if bool(hit_b.any()):
+            # create_graph only when the normals can carry gradients: grad mode on and the
+            # callable's output depends on a parameter that requires one (a render with grad
+            # mode on over frozen weights -- edit_dtu.py's bend around a loaded SDF -- keeps
+            # first-order normals, which every HIP MLP supports)
+            graph = self._callable_needs_graph(p0[hit_b])
             raw = self._callable_normals(p0[hit_b], create_graph=graph)
             nh = F.normalize(raw, eps=1e-6, dim=-1)
             n = n.index_put((hit_b,), nh)
@@ -422,6 +427,15 @@ class SDF:
             si._nrt_train = True  # raw_normals keeps its graph (the eikonal term)
             si._nrt_raw_train = raw
         return si, hit_b.reshape(lead)
+
+    def _callable_needs_graph(self, p):
+        """True when grad mode is on and sdf(p) requires grad for points that do not: some
+        parameter the callable closes over takes gradients."""
+        if not torch.is_grad_enabled():
+            return False
+        with torch.enable_grad():
+            out = self.sdf(p.detach())
+        return torch.is_tensor(out) and out.requires_grad
 
     def _callable_normals(self, p, create_graph=True):
         """SDF.autograd_diff (sdfs.py:184-197) through the callable: create_graph, so the normal

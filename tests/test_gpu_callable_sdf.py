@@ -267,3 +267,23 @@ def test_callable_training_through_an_mlp_raises():
     rays = _rays(16, 6, eye=(0.0, 0.2, 1.1)).cuda()
     with pytest.raises(_lib.NrtError):
         SDF(sdf=f_mine, max_steps=32).intersect(rays)
+
+
+def test_callable_over_frozen_mlp_with_grad_mode_on():
+    """grad mode on but nothing the callable closes over takes gradients (a bend
+    around a loaded, frozen SDF): the normals need no graph, so the intersect runs and equals the
+    no_grad one (sdfs.py:184-197 differentiates any callable)."""
+    from neural_raytracing_amd.pathtracer.shapes import SDF
+    ref, mine = _blob(128, 128, 32, "softplus")
+    for q in mine.parameters():
+        q.requires_grad_(False)
+    f = bend(mine)
+    rays = _rays(20, 6, eye=(0.0, 0.2, 1.1)).cuda()
+    random.seed(3)
+    it, hit = SDF(sdf=f, max_steps=32).intersect(rays)
+    random.seed(3)
+    with torch.no_grad():
+        it0, hit0 = SDF(sdf=f, max_steps=32).intersect(rays)
+    assert torch.equal(hit, hit0) and bool(hit.any())
+    assert torch.equal(it.n, it0.n) and torch.equal(it.p, it0.p)
+    assert not it.n.requires_grad

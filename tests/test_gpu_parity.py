@@ -507,11 +507,11 @@ def test_ring_march_schedule_invariant(monkeypatch):
     rays = _scene_rays(3001, 12).cuda()
     set_precision("fp16")
     outs = []
-    for blocks in (None, "1", "5"):
-        if blocks is None:
-            _lib_opt("march_blocks", 0)
-        else:
-            _lib_opt("march_blocks", int(blocks))
+    # (blocks, xcd_lines): the default grid with both ray deals, and grids of 1, 5, 13 blocks
+    # (fewer XCD groups than XCDs, a group with one block more than another)
+    for blocks, xcd in ((0, 1), (0, 0), (1, 1), (5, 1), (13, 1), (5, 0)):
+        _lib_opt("march_blocks", blocks)
+        _lib_opt("xcd_lines", xcd)
         random.seed(2)
         with torch.no_grad():
             it, hit = SDF(sdf=mine, max_steps=64).intersect(rays, primary=True)

@@ -167,8 +167,9 @@ def test_ring32_independent_of_grid_size():
     _, mine = _blob(128, 128, 32, "softplus", seed=9)
     rays = _rays(24, 11, eye=(0.0, 0.2, 1.1))
     base, bh, _ = _march(mine, rays)
-    for blocks in ("1", "5"):
-        _lib_opt("march_blocks", int(blocks))
+    for blocks, xcd in ((1, 1), (5, 1), (13, 1), (0, 0), (5, 0)):
+        _lib_opt("march_blocks", blocks)
+        _lib_opt("xcd_lines", xcd)
         it, h, _ = _march(mine, rays)
         assert torch.equal(h, bh)
         assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)
