@@ -440,9 +440,9 @@ int nrt_profile_evals(uint64_t* evals);
  *                      k_light3 / k_bsdf3 (0: the per-wave k_shade_direct)
  *   "normals_ring"  1  after an FP32 / fp32-split ring march, normals by forward mode on the same
  *                      engine (k_normal32 / k_normal3; 0: the per-wave FP32 backward k_sdf_grad)
- *   "xcd_lines"     1  ring marches deal rays to waves XCD by XCD: each 32-ray line of the outputs
- *                      is stored by waves of one XCD, so it merges in one L2 (0: one strided deal
- *                      over all waves); results are bit-identical either way
+ *   "xcd_lines"     0  1: ring marches deal rays to waves XCD by XCD (each 32-ray line of the
+ *                      outputs stored by waves of one XCD); measured: more HBM write traffic
+ *                      than the plain strided deal (0), kept for A/B runs; bit-identical results
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
 int nrt_set_option(const char* name, int64_t value);

@@ -406,8 +406,11 @@ __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
 // of kLineRays consecutive rays (128 B of t, a line of p / n / keys between them); line k belongs
 // to XCD group k % X, and a group's rays are dealt one at a time to the waves of its blocks
 // (workgroups are dispatched round-robin over the 8 XCDs: block b runs on XCD b % 8).  The 32
-// lane-scattered stores of a line then come from waves of one XCD and merge in its L2 instead of
-// reaching HBM as partial lines from up to 8 L2s; every wave still samples the whole image.
+// lane-scattered stores of a line then come from waves of one XCD and could merge in its L2 instead
+// of reaching HBM as partial lines from up to 8 L2s.  Measured (PMC, 800^2 FP32 frame): HBM writes
+// 131 -> 158 MB per k_march32 launch -- worse, so off by default (the lines are written over the
+// whole launch and leave the L2 between stores anyway); the fix that works is fewer scattered
+// bytes (k_march_finish).
 #ifndef NRT_RAY_CHUNK
 #define NRT_RAY_CHUNK 1  // 32 measured 7 % slower (chunk-correlated march lengths unbalance the waves)
 #endif
@@ -572,13 +575,20 @@ __device__ __forceinline__ void march_body(
         // sdfs.py:119-131: a march ends on a hit, when t leaves [0, max_t) or after max_steps
         if (ended || !(t < a.max_t) || i >= a.max_steps) {
           if (lane < RPW) {
-            t_out[ray] = t;
-            hit_out[ray] = hit ? 1 : 0;
-            p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
-            p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
-            p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
-            n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
-            if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+            if (p_out) {
+              t_out[ray] = t;
+              hit_out[ray] = hit ? 1 : 0;
+              p_out[ray * 3] = __fadd_rn(ox, __fmul_rn(t, dx));
+              p_out[ray * 3 + 1] = __fadd_rn(oy, __fmul_rn(t, dy));
+              p_out[ray * 3 + 2] = __fadd_rn(oz, __fmul_rn(t, dz));
+              n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
+              if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+            } else {
+              // packed: t >= 0 always (it only grows by d > eps) and a hit's t is finite (a NaN t
+              // ends the march as a miss), so the hit flag rides in the sign bit; k_march_finish unpacks it and writes p / n / hit with coalesced stores
+              // (this lane-scattered 4-byte store is the march's only per-ray output)
+              t_out[ray] = hit ? -t : t;
+            }
           }
           kind = -1;
         }
@@ -795,6 +805,44 @@ __global__ void k_keys_index(const unsigned long long* __restrict__ keys, int64_
                              int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P) idx[i] = (int32_t)(uint32_t)keys[i];
+}
+
+// After a ring march that packed (hit, t) into t's sign bit (march_body with p_out == nullptr):
+// per ray, t = |t|, hit, p = o + t d (the march's rounding), n = raw_n = 0, and the hit list --
+// one coalesced pass instead of ~45 lane-scattered bytes per ray inside the march (the strided
+// ray deal writes every line of t / p / n in 4-byte pieces from many waves).
+template <int = 0>
+__global__ void k_march_finish(const float* __restrict__ rays, int64_t P, float* __restrict__ t_io,
+                               uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
+                               float* __restrict__ n_out, float* __restrict__ rawn_out,
+                               int32_t* __restrict__ idx, int32_t* __restrict__ cnt) {
+  const int lane = lane_id();
+  for (int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ray - lane < P;
+       ray += (int64_t)gridDim.x * blockDim.x) {
+    bool h = false;
+    if (ray < P) {
+      // a NaN t (an SDF value that went NaN mid-march) ended as a miss; its sign bit is noise
+      const float te = t_io[ray];
+      h = __builtin_signbit(te) != 0 && te == te;
+      const float t = fabsf(te);
+      const float* r = rays + ray * 6;
+      t_io[ray] = t;
+      hit_out[ray] = h ? 1 : 0;
+      p_out[ray * 3] = __fadd_rn(r[0], __fmul_rn(t, r[3]));
+      p_out[ray * 3 + 1] = __fadd_rn(r[1], __fmul_rn(t, r[4]));
+      p_out[ray * 3 + 2] = __fadd_rn(r[2], __fmul_rn(t, r[5]));
+      n_out[ray * 3] = 0.f; n_out[ray * 3 + 1] = 0.f; n_out[ray * 3 + 2] = 0.f;
+      if (rawn_out) { rawn_out[ray * 3] = 0.f; rawn_out[ray * 3 + 1] = 0.f; rawn_out[ray * 3 + 2] = 0.f; }
+    }
+    if (idx) {
+      const uint64_t mk = __ballot(h);
+      const int c = __popcll(mk);
+      int base = 0;
+      if (lane == 0 && c) base = atomicAdd(cnt, c);
+      base = __shfl(base, 0);
+      if (h) idx[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
+    }
+  }
 }
 
 // hit list of a finished march (order is irrelevant downstream): wave-aggregated appends

@@ -39,7 +39,7 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, a, t, hit, p, n, raw_n, thr, keys);
+          s->host_dev, s->mlp->host_dev, rays, P, a, t, hit, nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
@@ -49,9 +49,11 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
   if (rc) return rc;
   if (best32)
     if (int rc2 = ring_scan_best32(s, rays, P, ma, thr, keys, st)) return rc2;
-  if (idx) {
-    k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
-    if (int rc2 = check_launch("k_hit_list")) return rc2;
+  // the march packed (hit, t) into t: unpack, p / n / raw_n and the hit list, coalesced
+  {
+    k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
+        rays, P, t, hit, p, n, raw_n, idx, cnt);
+    if (int rc2 = check_launch("k_march_finish")) return rc2;
   }
   return NRT_OK;
 }

@@ -59,8 +59,9 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * WV)));
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, p, n,
-                                                     raw_n, thr, keys);
+      // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, nullptr,
+                                                     nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     if (int rc = launch(k_march3<KH, KQ, WV, ACT>, "k_march3")) return rc;
@@ -80,9 +81,10 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
   }
 #undef NRT_R3
   if (rc) return rc;
-  if (idx) {
-    k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
-    if (int rc2 = check_launch("k_hit_list")) return rc2;
+  {
+    k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
+        rays, P, t, hit, p, n, raw_n, idx, cnt);
+    if (int rc2 = check_launch("k_march_finish")) return rc2;
   }
   return NRT_OK;
 }

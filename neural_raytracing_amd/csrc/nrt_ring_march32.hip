@@ -28,8 +28,9 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * WV)));
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, p, n,
-                                                     raw_n, thr, keys);
+      // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, nullptr,
+                                                     nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     if (which == 0)
@@ -61,11 +62,10 @@ int ring_march32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
                  uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                  int32_t* cnt, unsigned long long* keys, hipStream_t st) {
   if (int rc = ring32_launch(s, rays, P, ma, t, hit, p, n, raw_n, thr, keys, st, 0)) return rc;
-  if (idx) {
-    k_hit_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 1024)), dim3(256), 0, st>>>(hit, P, idx, cnt);
-    if (int rc2 = check_launch("k_hit_list")) return rc2;
-  }
-  return NRT_OK;
+  // the march packed (hit, t) into t: unpack, p / n / raw_n and the hit list, coalesced
+  k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
+      rays, P, t, hit, p, n, raw_n, idx, cnt);
+  return check_launch("k_march_finish");
 }
 
 }  // namespace nrt

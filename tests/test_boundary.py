@@ -269,7 +269,7 @@ def test_runtime_options_roundtrip():
     defaults = {n: _lib.get_option(n) for n in names}
     assert defaults == {"ring16": 1, "ring32": 1, "normals16": 1, "scan_best32": 1,
                         "march_blocks": 0, "shade_program": 1, "nerf_fused": 1, "max_waves": 0,
-                        "shade_ring": 1, "normals_ring": 1, "xcd_lines": 1}
+                        "shade_ring": 1, "normals_ring": 1, "xcd_lines": 0}
     with _lib.options(march_blocks=5, ring32=0):
         assert _lib.get_option("march_blocks") == 5 and _lib.get_option("ring32") == 0
     assert _lib.get_option("march_blocks") == 0 and _lib.get_option("ring32") == 1
