@@ -667,22 +667,73 @@ __device__ __forceinline__ float sp2(float x) {
 // lanes of a ray (l, l + 32) sum exp(-k d_i) over the even / odd spheres from the LDS table and
 // add the halves (commutative: both lanes get the same bits) -- half the VALU of every lane
 // walking the whole table.  FP16-path math: fast exp, as spheres_value<true>.
-__device__ __forceinline__ float spheres_value_halves(const SdfDev& s, const float4* sp, int lane,
-                                                      float x, float y, float z) {
-  float acc = 0.f;
-  const float nk = -s.k;
-  for (int i = lane >> 5; i < s.n_spheres; i += 2) {
-    const float4 r0 = sp[4 * i], r1 = sp[4 * i + 1], r2 = sp[4 * i + 2];
-    const float r = sp[4 * i + 3].x;
-    // row-major (I+T): r0 = (m00 m01 m02 m10), r1 = (m11 m12 m20 m21), r2 = (m22 cx cy cz)
-    const float qx = fmaf(r0.z, z, fmaf(r0.y, y, r0.x * x)) - r2.y;
-    const float qy = fmaf(r1.y, z, fmaf(r1.x, y, r0.w * x)) - r2.z;
-    const float qz = fmaf(r2.x, z, fmaf(r1.w, y, r1.z * x)) - r2.w;
-    const float d = sqrtf(qx * qx + qy * qy + qz * qz) - r;
-    acc += __expf(nk * d);
+// The FP16 march's SphereSDF table in LDS as sphere PAIRS for packed-f32 VALU (v_pk_fma_f32 /
+// v_pk_mul_f32 handle two spheres per instruction): record 2 j + h holds spheres h + 4 j and
+// h + 4 j + 2 (the two lanes of a ray, h = lane >> 5, split the spheres by parity), as 13 float2
+// (m00 m01 m02 m10 m11 m12 m20 m21 m22 cx cy cz, c) + pad = 7 float4, where c = k log2(e) r puts
+// the radius into the exponent: exp(-k (|q| - r)) = exp2(-k log2(e) |q| + c).  A missing second
+// sphere has c = -inf (exp2 -> 0).
+constexpr int kSpherePairF4 = 7;
+__host__ __device__ inline int sphere_pair_records(int n) {
+  const int pairs = ((n + 1) / 2 + 1) / 2;  // pairs of the half with more spheres (h = 0)
+  return 2 * pairs;
+}
+__device__ __forceinline__ void build_sphere_pairs(const SdfDev& s, float4* out) {
+  const int n = s.n_spheres, R = sphere_pair_records(n);
+  const float kl = s.k * 1.4426950408889634f;
+  const float4* src = reinterpret_cast<const float4*>(s.spheres);
+  for (int rec = threadIdx.x; rec < R; rec += blockDim.x) {
+    const int h = rec & 1, j = rec >> 1;
+    float v[2][13];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = h + 4 * j + 2 * u;
+      if (i < n) {
+        const float4 r0 = src[4 * i], r1 = src[4 * i + 1], r2 = src[4 * i + 2], r3 = src[4 * i + 3];
+        const float m[13] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
+                             kl * r3.x};
+        for (int k = 0; k < 13; ++k) v[u][k] = m[k];
+      } else {
+        for (int k = 0; k < 12; ++k) v[u][k] = 0.f;
+        v[u][12] = -__builtin_inff();
+      }
+    }
+    float* o = reinterpret_cast<float*>(out + rec * kSpherePairF4);
+    for (int k = 0; k < 13; ++k) { o[2 * k] = v[0][k]; o[2 * k + 1] = v[1][k]; }
+    o[26] = 0.f; o[27] = 0.f;
   }
-  acc += __shfl_xor(acc, 32);
-  return -logf(fmaxf(acc, 1e-4f)) / s.k;
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+// FP16-path sphere smooth-min over the pair table (the FP16 march's SDF precision: fast v_sqrt,
+// fused arithmetic, pairwise sums -- ~10 VALU per sphere instead of ~30); the two lanes of a
+// ray sum their spheres and combine with one cross-half add
+__device__ __forceinline__ float spheres_value_pairs(const SdfDev& s, const float4* sp, int lane,
+                                                     float x, float y, float z) {
+  const int h = lane >> 5, R = sphere_pair_records(s.n_spheres);
+  const f2v xx = {x, x}, yy = {y, y}, zz = {z, z};
+  const float nkl = -s.k * 1.4426950408889634f;
+  const f2v nk2 = {nkl, nkl};
+  f2v acc = {0.f, 0.f};
+  for (int rec = h; rec < R; rec += 2) {
+    const float4* q = sp + rec * kSpherePairF4;
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5], g = q[6];
+    const f2v m00 = {a.x, a.y}, m01 = {a.z, a.w}, m02 = {b.x, b.y}, m10 = {b.z, b.w};
+    const f2v m11 = {c.x, c.y}, m12 = {c.z, c.w}, m20 = {d.x, d.y}, m21 = {d.z, d.w};
+    const f2v m22 = {e.x, e.y}, cx = {e.z, e.w}, cy = {f.x, f.y}, cz = {f.z, f.w};
+    const f2v cr = {g.x, g.y};
+    const f2v qx = __builtin_elementwise_fma(m02, zz, __builtin_elementwise_fma(m01, yy, __builtin_elementwise_fma(m00, xx, -cx)));
+    const f2v qy = __builtin_elementwise_fma(m12, zz, __builtin_elementwise_fma(m11, yy, __builtin_elementwise_fma(m10, xx, -cy)));
+    const f2v qz = __builtin_elementwise_fma(m22, zz, __builtin_elementwise_fma(m21, yy, __builtin_elementwise_fma(m20, xx, -cz)));
+    const f2v q2 = __builtin_elementwise_fma(qx, qx, __builtin_elementwise_fma(qy, qy, qz * qz));
+    const f2v len = {__builtin_amdgcn_sqrtf(q2.x), __builtin_amdgcn_sqrtf(q2.y)};
+    const f2v ex = __builtin_elementwise_fma(nk2, len, cr);
+    const f2v w = {__builtin_amdgcn_exp2f(ex.x), __builtin_amdgcn_exp2f(ex.y)};
+    acc += w;
+  }
+  float t = acc.x + acc.y;
+  t += __shfl_xor(t, 32);
+  return -logf(fmaxf(t, 1e-4f)) / s.k;
 }
 
 // Chunk schedule of one 8-layer (L hidden, skip period SK) evaluation, fixed at compile time:

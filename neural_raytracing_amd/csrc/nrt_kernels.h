@@ -468,8 +468,7 @@ struct RingPol16 {
     E.lspheres = nullptr;
     if (s.kind == 2 && a.lds_spheres > 0) {
       float4* ls = reinterpret_cast<float4*>(lds + a.lds_spheres);
-      for (int i = threadIdx.x; i < s.n_spheres * 4; i += blockDim.x)
-        ls[i] = reinterpret_cast<const float4*>(s.spheres)[i];
+      ring::build_sphere_pairs(s, ls);  // the pair layout of spheres_value_pairs
       __syncthreads();
       E.lspheres = ls;
     }
@@ -477,7 +476,7 @@ struct RingPol16 {
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     float d = 0.f;
     if (s.kind == 2)
-      d = E.lspheres ? ring::spheres_value_halves(s, E.lspheres, E.lane, x, y, z)
+      d = E.lspheres ? ring::spheres_value_pairs(s, E.lspheres, E.lane, x, y, z)
                      : spheres_value<true>(s, x, y, z);
     return d + ring::eval<NB, NE, WV, FOLD, 8, 3>(E, m, x, y, z);
   }

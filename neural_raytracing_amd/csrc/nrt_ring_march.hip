@@ -23,7 +23,9 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
     constexpr int kLdsSpheresMin = 8;
     const size_t base = ring::Cfg<NB, NE, kRingWaves>::lds_bytes(bias_bytes);
     const size_t ring_lds = (base + 15) & ~size_t(15);
-    const size_t sph = ring32_sphere_bytes(s);
+    const size_t sph = s->host_dev.kind == 2
+                           ? (size_t)ring::sphere_pair_records(s->host_dev.n_spheres) * ring::kSpherePairF4 * 16
+                           : 0;  // the pair table (ring::build_sphere_pairs)
     MarchArgs a = ma;
     a.lds_spheres = (sph > 0 && s->host_dev.n_spheres >= kLdsSpheresMin && ring_lds + sph <= (size_t)kLdsBytes &&
                      kLdsBytes / (ring_lds + sph) == kLdsBytes / base) ? (int)ring_lds : 0;
