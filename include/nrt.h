@@ -355,6 +355,22 @@ int nrt_composite(const float* rgb, const float* throughput, const uint8_t* hit,
                   float background, float* image, int32_t img_w, int32_t img_h,
                   int32_t channels, int32_t X0, int32_t Y0, void* stream);
 
+/* One fused pathtrace tile (main.py:63-90) of Direct / NeRFIntegrator(Direct) (integrators.py:
+ * 156-206, 243-257) in one call: nrt_raygen -> nrt_sdf_intersect (march, coarse scan when
+ * params->primary, normals) -> nrt_shade_direct -> nrt_composite into image[N, img_w, img_h,
+ * channels] at (X0, Y0).  noise: the camera's uniforms as nrt_raygen takes them (NULL: no
+ * jitter); with_alpha = 1 (NeRFIntegrator: channels 4, alpha = sigmoid(throughput), misses kept)
+ * or 0 (Direct: channels 3, misses = background).  workspace: nrt_render_tile_workspace_bytes
+ * bytes of device memory (every intermediate; nothing is allocated).  The same launches as the
+ * Python chain render.render_tile, so the results are bit-identical. */
+size_t nrt_render_tile_workspace_bytes(const nrt_sdf* sdf, int32_t N, int32_t W, int32_t H);
+int nrt_render_tile(const nrt_camera* host_cams, int32_t N, int32_t x0, int32_t y0, int32_t W,
+                    int32_t H, float with_noise, const float* noise, const nrt_sdf* sdf,
+                    const nrt_march_params* params, const nrt_bsdf* bsdf, const nrt_light* light,
+                    int32_t with_alpha, float background, float* image, int32_t img_w,
+                    int32_t img_h, int32_t channels, int32_t X0, int32_t Y0, void* workspace,
+                    void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * NeRFLE (shapes/nerf.py:153-214), driven by NeRFReproduce.sample (integrators.py:260-267):
  * for each ray and each depth ts[s] (the caller's linspace(0, 2 + random()*0.1, S)),

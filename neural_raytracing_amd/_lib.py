@@ -96,6 +96,10 @@ _SIGNATURES = {
     "nrt_path_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "nrt_path_bounce": (_I32, [_P, _P, _P, _I32, _P, _I32, _F, _P, _P, _P, _I64, _P, _P, _P, _P, _P,
                                _P, _P, _I32, _P]),
+    "nrt_render_tile_workspace_bytes": (ctypes.c_size_t, [_P, _I32, _I32, _I32]),
+    "nrt_render_tile": (_I32, [_P, _I32, _I32, _I32, _I32, _I32, _F, _P, _P,
+                               ctypes.POINTER(MarchParams), _P, _P, _I32, _F, _P, _I32, _I32, _I32,
+                               _I32, _I32, _P, _P]),
     "nrt_nerfle_workspace_bytes": (ctypes.c_size_t, [_I64, _I32, _I32]),
     "nrt_nerfle_workspace_bytes_for": (ctypes.c_size_t, [_P, _P, _I64, _I32, _I32, _I32]),
     "nrt_nerfle_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P, _I32, _P, _P, _I32, _P]),

@@ -162,3 +162,61 @@ def test_pathtrace_batched_tiles_with_jitter_match_oracle(prec):
     report(f"batched_tiles_vs_oracle[{prec}]", tiles=n_tiles, maxabs=err.max().item(),
            pixels_over_1e4=int((err.amax(-1) > 1e-4).sum()))
     assert err.max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("alpha", [True, False])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split"])
+def test_render_tile_entry_matches_python_chain(alpha, prec):
+    """nrt_render_tile (one C-ABI call per pathtrace tile: raygen, march + scan + normals,
+    Direct shading, composite) equals the Python launch chain render.render_tile bit for bit:
+    same camera jitter uniforms, same scan jitter draw (NeRFIntegrator(Direct): alpha channel;
+    Direct: background fill)."""
+    import ctypes
+    import random
+    import bench
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from neural_raytracing_amd.pathtracer.integrators.integrators import _bsdf_handle, _light_handle
+    from neural_raytracing_amd.pathtracer.render import fused_integrator, render_tile
+    from neural_raytracing_amd.pathtracer.shapes.sdfs import sdf_handle
+    nra.set_precision(prec)
+    try:
+        sc = bench.build_scene("cuda", 32, seed=2, light_gain=bench.LIGHT_GAIN)
+        pt = sc["pt"]
+        size, chunk, x0, y0 = 96, 32, 32, 16
+        focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+        cam = pt.cameras.NeRFCamera(cam_to_world=bench.view_c2w(0, 1)[None].cuda(), focal=focal)
+        integ = NeRFIntegrator(Direct()) if alpha else Direct()
+        C = 4 if alpha else 3
+        bg = 0.25
+        want = torch.full((1, size, size, C), bg, device="cuda")
+        got = want.clone()
+        torch.manual_seed(3)
+        random.seed(4)
+        with torch.no_grad():
+            render_tile(fused_integrator(integ), sc["shape"], sc["lights"], cam, sc["bsdf"], want,
+                        x0, y0, chunk, size, 1e-3, bg)
+        torch.manual_seed(3)
+        noise = torch.rand(2, chunk, chunk, device="cuda")
+        random.seed(4)
+        shapes = sc["shape"]
+        mp = _lib.MarchParams(int(shapes.max_steps), float(shapes.epsilon), 10.0, 1,
+                              float(shapes.dist + random.random() * (2 / 128)),
+                              _lib.precision_code())
+        sh = sdf_handle(shapes.sdf)
+        lib = _lib.load(require_device=True)
+        ws = torch.empty(lib.nrt_render_tile_workspace_bytes(sh, 1, chunk, chunk), dtype=torch.uint8,
+                         device="cuda")
+        arr = (_lib.Camera * 1)(*cam._structs(size))
+        with torch.no_grad():
+            _lib.call("nrt_render_tile", ctypes.cast(arr, ctypes.c_void_p), 1, x0, y0, chunk, chunk,
+                      1e-3, _lib.ptr(noise), sh, ctypes.byref(mp), _bsdf_handle(sc["bsdf"]),
+                      _light_handle(sc["lights"]), int(alpha), bg, _lib.ptr(got), size, size, C, x0,
+                      y0, _lib.ptr(ws), _lib.stream())
+        torch.cuda.synchronize()
+        tile = (slice(None), slice(x0, x0 + chunk), slice(y0, y0 + chunk))
+        assert torch.equal(got, want)
+        assert (want[tile] != bg).any() and (want[..., :3][tile] > 0).any()
+    finally:
+        nra.set_precision("fp32")
