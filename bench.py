@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--samples", type=int, default=None,
                     help="march steps per ray (max_steps) or NeRF depths per ray "
                          "(default 64; 256 for --scene nerfle, BASELINE cfg5)")
-    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32", "fp32-split"],
+    ap.add_argument("--precision", default="fp32", choices=["fp16", "fp32", "fp32-split", "mixed"],
                     help="arithmetic of the headline frame (default fp32, the reference's; the "
                          "fp16 frame is reported as the `fp16` leg)")
     ap.add_argument("--tile-rows", type=int, default=10)
@@ -291,8 +291,8 @@ def main():
     rays_per_rank = len(rows) * size * world  # this rank's rows of every view
     rays_total = world * size * size * args.steps
     value = rays_total * args.samples / elapsed
-    roof = march_roofline(march_kernel, args.precision, rays_per_rank, args.samples, k_ms, k_n,
-                          evals, size)
+    roof = march_roofline(march_kernel, "fp16" if args.precision == "mixed" else args.precision,
+                          rays_per_rank, args.samples, k_ms, k_n, evals, size)
     roof["intersect_ms"] = i_ms / max(i_n, 1)
 
     extra = {}
@@ -304,6 +304,7 @@ def main():
             if args.precision == "fp32":
                 extra["fp32_split"] = split_leg(rr, args, rows, size)
                 extra["fp16"] = fp16_leg(rr, args, rows, size)
+                extra["mixed"] = fp16_leg(rr, args, rows, size, precision="mixed")
             extra.update(extra_legs(scene, cameras, size, args, rows))
             extra["api_paths"] = api_path_legs(scene, args)
         if not args.no_cpu_baseline:
@@ -344,7 +345,8 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-MARCH_KERNEL = {"fp16": "k_march16", "fp32": "k_march32", "fp32-split": "k_march3"}
+MARCH_KERNEL = {"fp16": "k_march16", "fp32": "k_march32", "fp32-split": "k_march3",
+                "mixed": "k_march16"}
 
 
 def march_roofline(kernel, precision, rays, samples, k_ms, k_n, evals, size):
@@ -429,18 +431,20 @@ def frame_accuracy(got, want, hit, rhit, t, rt):
     }
 
 
-def fp16_leg(rr, args, rows, size, steps=5, warmup=2):
+def fp16_leg(rr, args, rows, size, steps=5, warmup=2, precision="fp16"):
     """The same frame on the FP16 MFMA path (march k_march16 on the 2.5 PF FP16 peak; sdf(best)
-    FP32, option scan_best32), timed, and compared over the whole frame with the FP32 frame of
-    the same rays and weights."""
+    FP32, option scan_best32) -- or with precision "mixed" (include/nrt.h NRT_MIXED: the same
+    FP16 march + scan, the undecidable steps re-taken on the split engine by k_refine3, sdf(best)
+    over the top two by k_best3, split normals and shading) -- timed, and compared over the whole
+    frame with the FP32 frame of the same rays and weights."""
     import neural_raytracing_amd as nra
     from neural_raytracing_amd import _lib
+    names = ["k_march16", "k_intersect", "k_scan_best32", "k_refine3", "k_best3"]
     with torch.no_grad():
         want, rhit, rt = _frame_state(rr, 1234)
-        nra.set_precision("fp16")
+        nra.set_precision(precision)
         try:
-            el, ks, evals = _time_frames(rr.render, steps, warmup,
-                                         ["k_march16", "k_intersect", "k_scan_best32"])
+            el, ks, evals = _time_frames(rr.render, steps, warmup, names)
             got, hit, t = _frame_state(rr, 1234)
         finally:
             nra.set_precision(args.precision)
@@ -448,9 +452,14 @@ def fp16_leg(rr, args, rows, size, steps=5, warmup=2):
     roof = march_roofline("k_march16", "fp16", frame_rays, args.samples, *ks["k_march16"],
                           evals, size)
     roof["intersect_ms"] = ks["k_intersect"][0] / max(ks["k_intersect"][1], 1)
-    roof["scan_best32_ms"] = ks["k_scan_best32"][0] / max(ks["k_scan_best32"][1], 1)
+    for k in names[2:]:
+        if ks[k][1]:
+            roof[k + "_ms"] = ks[k][0] / ks[k][1]
+    if precision == "mixed":
+        roof["note"] = ("the evaluations counted include the split refinement's; the FP16 peak "
+                        "prices them all, so the fraction is a lower bound")
     return {"value": frame_rays * args.samples * steps / el, "unit": "ray-samples/s",
-            "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": "fp16",
+            "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": precision,
             "roofline": roof,
             "vs_fp32_full_frame": frame_accuracy(got.cpu(), want.cpu(), hit.cpu(), rhit.cpu(),
                                                  t.cpu(), rt.cpu())}

@@ -21,7 +21,11 @@
  *     NRT_FP32 except that the SDF march + coarse scan of the ring-engine SDFs runs every layer on
  *     v_mfma_f32_16x16x32_f16 with each f32 operand split into two f16 halves and three products
  *     (hi*hi + hi*lo + lo*hi, f32 accumulation): FP32 accuracy (22-bit operands, fewer
- *     accumulation roundings than an fma chain) at FP16 matrix-core throughput.
+ *     accumulation roundings than an fma chain) at FP16 matrix-core throughput.  NRT_MIXED is
+ *     NRT_FP32_SPLIT except that the ring-engine SDF march + scan runs at FP16 and every decision
+ *     FP16 cannot make (a step whose value lies within the "mixed_refine_d" bound of eps or of
+ *     max_t, a scan whose two smallest values lie within "mixed_refine_s") is taken again on the
+ *     split engine; sdf(best), the normals and the shading are split.
  */
 #ifndef NRT_H_
 #define NRT_H_
@@ -42,6 +46,7 @@ extern "C" {
 #define NRT_FP32 0
 #define NRT_FP16 1
 #define NRT_FP32_SPLIT 2
+#define NRT_MIXED 3
 
 /* activations (neural_blocks.py:26 leaky_relu default; sdfs.py:29 softplus) */
 #define NRT_ACT_LEAKY_RELU 0
@@ -160,7 +165,7 @@ typedef struct {
   float max_t;         /* intersect(max_t=10)                                              */
   int32_t primary;     /* 1: run the 128-step coarse scan (SDF.throughput, sdfs.py:232)     */
   double scan_max_t;   /* dist + random.random()*(2/128), computed by the caller           */
-  int32_t precision;   /* NRT_FP32 / NRT_FP16 / NRT_FP32_SPLIT                              */
+  int32_t precision;   /* NRT_FP32 / NRT_FP16 / NRT_FP32_SPLIT / NRT_MIXED                  */
   int32_t* scan_index; /* optional [P] output: the coarse-scan argmin idxs (sdfs.py:243-246), so a
                           training caller can rebuild best_pos = o + idx*step*d; NULL = unused  */
   /* Batched tiles (pathtrace's chunk_size^2 tile loop in one call, main.py:63-90): when not NULL,
@@ -459,6 +464,11 @@ int nrt_profile_evals(uint64_t* evals);
  *   "xcd_lines"     0  1: ring marches deal rays to waves XCD by XCD (each 32-ray line of the
  *                      outputs stored by waves of one XCD); measured: more HBM write traffic
  *                      than the plain strided deal (0), kept for A/B runs; bit-identical results
+ *   "mixed_refine_d" 1200 NRT_MIXED: a march step is re-taken at FP32 accuracy when its FP16
+ *                      value lies within d * (1 + step/16) of eps (or its next t of max_t); 1e-7
+ *                      units (the FP16 SDF error of the headline scene is <= 7.3e-5)
+ *   "mixed_refine_s" 2000 NRT_MIXED: sdf(best) re-evaluates the scan's runner-up when the FP16
+ *                      minimum and runner-up lie within s (1e-7 units)
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
 int nrt_set_option(const char* name, int64_t value);

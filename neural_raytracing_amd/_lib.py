@@ -16,7 +16,9 @@ LIB_PATH = os.environ.get("NRT_LIB") or os.path.join(HERE, "libnrt_hip.so")
 NRT_FP32 = 0
 NRT_FP16 = 1
 NRT_FP32_SPLIT = 2
-_PRECISIONS = {"fp32": NRT_FP32, "fp16": NRT_FP16, "fp32-split": NRT_FP32_SPLIT}
+NRT_MIXED = 3
+_PRECISIONS = {"fp32": NRT_FP32, "fp16": NRT_FP16, "fp32-split": NRT_FP32_SPLIT,
+               "mixed": NRT_MIXED}
 
 ACT = {"leaky_relu": 0, "softplus": 1, "none": 2, "sigmoid": 3, "relu": 4}
 
@@ -183,7 +185,10 @@ _precision = {"value": NRT_FP16 if os.environ.get("NRT_PRECISION", "fp32") == "f
 def set_precision(p):
     """'fp32' (exact-f32 MFMA, parity with the reference), 'fp16' (f16 MFMA, f32 accumulate) or
     'fp32-split' ('fp32', with the SDF march + scan at FP32 accuracy on FP16 MFMA: every operand
-    split into two f16 halves, three products; include/nrt.h NRT_FP32_SPLIT)."""
+    split into two f16 halves, three products; include/nrt.h NRT_FP32_SPLIT) or 'mixed'
+    ('fp32-split', with the SDF march + scan at FP16 and every decision FP16 cannot make --
+    a hit / max_t test near its threshold, a scan argmin between near-equal values -- taken
+    again at FP32 accuracy; include/nrt.h NRT_MIXED)."""
     if p not in _PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(_PRECISIONS)}")
     _precision["value"] = _PRECISIONS[p]

@@ -109,7 +109,8 @@ int nrt_sdf_eval(const nrt_sdf* s, const float* p, int64_t M, float* out, int pr
   if (!s || M < 0) { set_error("nrt_sdf_eval: bad argument"); return NRT_EINVAL; }
   if (M == 0) return NRT_OK;
   if (!p || !out) { set_error("nrt_sdf_eval: null p / out"); return NRT_EINVAL; }
-  if (precision == NRT_FP32_SPLIT && ring3_supported(s) && option(OPT_RING32) != 0)
+  if ((precision == NRT_FP32_SPLIT || precision == NRT_MIXED) && ring3_supported(s) &&
+      option(OPT_RING32) != 0)
     return ring_eval3(s, p, M, out, (hipStream_t)stream);
   const bool f16 = precision == NRT_FP16;
   int hidden, ke;
@@ -187,7 +188,10 @@ static size_t grad_ws_aligned(const nrt_sdf* s) { return (grad_workspace_bytes(s
 size_t nrt_intersect_workspace_bytes(const nrt_sdf* s, int64_t P) {
   if (!s) return 0;
   const bool keys = ring_supported(s) || ring32_supported(s);
-  return grad_ws_aligned(s) + (keys ? ring_march_ws_bytes(std::max<int64_t>(P, 0)) : 0) + 256;
+  P = std::max<int64_t>(P, 0);
+  // NRT_MIXED's runner-up keys, march flags and refinement list behind the keys
+  return grad_ws_aligned(s) + (keys ? ring_march_ws_bytes(P) : 0) +
+         (mixed_supported(s) ? mixed_ws_bytes(P) : 0) + 256;
 }
 
 int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_march_params* a,
@@ -202,7 +206,12 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   if (s->mlp && !workspace) { set_error("nrt_sdf_intersect: workspace required"); return NRT_EINVAL; }
   if (P == 0) return NRT_OK;
   hipStream_t st = (hipStream_t)stream;
-  const bool f16 = a->precision == NRT_FP16;
+  // NRT_MIXED: the FP16 march + scan with split refinement (nrt_ring_mixed.hip); its normals, and
+  // the whole intersect of an SDF without both ring engines, at fp32-split
+  const bool mixed = a->precision == NRT_MIXED && mixed_supported(s) && option(OPT_RING16) != 0 &&
+                     option(OPT_RING32) != 0;
+  const int prec = a->precision == NRT_MIXED ? NRT_FP32_SPLIT : a->precision;
+  const bool f16 = prec == NRT_FP16;
   int hidden, ke;
   sdf_dims(s, hidden, ke);
   MarchArgs ma;
@@ -241,11 +250,13 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
   // ... and FP32 SDF MLPs of those widths the FP32 ring kernel (refreshed training handles too)
   const bool ring32 = !f16 && ring32_supported(s) && option(OPT_RING32) != 0;
   // ... and the fp32-split precision the FP32-accurate FP16-MFMA engine (nrt_ring3.h)
-  const bool ring3 = ring32 && a->precision == NRT_FP32_SPLIT && ring3_supported(s);
+  const bool ring3 = ring32 && prec == NRT_FP32_SPLIT && ring3_supported(s);
   if (ring16 || ring32) {
     ProfScope prof("k_intersect", st);
     auto* keys = reinterpret_cast<unsigned long long*>(ws + grad_ws_aligned(s));
-    rc0 = ring16 ? ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
+    rc0 = mixed  ? ring_march_mixed(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys,
+                                    ws + grad_ws_aligned(s) + ring_march_ws_bytes(P), st)
+        : ring16 ? ring_march(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
         : ring3  ? ring_march3(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st)
                  : ring_march32(s, rays, P, ma, t, hit, p, n, raw_n, throughput, idx, cnt, keys, st);
     if (!rc0 && ma.scan_idx) {

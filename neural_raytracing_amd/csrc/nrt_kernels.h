@@ -264,6 +264,23 @@ struct MarchArgs {
   int lds_spheres = 0;
   // ring marches: deal rays to waves by XCD lines (OwnedRays; option "xcd_lines")
   int xcd_lines = 0;
+  // NRT_MIXED (the FP16 march refined where FP16 cannot decide, nrt_ring_mixed.hip):
+  //  * FP16 march: a step whose value lies within refine_d * (1 + i/16) of eps, or whose t lies that
+  //    close to max_t, marks the ray -- amb[ray] = (i << 32 | t bits), the first such step's state
+  //    (the march goes on; amb stays all-ones for a ray FP16 decided clearly);
+  //  * FP16 scan: keys2[ray] = the runner-up key beside keys[ray] (top two over the 129 samples,
+  //    merged lock-free across segments), so sdf(best) can re-evaluate both when they lie within
+  //    refine_s of each other;
+  //  * refinement launches: job k's ray is list[k] for k < *count, and a march starts from the
+  //    state in start[ray] instead of (t = 0, i = 0);
+  //  * sdf(best) with keys2: both candidates' values merge into kbest[ray] (atomic min of the key)
+  float refine_d = 0.f, refine_s = 0.f;
+  unsigned long long* amb = nullptr;
+  unsigned long long* keys2 = nullptr;
+  unsigned long long* kbest = nullptr;
+  const unsigned long long* start = nullptr;
+  const int32_t* list = nullptr;
+  const int32_t* count = nullptr;
 };
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
@@ -394,6 +411,12 @@ __device__ __forceinline__ uint64_t scan_key(float v, int idx) {
   uint32_t b = __float_as_uint(v + 0.f);  // -0 -> +0: equal values tie, as under the reference's <
   b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
   return ((uint64_t)b << 32) | (uint32_t)idx;
+}
+// the value of a scan key (inverse of scan_key's order-preserving map; all-ones -> NaN)
+__device__ __forceinline__ float scan_key_value(uint64_t k) {
+  uint32_t b = (uint32_t)(k >> 32);
+  b = (b & 0x80000000u) ? (b & 0x7fffffffu) : ~b;
+  return __uint_as_float(b);
 }
 
 // Rays owned by wave w of nw (the strided deal, kRayChunk = 1: ray w, w + nw, ...): every wave
@@ -535,7 +558,9 @@ struct RingPol3 {
   }
 };
 
-template <class Pol, int MODE>
+// MX: the NRT_MIXED variant (MarchArgs' refine fields live); the plain kernels compile without
+// any of it
+template <class Pol, int MODE, bool MX = false>
 __device__ __forceinline__ void march_body(
     const SdfDev s, const MlpDev m, const float* __restrict__ rays, int64_t P, MarchArgs a,
     float* __restrict__ t_out, uint8_t* __restrict__ hit_out, float* __restrict__ p_out,
@@ -548,13 +573,20 @@ __device__ __forceinline__ void march_body(
   const int lane = lane_id(), r = lane & (RPW - 1);
   const int64_t nw = (int64_t)gridDim.x * WV;
   const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const OwnedRays own(P, nw, w, WV, a.xcd_lines != 0);
+  // a refinement launch works through the first *count entries of a ray list
+  const int64_t Pe =
+      (MX && a.count) ? (int64_t)__builtin_amdgcn_readfirstlane(*(const NRT_GLOBAL int32_t*)a.count)
+                      : P;
+  const OwnedRays own(Pe, nw, w, WV, a.xcd_lines != 0);
   const int64_t R = own.R;  // rays owned by this wave
   const bool scan = mode == 0 && a.primary;
   // scan jobs: the whole 129-point scan of each of the first R - T rays (one plain key store),
   // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail
   const int64_t T = kScanSplit < 0 ? R : (R < kScanSplit ? R : (int64_t)kScanSplit);
-  const int64_t J = mode == 0 ? (scan ? R + (R - T) + T * kScanSegs : R) : R;
+  // sdf(best) with a runner-up key: a second job per ray re-evaluates the runner-up where the
+  // FP16 scan could not order the two (skipped elsewhere)
+  const bool alt = MX && mode == 1 && a.keys2 != nullptr;
+  const int64_t J = mode == 0 ? (scan ? R + (R - T) + T * kScanSegs : R) : (alt ? 2 * R : R);
   const uint32_t lt = (1u << r) - 1u;
   typename Pol::Eng E;
   Pol::init(E, s, m, smem_c, a);
@@ -562,10 +594,11 @@ __device__ __forceinline__ void march_body(
   int kind = -1;
   int64_t ray = 0;
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 0.f, dz = 0.f;
-  float t = 0.f, best = 0.f;
+  float t = 0.f, best = 0.f, second = 0.f;
   double step = a.step;  // this lane's scan step (per tile group when batched)
-  int i = 0, j = 0, jend = 0, idx = 0;
+  int i = 0, j = 0, jend = 0, idx = 0, idx2 = 0;
   bool ended = false, hit = false, whole = false;
+  unsigned long long ambs = ~0ull;  // NRT_MIXED: the first undecidable step's (i, t), or none
   int64_t cursor = 0;  // wave-uniform
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
@@ -573,6 +606,7 @@ __device__ __forceinline__ void march_body(
       if (kind == 0) {
         // sdfs.py:119-131: a march ends on a hit, when t leaves [0, max_t) or after max_steps
         if (ended || !(t < a.max_t) || i >= a.max_steps) {
+          if (MX && lane < RPW && a.amb && ambs != ~0ull) a.amb[ray] = ambs;
           if (lane < RPW) {
             if (p_out) {
               t_out[ray] = t;
@@ -596,10 +630,19 @@ __device__ __forceinline__ void march_body(
           // a whole scan stores its key; a segment merges into it (all segments of a ray are
           // in this wave's list; the key buffer starts at all-ones)
           if (lane < RPW) {
-            if (whole)
-              keys[ray] = (unsigned long long)scan_key(best, idx);
-            else
-              atomicMin(keys + ray, (unsigned long long)scan_key(best, idx));
+            const unsigned long long k1 = scan_key(best, idx);
+            if (whole) {
+              keys[ray] = k1;
+              if (MX && a.keys2) a.keys2[ray] = scan_key(second, idx2);
+            } else {
+              const unsigned long long old = atomicMin(keys + ray, k1);
+              if (MX && a.keys2) {
+                // top two over the union, lock-free: every key that is not the final minimum
+                // is either a segment's runner-up or lost one atomic min (old vs k1)
+                atomicMin(a.keys2 + ray, old > k1 ? old : k1);
+                atomicMin(a.keys2 + ray, (unsigned long long)scan_key(second, idx2));
+              }
+            }
           }
           kind = -1;
         }
@@ -627,7 +670,10 @@ __device__ __forceinline__ void march_body(
               k = R - T + (k - (int64_t)seg * T);
             }
           }
+          const bool second_job = alt && q >= R;  // sdf(best)'s runner-up job
+          if (second_job) k = q - R;
           ray = own.ray(k);
+          if (MX && a.list) ray = a.list[ray];
           if (mode == 2) {  // point evaluation: `rays` holds [P, 3] points, sdf(p) -> thr_out
             const float* pp = rays + ray * 3;
             ox = pp[0]; oy = pp[1]; oz = pp[2];
@@ -642,9 +688,21 @@ __device__ __forceinline__ void march_body(
             idx = 0;
           } else if (mode == 1) {
             kind = 2;
-            idx = (int)(uint32_t)keys[ray];
+            const unsigned long long k1 = keys[ray];
+            idx = (int)(uint32_t)k1;
+            if (second_job) {
+              // the runner-up only where the FP16 values of the two lie within refine_s
+              const unsigned long long k2 = a.keys2[ray];
+              idx = (int)(uint32_t)k2;
+              if (!(scan_key_value(k2) - scan_key_value(k1) <= a.refine_s)) kind = -1;
+            }
           } else if (seg < 0) {
-            kind = 0; t = 0.f; i = 0; hit = false;
+            kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull;
+            if (MX && a.start) {
+              const unsigned long long s0 = a.start[ray];
+              t = __uint_as_float((uint32_t)s0);
+              i = (int)(s0 >> 32);
+            }
           } else {
             kind = 1;
             whole = seg == kScanSegs;
@@ -687,19 +745,38 @@ __device__ __forceinline__ void march_body(
     // iteration, so the block's ring barriers stay matched)
     if (Pol::retry(E, kind >= 0, d)) continue;
     if (kind == 0) {
+      if (MX && a.amb && ambs == ~0ull) {
+        // NRT_MIXED: FP16 cannot tell this step's hit test (or the next t's max_t test) from
+        // the FP32 one.  refine_d covers the FP16 value's own error; t's drift from the FP32
+        // march is a sum of those errors damped by (1 - cos) at every step towards a surface,
+        // so the bound grows slowly with the steps (x2 after 16)
+        const float bound = a.refine_d * (1.f + 0.0625f * (float)i);
+        const float tn = t + d;
+        if (fabsf(d - a.eps) <= bound || (d > a.eps && fabsf(tn - a.max_t) <= bound))
+          ambs = ((unsigned long long)(uint32_t)i << 32) | __float_as_uint(t);
+      }
       if (d <= a.eps) { hit = true; ended = true; }
       else t = t + d;
       ++i;
     } else if (kind == 1) {
       // sdfs.py:246-248: idx = where(s < m, i + 1, idx); m = min(m, s)
-      if (idx < 0) { best = d; idx = j; }  // first sample of the segment
-      else {
+      if (idx < 0) { best = d; idx = j; second = __builtin_inff(); idx2 = j; }  // first sample
+      else if constexpr (MX) {  // (second, idx2): the runner-up, for NRT_MIXED's sdf(best)
+        if (d < best) { second = best; idx2 = idx; idx = j; }
+        else if (d < second) { second = d; idx2 = j; }
+        best = fminf(best, d);
+      } else {
         if (d < best) idx = j;
         best = fminf(best, d);
       }
       ++j;
     } else if (kind == 2) {
-      if (lane < RPW) thr_out[ray] = mode == 2 ? d : -1000.f * d;
+      if (lane < RPW) {
+        if (MX && mode == 1 && a.kbest)  // both candidates of a ray merge; k_scan_pick writes thr
+          atomicMin(a.kbest + ray, (unsigned long long)scan_key(d, idx));
+        else
+          thr_out[ray] = mode == 2 ? d : -1000.f * d;
+      }
       ended = true;
     }
   }
@@ -713,9 +790,9 @@ __device__ __forceinline__ void march_body(
       float* __restrict__ n_out, float* __restrict__ rawn_out, float* __restrict__ thr_out,    \
       unsigned long long* __restrict__ keys
 #define NRT_MARCH_PASS t_out, hit_out, p_out, n_out, rawn_out, thr_out, keys
-template <int NB, int NE, int WV, bool FOLD>
+template <int NB, int NE, int WV, bool FOLD, bool MX = false>
 __global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_march16(NRT_MARCH_ARGS) {
-  march_body<RingPol16<NB, NE, WV, FOLD>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
+  march_body<RingPol16<NB, NE, WV, FOLD>, 0, MX>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 template <int NB, int NE, int WV, bool FOLD>
 __global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_scan_best16(NRT_MARCH_ARGS) {
@@ -732,13 +809,13 @@ __global__ void __launch_bounds__(64 * WV, 1) k_scan_best32(NRT_MARCH_ARGS) {
   march_body<RingPol32<KH, KE, WV, ACT>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 // fp32-split (FP32-accurate on FP16 MFMA): one block of WV waves per CU, two waves per SIMD
-template <int KH, int KQ, int WV, int ACT>
+template <int KH, int KQ, int WV, int ACT, bool MX = false>
 __global__ void __launch_bounds__(64 * WV, 1) k_march3(NRT_MARCH_ARGS) {
-  march_body<RingPol3<KH, KQ, WV, ACT>, 0>(s, m, rays, P, a, NRT_MARCH_PASS);
+  march_body<RingPol3<KH, KQ, WV, ACT>, 0, MX>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
-template <int KH, int KQ, int WV, int ACT>
+template <int KH, int KQ, int WV, int ACT, bool MX = false>
 __global__ void __launch_bounds__(64 * WV, 1) k_scan_best3(NRT_MARCH_ARGS) {
-  march_body<RingPol3<KH, KQ, WV, ACT>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
+  march_body<RingPol3<KH, KQ, WV, ACT>, 1, MX>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 // sdf(p) of P points on the ring engines (nrt_sdf_eval: fp32-split and FP32 precision)
 template <int KH, int KQ, int WV, int ACT>
@@ -804,6 +881,37 @@ __global__ void k_keys_index(const unsigned long long* __restrict__ keys, int64_
                              int32_t* __restrict__ idx) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < P) idx[i] = (int32_t)(uint32_t)keys[i];
+}
+
+// NRT_MIXED: the rays whose FP16 march met an undecidable step (amb != all-ones), as a list for
+// the refinement march (wave-aggregated appends; order is irrelevant)
+template <int = 0>
+__global__ void k_refine_list(const unsigned long long* __restrict__ amb, int64_t P,
+                              int32_t* __restrict__ list, int32_t* __restrict__ cnt) {
+  const int lane = lane_id();
+  for (int64_t ray = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ray - lane < P;
+       ray += (int64_t)gridDim.x * blockDim.x) {
+    const bool f = ray < P && amb[ray] != ~0ull;
+    const uint64_t mk = __ballot(f);
+    const int c = __popcll(mk);
+    int base = 0;
+    if (lane == 0 && c) base = atomicAdd(cnt, c);
+    base = __shfl(base, 0);
+    if (f) list[base + __popcll(mk & ((1ull << lane) - 1ull))] = (int32_t)ray;
+  }
+}
+
+// NRT_MIXED sdf(best): kbest holds the smaller (value, index) key of the candidates evaluated at
+// FP32 accuracy; thr = -1000 * value (sdfs.py:137) and the key's index replaces the FP16 argmin
+template <int = 0>
+__global__ void k_scan_pick(const unsigned long long* __restrict__ kbest, int64_t P,
+                            unsigned long long* __restrict__ keys, float* __restrict__ thr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < P) {
+    const unsigned long long k = kbest[i];
+    thr[i] = -1000.f * scan_key_value(k);
+    keys[i] = k;
+  }
 }
 
 // After a ring march that packed (hit, t) into t's sign bit (march_body with p_out == nullptr):

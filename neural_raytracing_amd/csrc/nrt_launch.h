@@ -27,6 +27,8 @@ enum Option {
   OPT_SHADE_RING,      // "shade_ring"
   OPT_NORMALS_RING,    // "normals_ring"
   OPT_XCD_LINES,       // "xcd_lines"
+  OPT_MIXED_D,         // "mixed_refine_d" (1e-7 units)
+  OPT_MIXED_S,         // "mixed_refine_s" (1e-7 units)
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -145,6 +147,10 @@ int ring_dispatch(const nrt_sdf* s, F&& f) {
 int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                int32_t* cnt, unsigned long long* keys, hipStream_t st);
+// k_march16 alone (packed t, scan keys; the caller initialises keys): NRT_MIXED's first pass
+int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                        float* t, float* thr, unsigned long long* keys, hipStream_t st,
+                        bool best16);
 
 // ---- FP32 ring engine (nrt_ring_march32.hip) ----
 // SDF MLPs with a compiled FP32 ring kernel: hidden 128 / 256, F = 16 / 32 with 3 inputs and no
@@ -184,6 +190,24 @@ int ring_eval3(const nrt_sdf* s, const float* pts, int64_t M, float* out, hipStr
 int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                 int32_t* cnt, unsigned long long* keys, hipStream_t st);
+// the split engine's launches alone: which = 0 k_march3 (+ k_scan_best3 when primary), 1
+// k_scan_best3 (the caller initialises keys); 2 / 3 the same as NRT_MIXED's refinement passes
+int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                 float* thr, unsigned long long* keys, hipStream_t st, int which);
+// NRT_MIXED intersect (nrt_ring_mixed.hip): FP16 march + scan, split refinement of the
+// undecidable steps and scan orders, split sdf(best); same outputs as ring_march
+// the FP16 SDF error of the headline scene (tools/fp16_decompose.py, 1M scan points and the
+// FP32 march's 279k stop points): median 1.9e-5, 99.99 % 5.6e-5, max 7.3e-5
+constexpr int64_t kMixedRefineD = 1200;  // 1.2e-4: the max error, with margin
+constexpr int64_t kMixedRefineS = 2000;  // 2e-4: two values' errors, with margin
+inline bool mixed_supported(const nrt_sdf* s) { return ring_supported(s) && ring3_supported(s); }
+inline size_t mixed_ws_bytes(int64_t P) {
+  // keys2 | amb (reused as kbest) | list | count
+  return 2 * (((size_t)P * 8 + 255) & ~(size_t)255) + (((size_t)P * 4 + 255) & ~(size_t)255) + 256;
+}
+int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                     uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                     int32_t* cnt, unsigned long long* keys, char* mixed_ws, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
 inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
 int ring_normals32(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,

@@ -4,19 +4,15 @@
 
 namespace nrt {
 
-int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
-               uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
-               int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                        float* t, float* thr, unsigned long long* keys, hipStream_t st,
+                        bool best16) {
   const size_t bias_bytes = ring_bias_bytes(s);
   int dev = 0, cus = 0;
   NRT_HIP(hipGetDevice(&dev));
   NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const bool scan = ma.primary != 0;
-  // option "scan_best32": sdf(best) on the FP32 engine -- the throughput -1000 sdf(best)
-  // (sdfs.py:137) multiplies the FP16 SDF error by 1000 in the alpha logit
-  const bool best32 = scan && option(OPT_SCAN_BEST32) != 0 && ring32_supported(s);
-  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
-  int rc = ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
+  return ring_dispatch(s, [&]<int NB, int NE, bool FOLD>() -> int {
     // the SphereSDF table goes into LDS behind the ring when it fits and costs no resident block
     // (spheres_value_halves: the two lanes of a ray split the spheres; colocate's 64 spheres:
     // k_march16 51.3 -> 43.8 ms); a table of a few spheres stays on scalar loads
@@ -41,23 +37,32 @@ int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& 
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, a, t, hit, nullptr, nullptr, nullptr, thr, keys);
+          s->host_dev, s->mlp->host_dev, rays, P, a, t, nullptr, nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
+    // NRT_MIXED's flagging march is its own instantiation (the plain one carries none of it)
+    if (ma.amb) return launch(k_march16<NB, NE, kRingWaves, FOLD, true>, "k_march16");
     if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
-    if (scan && !best32) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
+    if (scan && best16) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
     return NRT_OK;
   });
-  if (rc) return rc;
+}
+
+int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+               uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+               int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+  const bool scan = ma.primary != 0;
+  // option "scan_best32": sdf(best) on the FP32 engine -- the throughput -1000 sdf(best)
+  // (sdfs.py:137) multiplies the FP16 SDF error by 1000 in the alpha logit
+  const bool best32 = scan && option(OPT_SCAN_BEST32) != 0 && ring32_supported(s);
+  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
+  if (int rc = ring_march16_launch(s, rays, P, ma, t, thr, keys, st, !best32)) return rc;
   if (best32)
     if (int rc2 = ring_scan_best32(s, rays, P, ma, thr, keys, st)) return rc2;
   // the march packed (hit, t) into t: unpack, p / n / raw_n and the hit list, coalesced
-  {
-    k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
-        rays, P, t, hit, p, n, raw_n, idx, cnt);
-    if (int rc2 = check_launch("k_march_finish")) return rc2;
-  }
-  return NRT_OK;
+  k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
+      rays, P, t, hit, p, n, raw_n, idx, cnt);
+  return check_launch("k_march_finish");
 }
 
 }  // namespace nrt

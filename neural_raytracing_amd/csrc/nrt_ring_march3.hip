@@ -38,16 +38,14 @@ int ring_eval3(const nrt_sdf* s, const float* pts, int64_t M, float* out, hipStr
   return NRT_EINVAL;
 }
 
-int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
-                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
-                int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                 float* thr, unsigned long long* keys, hipStream_t st, int which) {
   const MlpDev& md = s->mlp->host_dev;
   const size_t extra = (size_t)md.freqs * 16 + ring32_bias_bytes(s) + ring32_sphere_bytes(s);
   int dev = 0, cus = 0;
   NRT_HIP(hipGetDevice(&dev));
   NRT_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const bool scan = ma.primary != 0;
-  if (scan) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   auto run = [&]<int KH, int KQ, int ACT>() -> int {
     constexpr int WV = kRing3Waves;
     auto launch = [&](auto kern, const char* name) -> int {
@@ -60,11 +58,15 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, nullptr,
-                                                     nullptr, nullptr, thr, keys);
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, nullptr,
+                                                     nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
-    if (int rc = launch(k_march3<KH, KQ, WV, ACT>, "k_march3")) return rc;
+    // profile names: the NRT_MIXED refinement launches (which 2 / 3) apart from the plain ones
+    if (which == 2) return launch(k_march3<KH, KQ, WV, ACT, true>, "k_refine3");
+    if (which == 3) return launch(k_scan_best3<KH, KQ, WV, ACT, true>, "k_best3");
+    if (which == 0)
+      if (int rc = launch(k_march3<KH, KQ, WV, ACT>, "k_march3")) return rc;
     if (scan) return launch(k_scan_best3<KH, KQ, WV, ACT>, "k_scan_best3");
     return NRT_OK;
   };
@@ -80,13 +82,17 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
     return NRT_EINVAL;
   }
 #undef NRT_R3
-  if (rc) return rc;
-  {
-    k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
-        rays, P, t, hit, p, n, raw_n, idx, cnt);
-    if (int rc2 = check_launch("k_march_finish")) return rc2;
-  }
-  return NRT_OK;
+  return rc;
+}
+
+int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
+                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
+                int32_t* cnt, unsigned long long* keys, hipStream_t st) {
+  if (ma.primary) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
+  if (int rc = ring3_launch(s, rays, P, ma, t, thr, keys, st, 0)) return rc;
+  k_march_finish<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
+      rays, P, t, hit, p, n, raw_n, idx, cnt);
+  return check_launch("k_march_finish");
 }
 
 }  // namespace nrt

@@ -283,7 +283,7 @@ int with_depth(const RProgDev& d, F&& f) {
 int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
                const float* lscale, float* rgb, float* weights_out, int precision, hipStream_t st) {
-  const bool split = precision == NRT_FP32_SPLIT;
+  const bool split = precision == NRT_FP32_SPLIT || precision == NRT_MIXED;  // NRT_MIXED shades at fp32-split
   const int pi = split ? 1 : 0;
   const bool field = l->host_dev.kind == 0;
   if (b->host_dev.n > 16) return NRT_EUNSUPPORTED;

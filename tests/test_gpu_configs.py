@@ -62,7 +62,7 @@ def _camera_rays(n, seed, eye=(0.0, 0.1, 1.0), spread=0.9):
     return torch.cat([o, d], -1)
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "mixed"])
 def test_bare_mlp_sdf_march_matches_oracle(prec):
     """SDF(sdf=SkipConnMLP 8x256) -- the kind cfg2/cfg4 march -- vs MarchedSDF on sdf(p)[..., 0]
     (sdfs.py:111-160, 232-249; the reference's SDF wants a [...] output, so the bare MLP's single
@@ -101,7 +101,7 @@ def test_bare_mlp_sdf_march_matches_oracle(prec):
            step_flips=int(step.sum()), t_maxabs=t_err, n_maxabs=n_err, p_maxabs=p_err,
            thr_maxabs=thr.max().item(), thr_over_0p1=int((thr > 0.1).sum()))
     assert 0.15 < rhit.float().mean() < 0.85
-    if prec == "fp32":
+    if prec != "fp16":  # fp32, and mixed (FP16 march refined where FP16 cannot decide): FP32 bar
         assert flips + int(step.sum()) <= 0.005 * hit.numel()
         assert t_err <= 1e-4 and p_err <= 1e-4 and n_err <= 1e-4
         # throughput = -1000 sdf(best): 1e-4 abs on sdf is 0.1 here
@@ -151,7 +151,7 @@ def _agreement(prod_shape, oracle_shape, prod_rays, oracle_rays):
     return (h == rh) & ~step, rh, int((h != rh).sum()), int(step.sum())
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "mixed"])
 def test_metric_config_crop_matches_oracle(prec):
     """bench.py's headline scene (800x800 NeRFCamera frame, SDF = one-sphere prior + 8x256
     softplus shift MLP, 64 march steps + 130-eval coarse scan, ComposeSpatialVarying of 8
@@ -192,11 +192,12 @@ def test_metric_config_crop_matches_oracle(prec):
            step_flips=steps, maxabs_agreeing=err[agree].max().item(),
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.95
-    if prec == "fp32":
+    if prec != "fp16":  # fp32 and mixed: the FP32 bar
         assert int((~agree).sum()) <= 0.005 * crop * crop
         assert err[agree].max().item() <= 1e-4
-    else:
-        assert psnr > 40, psnr
+    else:  # measured: 90.5 dB, 4.3e-5 max on agreeing pixels, 60 step flips
+        assert psnr > 75, psnr
+        assert err[agree].max().item() <= 2e-4
 
 
 # ------------------------------------------------------------------------------------------
@@ -264,8 +265,9 @@ def test_dtu_like_render_matches_oracle(prec):
     if prec != "fp16":  # fp32 and fp32-split: the FP32 bar
         assert int((~agree).sum()) <= 0.005 * crop * crop
         assert err[agree].max().item() <= 1e-4
-    else:
-        assert psnr > 40, psnr
+    else:  # measured: 50.9 dB (2 hit flips), 1.0e-4 max on agreeing pixels
+        assert psnr > 45, psnr
+        assert err[agree].max().item() <= 5e-4
 
 
 # ------------------------------------------------------------------------------------------

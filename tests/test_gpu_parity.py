@@ -583,12 +583,10 @@ def test_direct_shadow_rays_match_oracle(prec):
     err = (got - want).abs().amax(-1)
     report(f"direct_shadow_rays[{prec}]", pixels=err.numel(), shadowed=int(shadowed.sum()),
            over_1e4=int((err > 1e-4).sum()), maxabs=err.max().item())
-    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar (flips at a shadow boundary aside)
-        close = err <= 1e-4
-        assert close.float().mean() >= 0.995, (got - want).abs().max()
-    else:
-        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
-        assert -10 * math.log10(max(mse, 1e-12)) > 40
+    # fp32 and fp32-split: the FP32 bar (flips at a shadow boundary aside); fp16 measured
+    # 4e-7 here (the Diffuse shading is FP32 math on FP16-march hits): the same bar
+    close = err <= 1e-4
+    assert close.float().mean() >= 0.995, (got - want).abs().max()
 
 
 def _occ_pair(out=1, seed=21):
@@ -764,12 +762,12 @@ def test_colocate_fov_render_matches_oracle(prec):
     report(f"colocate_fov_render[{prec}]", pixels=err.numel(), hits=int(rh.sum()), flips=flips,
            step_flips=steps, over_1e4=int((err > 1e-4).sum()),
            over_1e4_on_agreeing=int((err[agree] > 1e-4).sum()), maxabs=err.max().item())
+    assert int((~agree).sum()) <= 0.005 * err.numel()
     if prec != "fp16":  # fp32 and fp32-split: the FP32 bar on every ray whose march agrees
-        assert int((~agree).sum()) <= 0.005 * err.numel()
         assert int((err[agree] > 1e-4).sum()) == 0, err[agree].max()
-    else:
-        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
-        assert -10 * math.log10(max(mse, 1e-12)) > 40
+    else:  # measured 4.9e-4 max (FP16 SDF / shading MLP error), 299 of 4096 pixels > 1e-4
+        assert err[agree].max().item() <= 2e-3, err[agree].max()
+        assert int((err > 1e-4).sum()) <= 0.15 * err.numel()
 
 
 def _nerfle_pair(seed=19, envmap=False):
@@ -973,6 +971,6 @@ def test_path_integrator_matches_oracle(prec, w_isect):
            maxabs=err.max().item())
     if prec != "fp16":  # fp32 and fp32-split: no bounce flips on this scene (reported 0)
         assert int((err > 1e-4).sum()) == 0, err.max()
-    else:
-        mse = ((got.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
-        assert -10 * math.log10(max(mse, 1e-12)) > 30
+    else:  # measured 1.7e-4 max, 46 of 2304 pixels > 1e-4
+        assert err.max().item() <= 1e-3, err.max()
+        assert int((err > 1e-4).sum()) <= 0.05 * err.numel()
