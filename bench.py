@@ -33,6 +33,7 @@ SCAN_EVALS = 130             # sdf(o) + 128 samples + sdf(best)
 MARCH_KERNEL_SCAN_EVALS = 129
 PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}  # MI355X dense MFMA (MI355X_MICROARCH.md)
 PEAK_TFLOPS["fp32-split"] = PEAK_TFLOPS["fp16"]  # its MFMA work runs on the FP16 matrix cores
+PEAK_TFLOPS["mixed"] = PEAK_TFLOPS["fp16"]  # the FP16 march (+ split refinement, also FP16 MFMA)
 
 
 def parse():

@@ -464,9 +464,12 @@ int nrt_profile_evals(uint64_t* evals);
  *   "xcd_lines"     0  1: ring marches deal rays to waves XCD by XCD (each 32-ray line of the
  *                      outputs stored by waves of one XCD); measured: more HBM write traffic
  *                      than the plain strided deal (0), kept for A/B runs; bit-identical results
- *   "mixed_refine_d" 1200 NRT_MIXED: a march step is re-taken at FP32 accuracy when its FP16
- *                      value lies within d * (1 + step/16) of eps (or its next t of max_t); 1e-7
- *                      units (the FP16 SDF error of the headline scene is <= 7.3e-5)
+ *   "mixed_refine_d" 20000 NRT_MIXED: a ray is marched again at FP32 accuracy when one of its
+ *                      FP16 steps lies within d * (1 + step/16) of eps (or its next t of max_t);
+ *                      1e-7 units (the FP16 SDF error of the headline scene is <= 7.3e-5; slowly
+ *                      converging rays need the larger bound)
+ *   "mixed_restart"  1  1: a flagged ray marches again from t = 0; 0: it resumes at the flagged
+ *                      step (cheaper, but keeps the FP16 drift of t: measured 1,464 step flips)
  *   "mixed_refine_s" 2000 NRT_MIXED: sdf(best) re-evaluates the scan's runner-up when the FP16
  *                      minimum and runner-up lie within s (1e-7 units)
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.

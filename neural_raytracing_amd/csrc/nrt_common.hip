@@ -26,10 +26,10 @@ static const OptionDef kOptions[OPT_COUNT] = {
     {"ring16", 1}, {"ring32", 1}, {"normals16", 1}, {"scan_best32", 1},
     {"march_blocks", 0}, {"shade_program", 1}, {"nerf_fused", 1}, {"max_waves", 0},
     {"shade_ring", 1}, {"normals_ring", 1}, {"xcd_lines", 0},
-    {"mixed_refine_d", kMixedRefineD}, {"mixed_refine_s", kMixedRefineS},
+    {"mixed_refine_d", kMixedRefineD}, {"mixed_refine_s", kMixedRefineS}, {"mixed_restart", 1},
 };
 static std::atomic<int64_t> g_opts[OPT_COUNT] = {1, 1, 1, 1, 0, 1, 1, 0, 1, 1, 0,
-                                                 kMixedRefineD, kMixedRefineS};
+                                                 kMixedRefineD, kMixedRefineS, 1};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 

@@ -10,8 +10,9 @@
 //      that close to max_t) -- amb[ray] = that step's (i, t); the scan also keeps the runner-up
 //      key (keys2) beside the minimum;
 //   2. k_refine_list gathers the flagged rays, and k_march3 (the split engine, FP32 accuracy)
-//      resumes each of them at its flagged step's (i, t): the undecidable step and every later
-//      one are taken at FP32 accuracy (a resumed march is a handful of steps near a surface);
+//      marches each of them again from t = 0 (option "mixed_restart"; resuming at the flagged
+//      step's (i, t) instead keeps t's FP16 drift, and a slowly converging ray then still stops
+//      one step off the FP32 march: measured 1,464 step flips vs 4 on the 800^2 frame);
 //   3. sdf(best) runs on the split engine for every ray, and for a ray whose FP16 minimum and
 //      runner-up lie within refine_s of each other at the runner-up too; the smaller value (the
 //      first index on a tie, the reference's strict-<) gives the throughput and the argmin;
@@ -53,7 +54,9 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
   mr.scan_idx = nullptr;
   mr.list = list;
   mr.count = lcount;
-  mr.start = amb;
+  // option "mixed_restart" (default): a flagged ray marches again from t = 0 -- resumed at the
+  // flagged step instead, it would carry the FP16 march's drift of t into the decision
+  mr.start = option(OPT_MIXED_RESTART) ? nullptr : amb;
   if (int rc = ring3_launch(s, rays, P, mr, t, nullptr, nullptr, st, 2)) return rc;
   // 3. sdf(best) at FP32 accuracy, over both candidates where FP16 could not order them
   if (scan) {

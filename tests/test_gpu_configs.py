@@ -229,7 +229,7 @@ def _dtu_oracle(sc):
                 integrator=R.NeRFIntegratorRef(R.DirectRef()))
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16", "mixed"])
 def test_dtu_like_render_matches_oracle(prec):
     """cfg4 (dtu.py:91-113 with a synthetic DTU pinhole): DTUCamera (fx = fy = 2890, cx = 800,
     cy = 600 on the 1600x1200 sensor) + 8x256 MLP SDF + ComposeSpatialVarying([NeuralBSDF(
@@ -262,7 +262,7 @@ def test_dtu_like_render_matches_oracle(prec):
            step_flips=steps, maxabs_agreeing=err[agree].max().item(),
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.9, rh.float().mean()
-    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar
+    if prec != "fp16":  # fp32, fp32-split and mixed: the FP32 bar
         assert int((~agree).sum()) <= 0.005 * crop * crop
         assert err[agree].max().item() <= 1e-4
     else:  # measured: 50.9 dB (2 hit flips), 1.0e-4 max on agreeing pixels

@@ -551,7 +551,7 @@ def _shadow_scene():
     return oracle, prod
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16", "mixed"])
 def test_direct_shadow_rays_match_oracle(prec):
     """Direct with w_isect=True (sample_emitter_dir_w_isect, scene.py:290-298 + intersect_test,
     sdfs.py:162-181): HIP shadow march + masked shading vs the oracle.  FP32 within 1e-4 except
@@ -729,7 +729,7 @@ def _colocate_pair():
     return ref, mine
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-split", "fp16", "mixed"])
 def test_colocate_fov_render_matches_oracle(prec):
     """Full-frame pathtrace of the colocate-like scene (FoV camera, point light, 4-component
     spatially varying BSDF incl. Diffuse and Conductor) on the fused tile path vs the oracle."""
@@ -763,7 +763,7 @@ def test_colocate_fov_render_matches_oracle(prec):
            step_flips=steps, over_1e4=int((err > 1e-4).sum()),
            over_1e4_on_agreeing=int((err[agree] > 1e-4).sum()), maxabs=err.max().item())
     assert int((~agree).sum()) <= 0.005 * err.numel()
-    if prec != "fp16":  # fp32 and fp32-split: the FP32 bar on every ray whose march agrees
+    if prec != "fp16":  # fp32, fp32-split, mixed: the FP32 bar on every ray whose march agrees
         assert int((err[agree] > 1e-4).sum()) == 0, err[agree].max()
     else:  # measured 4.9e-4 max (FP16 SDF / shading MLP error), 299 of 4096 pixels > 1e-4
         assert err[agree].max().item() <= 2e-3, err[agree].max()
@@ -932,7 +932,7 @@ def _path_pair(seed=31):
 
 @pytest.mark.parametrize("prec,w_isect", [("fp32", False), ("fp32", True), ("fp16", True),
                                           ("fp32", "occ"), ("fp32-split", False),
-                                          ("fp32-split", True)])
+                                          ("fp32-split", True), ("mixed", True)])
 def test_path_integrator_matches_oracle(prec, w_isect):
     """Path (integrators.py:275-354), two bounces, with injected BSDF-sampling uniforms: the
     emitter term per bounce (optionally shadowed), ComposeSpatialVarying.sample, throughput
