@@ -964,7 +964,9 @@ def bench_train(args):
         "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {"fp32": "fp32", "fp16": "fp16 forward / fp32 backward",
-                  "fp32-split": "fp32-split forward (f16 hi/lo MFMA) / fp32 backward"}[prec],
+                  "fp32-split": "fp32-split forward (f16 hi/lo MFMA) / fp32 backward",
+                  "mixed": "mixed march (fp16 + split refinement) / fp32 MLP forwards and "
+                           "backward"}[prec],
         "data": "synthetic (seeded random-init weights, random target crops)",
         "config": {"workload": "forward (fused march + scan) + backward (MLP backward, SDF-normal "
                                "double backward, shading autograd) + AdamW",

@@ -48,6 +48,7 @@ struct nrt_mlp {
   std::vector<char> gather_f16;   // section kind (nrt_refresh.hip SecKind)
   bool refreshed = false;
   bool split_refreshed = false;  // the refresh also re-split stream3 (fp32-split march)
+  bool ring16_refreshed = false;  // ... and re-rounded stream16 (FP16 / mixed march)
   // single-MLP FP32 row program (nrt_shade_ring.hip) for nrt_mlp_forward on the ring engine;
   // nrt_mlp_refresh gathers its stream and bias table too once it exists
   mutable nrt_rprog solo32;

@@ -275,6 +275,7 @@ struct MarchArgs {
   //    state in start[ray] instead of (t = 0, i = 0);
   //  * sdf(best) with keys2: both candidates' values merge into kbest[ray] (atomic min of the key)
   float refine_d = 0.f, refine_s = 0.f;
+  int drift_model = 0;  // 1: the flag bound follows a per-ray drift estimate (option "mixed_drift")
   unsigned long long* amb = nullptr;
   unsigned long long* keys2 = nullptr;
   unsigned long long* kbest = nullptr;
@@ -599,6 +600,7 @@ __device__ __forceinline__ void march_body(
   int i = 0, j = 0, jend = 0, idx = 0, idx2 = 0;
   bool ended = false, hit = false, whole = false;
   unsigned long long ambs = ~0ull;  // NRT_MIXED: the first undecidable step's (i, t), or none
+  float drift = 0.f, dprev = 1.f;   // NRT_MIXED: t's drift bound (units of the FP16 error)
   int64_t cursor = 0;  // wave-uniform
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
@@ -697,7 +699,7 @@ __device__ __forceinline__ void march_body(
               if (!(scan_key_value(k2) - scan_key_value(k1) <= a.refine_s)) kind = -1;
             }
           } else if (seg < 0) {
-            kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull;
+            kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull; drift = 0.f;
             if (MX && a.start) {
               const unsigned long long s0 = a.start[ray];
               t = __uint_as_float((uint32_t)s0);
@@ -747,13 +749,16 @@ __device__ __forceinline__ void march_body(
     if (kind == 0) {
       if (MX && a.amb && ambs == ~0ull) {
         // NRT_MIXED: FP16 cannot tell this step's hit test (or the next t's max_t test) from
-        // the FP32 one.  refine_d covers the FP16 value's own error; t's drift from the FP32
-        // march is a sum of those errors damped by (1 - cos) at every step towards a surface,
-        // so the bound grows slowly with the steps (x2 after 16)
-        const float bound = a.refine_d * (1.f + 0.0625f * (float)i);
+        // the FP32 one.  The FP16 value is off by its own error e, and t has drifted from the
+        // FP32 march's by the earlier steps' errors: delta_{k+1} = delta_k (1 + g_k) + e_k with
+        // g_k = d(sdf)/dt along the ray, which the march observes as (d_k - d_{k-1}) / d_{k-1}.
+        // drift = that bound in units of e (a.drift_model), or the step-count rule 1 + i/16.
+        if (a.drift_model && i > 0) drift = drift * fabsf(d / dprev) + 1.f;
+        const float bound = a.refine_d * (a.drift_model ? 1.f + drift : 1.f + 0.0625f * (float)i);
         const float tn = t + d;
         if (fabsf(d - a.eps) <= bound || (d > a.eps && fabsf(tn - a.max_t) <= bound))
           ambs = ((unsigned long long)(uint32_t)i << 32) | __float_as_uint(t);
+        dprev = d;
       }
       if (d <= a.eps) { hit = true; ended = true; }
       else t = t + d;

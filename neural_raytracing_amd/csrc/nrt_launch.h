@@ -30,6 +30,7 @@ enum Option {
   OPT_MIXED_D,         // "mixed_refine_d" (1e-7 units)
   OPT_MIXED_S,         // "mixed_refine_s" (1e-7 units)
   OPT_MIXED_RESTART,   // "mixed_restart"
+  OPT_MIXED_DRIFT,     // "mixed_drift"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -109,7 +110,8 @@ static inline int sdf_dims(const nrt_sdf* s, int& hidden, int& ke) {
 // Configurations with a compiled ring kernel: 8 hidden layers of 128/256, skip 3, F = 16/32
 // (3 or 5 encoding k-steps), 3 inputs, no latent, <= 32 outputs.
 inline bool ring_supported(const nrt_sdf* s) {
-  if (!s->mlp || s->mlp->refreshed) return false;  // a refreshed handle's FP16 stream is stale
+  // a refreshed handle's FP16 ring stream is re-rounded by nrt_mlp_refresh (nrt_refresh.hip)
+  if (!s->mlp || (s->mlp->refreshed && !s->mlp->ring16_refreshed)) return false;
   const MlpDev& m = s->mlp->host_dev;
   const int ne = m.ke / 16;
   return (m.nb == 8 || m.nb == 4) && (ne == 3 || ne == 5) && s->mlp->desc.num_layers == 8 &&

@@ -5,9 +5,10 @@
 // fragment arrays the training kernels read -- FP16 / FP32 A fragments, FP32 W^T fragments,
 // padded biases, out.weight row 0 -- through a per-element index map built once on the host by
 // the same loops as nrt_pack.hip.  The FP32 ring stream is refreshed too (the FP32 march of a
-// training loop runs on it), and so is the fp32-split stream (folded, scaled and split into f16
-// halves on the device, k_refresh_all); the FP16 ring / program streams are not, and a refreshed
-// handle refuses those paths (ring_supported, build_program).
+// training loop runs on it), and so are the fp32-split stream (folded, scaled and split into f16
+// halves on the device, k_refresh_all) and the FP16 ring stream (folded, rounded to f16: the FP16
+// / mixed march of a training loop); the FP16 program streams of the shading kernels are not, and
+// a refreshed handle refuses those paths (build_program).
 #include <hip/hip_runtime.h>
 
 #include <vector>
@@ -24,7 +25,8 @@ struct SplitCoef {
 // map entries of the split sections: source index | layer << 25 | part << 30 (-1 = padding)
 constexpr int kSplitIdxBits = 25;
 
-enum SecKind { SEC_F32 = 0, SEC_F16 = 1, SEC_SPLIT = 2, SEC_SPLIT_BIAS = 3 };
+enum SecKind { SEC_F32 = 0, SEC_F16 = 1, SEC_SPLIT = 2, SEC_SPLIT_BIAS = 3, SEC_R16 = 4,
+               SEC_R16_BIAS = 5 };
 
 // Split sections: part 0 hi = RNE_f16(v), part 1 lo = RNE_f16(v - hi), or the scaled f32 biases
 // -- the packer's arithmetic, on the device.
@@ -72,6 +74,17 @@ __global__ void k_refresh_all(SectionTable t, const int* __restrict__ map,
   switch (t.kind[q]) {
     case SEC_F32: reinterpret_cast<float*>(t.dst[q])[j] = v < 0 ? 0.f : src[v]; break;
     case SEC_F16: reinterpret_cast<_Float16*>(t.dst[q])[j] = (_Float16)(v < 0 ? 0.f : src[v]); break;
+    // the FP16 ring stream: (_Float16)(fold_w[l] * W) and fold_b[l] * b, as nrt_pack.hip
+    case SEC_R16: {
+      const int k = v & ((1 << kSplitIdxBits) - 1), l = (v >> kSplitIdxBits) & 31;
+      reinterpret_cast<_Float16*>(t.dst[q])[j] = (_Float16)(v < 0 ? 0.f : src[k] * c.fold_w[l]);
+      break;
+    }
+    case SEC_R16_BIAS: {
+      const int k = v & ((1 << kSplitIdxBits) - 1), l = (v >> kSplitIdxBits) & 31;
+      reinterpret_cast<float*>(t.dst[q])[j] = v < 0 ? 0.f : src[k] * c.fold_b[l];
+      break;
+    }
     default: {
       const bool bias = t.kind[q] == SEC_SPLIT_BIAS;
       if (v < 0) {
@@ -223,6 +236,42 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
         map.push_back(r < ls[li].R ? (int)((ls[li].boff + r) | ((int64_t)li << kSplitIdxBits)) : -1);
     end();
   }
+  // the FP16 ring stream and its biases (the FP16 / mixed march of a training loop): the packer's
+  // chunk walk, each entry tagged with its layer for the softplus fold
+  if (n_src < (1 << kSplitIdxBits)) {
+    begin((void*)md.stream16, SEC_R16);
+    for (size_t li = 0; li < ls.size(); ++li) {
+      const Ly& l = ls[li];
+      const bool is_init = li == 0, is_out = li + 1 == ls.size();
+      const int nrb = (l.R + 31) / 32;
+      const int ks_h = l.hid ? 2 * NB : 0, ks_e = l.enc ? ke / 16 : 0;
+      auto frag = [&](int s2, int ib) {
+        for (int lane = 0; lane < 64; ++lane) {
+          const int i = lane & 31, hf = lane >> 5;
+          for (int j = 0; j < 8; ++j) {
+            const int col = s2 < ks_h ? 32 * (s2 >> 1) + 16 * (s2 & 1) + 8 * (j >> 2) + 4 * hf + (j & 3)
+                                      : col_slot(l, 16 * (s2 - ks_h) + 8 * hf + j);
+            const int k = idx(l, 32 * ib + i, col);
+            map.push_back(k < 0 ? -1 : (k | ((int)li << kSplitIdxBits)));
+          }
+        }
+      };
+      if (is_init || is_out || NB % kRingRB != 0) {
+        for (int ib = 0; ib < nrb; ++ib)
+          for (int s2 = 0; s2 < ks_h + ks_e; ++s2) frag(s2, ib);
+      } else {
+        for (int c = 0; c < nrb / kRingRB; ++c)
+          for (int s2 = 0; s2 < ks_h + ks_e; ++s2)
+            for (int b = 0; b < kRingRB; ++b) frag(s2, kRingRB * c + b);
+      }
+    }
+    end();
+    begin((void*)md.bias16, SEC_R16_BIAS);
+    for (size_t li = 0; li < ls.size(); ++li)
+      for (int r = 0; r < md.bias16_stride; ++r)
+        map.push_back(r < ls[li].R ? (int)((ls[li].boff + r) | ((int64_t)li << kSplitIdxBits)) : -1);
+    end();
+  }
   // the single-MLP FP32 row program of nrt_mlp_forward on the ring engine (nrt_shade_ring.hip)
   {
     std::vector<int> smap, bmap;
@@ -313,5 +362,6 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
   }
   m->refreshed = true;
   m->split_refreshed = m->n_src < (1 << kSplitIdxBits);
+  m->ring16_refreshed = m->split_refreshed;  // the same condition gates both tagged walks
   return NRT_OK;
 }

@@ -42,6 +42,7 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
   // 1. FP16 march + scan, flagging
   MarchArgs m16 = ma;
   m16.refine_d = rd;
+  m16.drift_model = (int)option(OPT_MIXED_DRIFT);
   m16.amb = amb;
   m16.keys2 = scan ? keys2 : nullptr;
   if (int rc = ring_march16_launch(s, rays, P, m16, t, thr, keys, st, false)) return rc;

@@ -176,9 +176,12 @@ def test_ring32_independent_of_grid_size():
         assert torch.equal(it.p, base.p) and torch.equal(it.n, base.n)
 
 
-def test_ring32_after_device_refresh_matches_fresh_pack():
-    """nrt_mlp_refresh re-gathers stream32 / bias32 on the device: a handle refreshed to new
-    weights marches exactly like a handle packed from them on the host."""
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp32-split", "mixed"])
+def test_ring32_after_device_refresh_matches_fresh_pack(prec):
+    """nrt_mlp_refresh re-gathers stream32 / bias32, the split stream and the FP16 ring stream
+    (folded, rounded to f16) on the device: a handle refreshed to new weights marches exactly like
+    a handle packed from them on the host, at every precision (fp16 / mixed: the FP16 ring march
+    of a training loop, which refused refreshed handles before round 4)."""
     import ctypes
     from neural_raytracing_amd import _lib
     from neural_raytracing_amd.pathtracer._handles import train_handle, mlp_handle
@@ -203,11 +206,26 @@ def test_ring32_after_device_refresh_matches_fresh_pack():
             c.shape[0], c.data_ptr(), r.data_ptr(), t.data_ptr(), 32.0, h.value, ctypes.byref(sh)),
             "nrt_sdf_create_sphere_blob")
         try:
-            outs.append(_intersect_raw(sh, rays, max_steps=64))
+            _lib.profile_reset()
+            _lib.profile_enable(True)
+            outs.append(_intersect_raw(sh, rays, max_steps=64,
+                                       precision=_lib._PRECISIONS[prec]))
+            _lib.profile_enable(False)
+            if prec in ("fp16", "mixed"):  # both handles on the FP16 ring march
+                assert _lib.profile_read("k_march16")[1] >= 1
         finally:
             _lib.load().nrt_sdf_destroy(sh)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    if prec in ("fp32", "fp16"):
+        for a, b in zip(outs[0], outs[1]):
+            assert torch.equal(a, b)
+    else:
+        # the split stream keeps its pack-time per-layer scales across refreshes (they only keep
+        # the lo halves normal), so the hi / lo halves -- not the products -- differ from a fresh
+        # pack's in the last bits
+        (t, h, p, n, thr), (t2, h2, p2, n2, thr2) = outs
+        assert torch.equal(h, h2)
+        assert (t - t2).abs().max().item() <= 1e-5 and (p - p2).abs().max().item() <= 1e-5
+        assert (n - n2).abs().max().item() <= 1e-4 and (thr - thr2).abs().max().item() <= 1e-2
 
 
 @pytest.mark.parametrize("n", [1, 15, 16, 17, 511, 3001])

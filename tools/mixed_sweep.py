@@ -20,6 +20,7 @@ def main():
     ds = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1200]
     ss = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2000]
     rs = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1]
+    ms = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0]
     dev = torch.device("cuda", 0)
     _lib.load(require_device=True)
     nra.set_precision("fp32")
@@ -32,8 +33,9 @@ def main():
                      size, range(size), background=0.0, with_noise=1e-3, device=dev)
     with torch.no_grad():
         want, rhit, rt = bench._frame_state(rr, 1234)
-        for d, s, r in [(d, s, r) for r in rs for d in ds for s in ss]:
+        for d, s, r, mdl in [(d, s, r, mdl) for mdl in ms for r in rs for d in ds for s in ss]:
             if True:
+                _lib.set_option("mixed_drift", mdl)
                 _lib.set_option("mixed_restart", r)
                 _lib.set_option("mixed_refine_d", d)
                 _lib.set_option("mixed_refine_s", s)
@@ -46,7 +48,7 @@ def main():
                                            rt.cpu())
                 both = (hit & rhit).reshape(-1)
                 dt = (t - rt).abs().reshape(-1)[both]
-                rec = {"refine_d": d, "refine_s": s, "restart": r, "frame_ms": 1000 * el / 3,
+                rec = {"refine_d": d, "refine_s": s, "restart": r, "drift_model": mdl, "frame_ms": 1000 * el / 3,
                        **{k + "_ms": v[0] / max(v[1], 1) for k, v in ks.items()},
                        "evals": evals, "dt_q": torch.quantile(dt.float()[: 1 << 20], torch.tensor(
                            [0.5, 0.9, 0.99, 0.999], device=dt.device)).tolist(), **acc}
