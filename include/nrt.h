@@ -473,6 +473,9 @@ int nrt_profile_evals(uint64_t* evals);
  *   "mixed_drift"    0  1: the flag bound is d * (1 + a per-ray drift estimate built from the
  *                      ratio of consecutive step values) instead of d * (1 + step/16); measured
  *                      to flag more rays for the same accuracy (152 vs 133 ms), kept for A/B
+ *   "ring_occlusion" 1  shadow rays (nrt_sdf_occlusion, the shadowed shading entries) march on
+ *                      the ring engine of the precision (k_occl16 / k_occl32 / k_occl3); 0: the
+ *                      per-wave k_occlusion; same visibility bar either way
  *   "mixed_refine_s" 2000 NRT_MIXED: sdf(best) re-evaluates the scan's runner-up when the FP16
  *                      minimum and runner-up lie within s (1e-7 units)
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.

@@ -306,8 +306,29 @@ int nrt_sdf_intersect(const nrt_sdf* s, const float* rays, int64_t P, const nrt_
 namespace nrt {
 // shadow march over rays[0, P) (or [0, *count) when count is a device counter)
 int launch_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const int32_t* count,
-                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible, bool f16,
-                     hipStream_t st) {
+                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible,
+                     int precision, hipStream_t st) {
+  const bool f16 = precision == NRT_FP16;
+  if (option(OPT_RING_OCCLUSION) != 0) {
+    MarchArgs ma{};
+    ma.max_steps = max_steps;
+    ma.eps = eps;
+    ma.max_t = 0.f;  // unused: each ray stops at its own distance to the light (occ_max_t)
+    ma.primary = 0;
+    ma.count = count;
+    ma.occ_max_t = max_t;
+    ma.evals = profile_eval_counter();
+    if (f16 && ring_supported(s) && option(OPT_RING16) != 0) {
+      ProfScope prof("k_occlusion", st);
+      return ring_march16_launch(s, rays, P, ma, nullptr, nullptr, nullptr, st, false, visible);
+    }
+    if (!f16 && ring32_supported(s) && option(OPT_RING32) != 0) {
+      ProfScope prof("k_occlusion", st);
+      const bool split = (precision == NRT_FP32_SPLIT || precision == NRT_MIXED) && ring3_supported(s);
+      return split ? ring3_launch(s, rays, P, ma, nullptr, nullptr, nullptr, st, 4, visible)
+                   : ring_occlusion32(s, rays, P, ma, visible, st);
+    }
+  }
   int hidden, ke;
   sdf_dims(s, hidden, ke);
   LdsPlan lp = plan_lds(hidden, ke, 1, f16, false);
@@ -334,8 +355,8 @@ int nrt_sdf_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const floa
   if (!s || P < 0) { set_error("nrt_sdf_occlusion: bad argument"); return NRT_EINVAL; }
   if (P == 0) return NRT_OK;
   if (!rays || !max_t || !visible) { set_error("nrt_sdf_occlusion: null argument"); return NRT_EINVAL; }
-  return launch_occlusion(s, rays, P, nullptr, max_t, max_steps, eps, visible,
-                          precision == NRT_FP16, (hipStream_t)stream);
+  return launch_occlusion(s, rays, P, nullptr, max_t, max_steps, eps, visible, precision,
+                          (hipStream_t)stream);
 }
 
 int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi, void* stream) {

@@ -204,7 +204,6 @@ int shade_shadowed_impl(const char* who, const nrt_bsdf* b, const nrt_light* l, 
   }
   if (P == 0) return NRT_OK;
   hipStream_t st = (hipStream_t)stream;
-  const bool f16 = precision == NRT_FP16;
   char* ws = (char*)workspace;
   size_t off = 0;
   auto take = [&](size_t bytes) { char* q = ws + off; off += align256(bytes); return q; };
@@ -218,7 +217,8 @@ int shade_shadowed_impl(const char* who, const nrt_bsdf* b, const nrt_light* l, 
   const dim3 grid(std::min<int64_t>(ceil_div64(P, 256), 1024)), block(256);
   k_point_shadow_rays<><<<grid, block, 0, st>>>(l->dev, p, hit_idx, hit_count, rays, max_t);
   if (int rc = check_launch("k_point_shadow_rays")) return rc;
-  if (int rc = launch_occlusion(s, rays, P, hit_count, max_t, max_steps, eps, vis, f16, st)) return rc;
+  if (int rc = launch_occlusion(s, rays, P, hit_count, max_t, max_steps, eps, vis, precision, st))
+    return rc;
   if (occ) {
     // occ(occ_rays) over the P list slots (rows past *hit_count are never read back)
     k_occ_inputs<><<<grid, block, 0, st>>>(p, hit_idx, hit_count, rays, occ_in);

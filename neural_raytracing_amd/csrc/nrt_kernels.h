@@ -282,6 +282,9 @@ struct MarchArgs {
   const unsigned long long* start = nullptr;
   const int32_t* list = nullptr;
   const int32_t* count = nullptr;
+  // shadow march (march_body mode 3): each ray's distance to the light; `count` (device) bounds
+  // the compacted ray list
+  const float* occ_max_t = nullptr;
 };
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
@@ -576,8 +579,9 @@ __device__ __forceinline__ void march_body(
   const int64_t w = (int64_t)blockIdx.x * WV + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // a refinement launch works through the first *count entries of a ray list
   const int64_t Pe =
-      (MX && a.count) ? (int64_t)__builtin_amdgcn_readfirstlane(*(const NRT_GLOBAL int32_t*)a.count)
-                      : P;
+      ((MX || MODE == 3) && a.count)
+          ? (int64_t)__builtin_amdgcn_readfirstlane(*(const NRT_GLOBAL int32_t*)a.count)
+          : P;
   const OwnedRays own(Pe, nw, w, WV, a.xcd_lines != 0);
   const int64_t R = own.R;  // rays owned by this wave
   const bool scan = mode == 0 && a.primary;
@@ -601,11 +605,19 @@ __device__ __forceinline__ void march_body(
   bool ended = false, hit = false, whole = false;
   unsigned long long ambs = ~0ull;  // NRT_MIXED: the first undecidable step's (i, t), or none
   float drift = 0.f, dprev = 1.f;   // NRT_MIXED: t's drift bound (units of the FP16 error)
+  float mt = 0.f;                   // mode 3: the ray's distance to the light
   int64_t cursor = 0;  // wave-uniform
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
     for (;;) {
-      if (kind == 0) {
+      if (mode == 3 && kind == 0) {
+        // intersect_test (sdfs.py:162-181): visible = t >= max_t | live after max_steps.  t only
+        // grows, so a march past the light is decided (visible) and stops there
+        if (ended || i >= a.max_steps || t >= mt) {
+          if (lane < RPW) hit_out[ray] = (t >= mt || !hit) ? 1 : 0;
+          kind = -1;
+        }
+      } else if (kind == 0) {
         // sdfs.py:119-131: a march ends on a hit, when t leaves [0, max_t) or after max_steps
         if (ended || !(t < a.max_t) || i >= a.max_steps) {
           if (MX && lane < RPW && a.amb && ambs != ~0ull) a.amb[ray] = ambs;
@@ -700,6 +712,10 @@ __device__ __forceinline__ void march_body(
             }
           } else if (seg < 0) {
             kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull; drift = 0.f;
+            if (mode == 3) {  // shadow rays start 100 eps out (sdfs.py:170)
+              t = 0.f + 1e2f * a.eps;
+              mt = a.occ_max_t[ray];
+            }
             if (MX && a.start) {
               const unsigned long long s0 = a.start[ray];
               t = __uint_as_float((uint32_t)s0);
@@ -760,8 +776,15 @@ __device__ __forceinline__ void march_body(
           ambs = ((unsigned long long)(uint32_t)i << 32) | __float_as_uint(t);
         dprev = d;
       }
-      if (d <= a.eps) { hit = true; ended = true; }
-      else t = t + d;
+      if (mode == 3) {  // sdfs.py:175-179: t advances on the hit step too, the test is strict
+        const bool now = d < a.eps;
+        t = t + d;
+        if (now) { hit = true; ended = true; }
+      } else if (d <= a.eps) {
+        hit = true; ended = true;
+      } else {
+        t = t + d;
+      }
       ++i;
     } else if (kind == 1) {
       // sdfs.py:246-248: idx = where(s < m, i + 1, idx); m = min(m, s)
@@ -802,6 +825,19 @@ __global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_march16(NRT_MARCH
 template <int NB, int NE, int WV, bool FOLD>
 __global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_scan_best16(NRT_MARCH_ARGS) {
   march_body<RingPol16<NB, NE, WV, FOLD>, 1>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+// shadow march (intersect_test) on each ring engine: visible -> hit_out
+template <int NB, int NE, int WV, bool FOLD>
+__global__ void __launch_bounds__(64 * WV, WV >= 16 ? 1 : 2) k_occl16(NRT_MARCH_ARGS) {
+  march_body<RingPol16<NB, NE, WV, FOLD>, 3>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+template <int KH, int KE, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_occl32(NRT_MARCH_ARGS) {
+  march_body<RingPol32<KH, KE, WV, ACT>, 3>(s, m, rays, P, a, NRT_MARCH_PASS);
+}
+template <int KH, int KQ, int WV, int ACT>
+__global__ void __launch_bounds__(64 * WV, 1) k_occl3(NRT_MARCH_ARGS) {
+  march_body<RingPol3<KH, KQ, WV, ACT>, 3>(s, m, rays, P, a, NRT_MARCH_PASS);
 }
 // FP32 (reference precision): one block of WV waves per CU (the ring takes most of the LDS), two
 // waves per SIMD

@@ -31,6 +31,7 @@ enum Option {
   OPT_MIXED_S,         // "mixed_refine_s" (1e-7 units)
   OPT_MIXED_RESTART,   // "mixed_restart"
   OPT_MIXED_DRIFT,     // "mixed_drift"
+  OPT_RING_OCCLUSION,  // "ring_occlusion"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -150,10 +151,11 @@ int ring_dispatch(const nrt_sdf* s, F&& f) {
 int ring_march(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                int32_t* cnt, unsigned long long* keys, hipStream_t st);
-// k_march16 alone (packed t, scan keys; the caller initialises keys): NRT_MIXED's first pass
+// k_march16 alone (packed t, scan keys; the caller initialises keys): NRT_MIXED's first pass;
+// with `visible`, the shadow march k_occl16 instead (MarchArgs::occ_max_t / count)
 int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
                         float* t, float* thr, unsigned long long* keys, hipStream_t st,
-                        bool best16);
+                        bool best16, uint8_t* visible = nullptr);
 
 // ---- FP32 ring engine (nrt_ring_march32.hip) ----
 // SDF MLPs with a compiled FP32 ring kernel: hidden 128 / 256, F = 16 / 32 with 3 inputs and no
@@ -194,9 +196,14 @@ int ring_march3(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs&
                 uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                 int32_t* cnt, unsigned long long* keys, hipStream_t st);
 // the split engine's launches alone: which = 0 k_march3 (+ k_scan_best3 when primary), 1
-// k_scan_best3 (the caller initialises keys); 2 / 3 the same as NRT_MIXED's refinement passes
+// k_scan_best3 (the caller initialises keys); 2 / 3 the same as NRT_MIXED's refinement passes;
+// 4 the shadow march k_occl3 (visible -> hit)
 int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
-                 float* thr, unsigned long long* keys, hipStream_t st, int which);
+                 float* thr, unsigned long long* keys, hipStream_t st, int which,
+                 uint8_t* hit = nullptr);
+// the FP32 ring's shadow march k_occl32
+int ring_occlusion32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                     uint8_t* visible, hipStream_t st);
 // NRT_MIXED intersect (nrt_ring_mixed.hip): FP16 march + scan, split refinement of the
 // undecidable steps and scan orders, split sdf(best); same outputs as ring_march
 // The FP16 SDF error of the headline scene (tools/fp16_decompose.py, 1M scan points and the
@@ -222,9 +229,11 @@ int ring_normals32(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
                  float* n, float* p_io, float eps, hipStream_t st);
 
+// shadow march (intersect_test) on the ring engine of `precision` (FP16 ring, FP32 ring, split
+// ring for fp32-split / mixed), or the per-wave k_occlusion where no ring kernel is compiled
 int launch_occlusion(const nrt_sdf* s, const float* rays, int64_t P, const int32_t* count,
-                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible, bool f16,
-                     hipStream_t st);
+                     const float* max_t, int32_t max_steps, float eps, uint8_t* visible,
+                     int precision, hipStream_t st);
 
 // ---- shading programs (nrt_prog.hip) ----
 int build_program(const std::vector<const nrt_mlp*>& mlps, nrt_prog& out);

@@ -6,7 +6,7 @@ namespace nrt {
 
 int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
                         float* t, float* thr, unsigned long long* keys, hipStream_t st,
-                        bool best16) {
+                        bool best16, uint8_t* visible) {
   const size_t bias_bytes = ring_bias_bytes(s);
   int dev = 0, cus = 0;
   NRT_HIP(hipGetDevice(&dev));
@@ -37,10 +37,12 @@ int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const Ma
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, a, t, nullptr, nullptr, nullptr, nullptr, thr, keys);
+          s->host_dev, s->mlp->host_dev, rays, P, a, t, visible, nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
-    // NRT_MIXED's flagging march is its own instantiation (the plain one carries none of it)
+    // the shadow march (visible != nullptr) and NRT_MIXED's flagging march are their own
+    // instantiations (the plain march carries none of them)
+    if (visible) return launch(k_occl16<NB, NE, kRingWaves, FOLD>, "k_occl16");
     if (ma.amb) return launch(k_march16<NB, NE, kRingWaves, FOLD, true>, "k_march16");
     if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
     if (scan && best16) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");

@@ -39,7 +39,7 @@ int ring_eval3(const nrt_sdf* s, const float* pts, int64_t M, float* out, hipStr
 }
 
 int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
-                 float* thr, unsigned long long* keys, hipStream_t st, int which) {
+                 float* thr, unsigned long long* keys, hipStream_t st, int which, uint8_t* hit) {
   const MlpDev& md = s->mlp->host_dev;
   const size_t extra = (size_t)md.freqs * 16 + ring32_bias_bytes(s) + ring32_sphere_bytes(s);
   int dev = 0, cus = 0;
@@ -58,11 +58,12 @@ int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
       ProfScope prof(name, st);
       // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, nullptr,
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit,
                                                      nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     // profile names: the NRT_MIXED refinement launches (which 2 / 3) apart from the plain ones
+    if (which == 4) return launch(k_occl3<KH, KQ, WV, ACT>, "k_occl3");
     if (which == 2) return launch(k_march3<KH, KQ, WV, ACT, true>, "k_refine3");
     if (which == 3) return launch(k_scan_best3<KH, KQ, WV, ACT, true>, "k_best3");
     if (which == 0)

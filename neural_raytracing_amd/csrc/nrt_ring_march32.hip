@@ -6,7 +6,8 @@
 namespace nrt {
 
 // which = 0: march + scan (k_march32, then k_scan_best32 when primary); 1: k_scan_best32 alone
-// at the argmins already in `keys` (an FP16 march's scan, option "scan_best32")
+// at the argmins already in `keys` (an FP16 march's scan, option "scan_best32"); 2: the shadow
+// march k_occl32 (visible -> hit)
 static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
                          float* t, uint8_t* hit, float* p, float* n, float* raw_n, float* thr,
                          unsigned long long* keys, hipStream_t st, int which) {
@@ -33,6 +34,7 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
                                                      nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
+    if (which == 2) return launch(k_occl32<KH, KE, WV, ACT>, "k_occl32");
     if (which == 0)
       if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32")) return rc;
     if (scan) return launch(k_scan_best32<KH, KE, WV, ACT>, "k_scan_best32");
@@ -51,6 +53,12 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
   }
 #undef NRT_R32
   return rc;
+}
+
+int ring_occlusion32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
+                     uint8_t* visible, hipStream_t st) {
+  return ring32_launch(s, rays, P, ma, nullptr, visible, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, st, 2);
 }
 
 int ring_scan_best32(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma,
