@@ -49,10 +49,14 @@ def _composite(out, values, mask, background, xs, ys, chunk, trim=0):
 
 def _fused(integrator, cameras, w_isect, addition):
     """Direct / NeRFIntegrator(Direct) tiles go through the fused kernels when nothing needs the
-    interaction record (addition is the default `nothing`)."""
-    if addition is not nothing or w_isect not in (None, False) or not hasattr(cameras, "rays_tile"):
+    interaction record (addition is the default `nothing`); with w_isect (a shadow ray or a
+    learned occlusion MLP, integrators.py:161-166) the tuple carries it to render_tiles."""
+    if addition is not nothing or not hasattr(cameras, "rays_tile"):
         return None
-    return fused_integrator(integrator)
+    fused = fused_integrator(integrator)
+    if fused is None or w_isect in (None, False):
+        return fused
+    return tuple(fused) + (w_isect,)
 
 
 def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=None, height=None,

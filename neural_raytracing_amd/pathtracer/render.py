@@ -13,7 +13,7 @@ import torch
 
 from .. import _lib
 from .integrators import Direct, NeRFIntegrator
-from .integrators.integrators import _bsdf_handle, _light_handle
+from .integrators.integrators import _bsdf_handle, _emitter_mode, _light_handle
 from .shapes.sdfs import sdf_handle
 
 
@@ -56,10 +56,12 @@ def _buffers(P, nb, device):
     return b
 
 
-def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None):
+def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None, w_isect=False):
     """Run intersect + shade on flat rays [P,6]; returns the buffer set (rgb zero on misses).
     scan_groups: for batched tiles, the number of tiles G; ray r belongs to tile r // (P // G)
-    and each tile draws its own scan jitter (random.random(), sdfs.py:236), in tile order."""
+    and each tile draws its own scan jitter (random.random(), sdfs.py:236), in tile order.
+    w_isect: Direct's emitter sample with a shadow ray (True) or a learned occlusion MLP, as
+    Direct.sample picks it (integrators.py:161-166)."""
     P = rays_flat.shape[0]
     dev = rays_flat.device
     nb = len(getattr(bsdf, "bsdfs", [bsdf]))
@@ -92,6 +94,14 @@ def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None):
     if not primary:
         b.thr.zero_()
     b.rgb.zero_()
+    shadow, occ = _emitter_mode(w_isect)
+    if shadow:
+        # nrt_shade_direct_shadowed / _learned_occ over the batch's hit list: the shadow march
+        # runs on the ring engines once for every tile of the batch
+        args = (_lib.ptr(b.p), _lib.ptr(b.n), _lib.ptr(b.wi), _lib.ptr(b.hit_idx),
+                _lib.ptr(b.hit_count), P, _lib.ptr(b.rgb), None)
+        Direct._shade(shapes, bsdf, lights, shadow, occ, args, P, dev)
+        return b
     _lib.call("nrt_shade_direct", _bsdf_handle(bsdf), _light_handle(lights), _lib.ptr(b.p),
               _lib.ptr(b.n), _lib.ptr(b.wi), _lib.ptr(b.hit_idx), _lib.ptr(b.hit_count), P,
               _lib.ptr(b.rgb), None, _lib.precision_code(), s)
@@ -130,7 +140,8 @@ def render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk, size, 
     keeps its own scan jitter (nrt_march_params.scan_max_t_groups) -- and composited tile by
     tile.  Equal to rendering the tiles one at a time; the GPU sees up to MAX_BATCH_RAYS rays per
     launch instead of chunk_size^2."""
-    direct, with_alpha = fused
+    direct, with_alpha = fused[:2]
+    w_isect = fused[2] if len(fused) > 2 else False  # pathtrace's w_isect (main.py _fused)
     N = len(cameras)
     per_tile = N * chunk * chunk
     dev = out.device
@@ -141,7 +152,7 @@ def render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk, size, 
         for k, (x0, y0) in enumerate(batch):
             rays[k] = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise).reshape(-1, 6)
         b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights,
-                           scan_groups=len(batch) if len(batch) > 1 else None)
+                           scan_groups=len(batch) if len(batch) > 1 else None, w_isect=w_isect)
         for k, (x0, y0) in enumerate(batch):
             sl = slice(k * per_tile, (k + 1) * per_tile)
             _lib.call("nrt_composite", _lib.ptr(b.rgb[sl]), _lib.ptr(b.thr[sl]), _lib.ptr(b.hit[sl]),

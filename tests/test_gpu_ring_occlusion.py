@@ -111,3 +111,36 @@ def test_ring_shadow_march_empty_and_far_light():
     slab = _visible(shape, rays, far, "fp32", False)
     assert int((ring != slab).sum()) <= max(1, 0.005 * ring.numel())
     assert math.isfinite(float(dist.max()))
+
+
+@pytest.mark.parametrize("prec", ["fp32", "mixed"])
+@pytest.mark.parametrize("mode", ["direct", "nerf", "occ"])
+def test_fused_shadowed_tiles_match_integrator_path(prec, mode):
+    """pathtrace(..., w_isect=True | <occlusion MLP>) now renders on the fused tile path (every
+    tile of a batch in one intersect + shadowed-shading chain, render.direct_kernels); it must
+    equal the per-tile integrator path (forced by an `addition` hook, main.py _fused) pixel for
+    pixel: same rays, same scan draws, same kernels per ray."""
+    import random
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
+    from tests.test_gpu_parity import _occ_pair, _shadow_scene
+    _, mine = _shadow_scene()
+    w = _occ_pair(1)[1] if mode == "occ" else True
+    integ = NeRFIntegrator(Direct()) if mode == "nerf" else Direct()
+    set_precision(prec)
+    outs = []
+    for hook in (None, lambda it: None):
+        random.seed(21)
+        kw = {} if hook is None else {"addition": hook}
+        with torch.no_grad():
+            img, _ = pt.pathtrace(mine["shape"], mine["lights"], mine["camera"], integ,
+                                  bsdf=mine["bsdf"], size=64, chunk_size=32, bundle_size=1,
+                                  background=0.5, with_noise=0.0, w_isect=w, **kw)
+        outs.append(img.cpu())
+    set_precision("fp32")
+    fused, plain = outs
+    err = (fused - plain).abs().max().item()
+    report(f"fused_shadowed_tiles[{prec},{mode}]", pixels=fused[..., 0].numel(), maxabs=err)
+    assert fused.shape == plain.shape
+    assert err <= 1e-6, err
