@@ -133,6 +133,24 @@ def _check_versions(ctx):
                            "(e.g. optimizer.step()) between this graph's forward and backward")
 
 
+# A backward compacts its rows to those whose incoming gradient is not all zero when that drops
+# at least this fraction of them: a zero row adds exactly nothing to any weight or bias gradient
+# and its dL/dx is 0.  Under the reference's masks (Direct.sample zeroes missed rays' shading,
+# integrators.py:167-189; ComposeSpatialVarying weights every ray, bsdfs.py:515-536) the shading
+# MLPs of a training step see dY = 0 on every ray that missed.
+COMPACT_MIN_DEAD = 0.1
+
+
+def _live_rows(dys, M):
+    """Indices of the rows with a nonzero (or NaN) incoming gradient in any output, or None when
+    compaction would not pay (one host synchronisation per backward call)."""
+    live = (dys[0] != 0).any(-1)
+    for d in dys[1:]:
+        live |= (d != 0).any(-1)
+    idx = torch.nonzero(live).reshape(-1)
+    return None if idx.numel() > (1.0 - COMPACT_MIN_DEAD) * M else idx
+
+
 class _MlpFn(torch.autograd.Function):
     """y = SkipConnMLP(x, latent) with gradients for x, latent and every nn.Linear weight and
     bias from nrt_mlp_backward.  basis_p is a plain tensor attribute in the
@@ -167,18 +185,32 @@ class _MlpFn(torch.autograd.Function):
         lib = _lib.load(require_device=True)
         M = x.shape[0]
         dy = dy.float().contiguous()
+        lins = mlp._linears()
+        idx = _live_rows([dy], M)
+        if idx is not None:  # the rows with a gradient only (COMPACT_MIN_DEAD)
+            full_x, full_lat = x, lat
+            x, dy = x[idx].contiguous(), dy[idx].contiguous()
+            lat = None if lat is None else lat[idx].contiguous()
+            M = x.shape[0]
         dx = torch.empty_like(x) if ctx.needs_input_grad[1] else None
         dlat = torch.empty_like(lat) if (lat is not None and ctx.needs_input_grad[2]) else None
-        lins = mlp._linears()
-        dws = [torch.empty_like(lin.weight) if lin.weight.requires_grad else None for lin in lins]
-        dbs = [torch.empty_like(lin.bias) if lin.bias.requires_grad else None for lin in lins]
+        zeros = M == 0
+        mk = torch.zeros_like if zeros else torch.empty_like
+        dws = [mk(lin.weight) if lin.weight.requires_grad else None for lin in lins]
+        dbs = [mk(lin.bias) if lin.bias.requires_grad else None for lin in lins]
         wp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dws])
         bp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dbs])
-        ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(ctx.handle.value, M),
-                         dtype=torch.uint8, device=x.device)
-        _lib.call("nrt_mlp_backward", ctx.handle.value, _lib.ptr(x), _lib.ptr(lat), M,
-                  _lib.ptr(dy), _lib.ptr(dx), _lib.ptr(dlat), wp, bp, _lib.ptr(ws),
-                  _lib.stream())
+        if not zeros:
+            ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(ctx.handle.value, M),
+                             dtype=torch.uint8, device=x.device)
+            _lib.call("nrt_mlp_backward", ctx.handle.value, _lib.ptr(x), _lib.ptr(lat), M,
+                      _lib.ptr(dy), _lib.ptr(dx), _lib.ptr(dlat), wp, bp, _lib.ptr(ws),
+                      _lib.stream())
+        if idx is not None:  # scatter back: dL/dx = 0 on the rows without a gradient
+            if dx is not None:
+                dx = torch.zeros_like(full_x).index_copy_(0, idx, dx)
+            if dlat is not None:
+                dlat = torch.zeros_like(full_lat).index_copy_(0, idx, dlat)
         grads = [g for pair in zip(dws, dbs) for g in pair]
         return (None, dx, dlat, *grads)
 
@@ -236,12 +268,20 @@ class _MultiMlpFn(torch.autograd.Function):
         mlps, n, M = ctx.mlps, len(ctx.mlps), x.shape[0]
         lib = _lib.load(require_device=True)
         dys = [dy.float().contiguous() for dy in dys]
+        idx = _live_rows(dys, M)
+        if idx is not None:  # the rows where any of the MLPs has a gradient (COMPACT_MIN_DEAD)
+            full_x = x
+            x = x[idx].contiguous()
+            dys = [dy[idx].contiguous() for dy in dys]
+            M = x.shape[0]
+        zeros = M == 0
+        mk = torch.zeros_like if zeros else torch.empty_like
         dx = torch.empty(n, M, x.shape[1], device=x.device) if ctx.needs_input_grad[1] else None
         grads, wptr, bptr = [], [], []
         for m in mlps:
             for lin in m._linears():
-                dw = torch.empty_like(lin.weight) if lin.weight.requires_grad else None
-                db = torch.empty_like(lin.bias) if lin.bias.requires_grad else None
+                dw = mk(lin.weight) if lin.weight.requires_grad else None
+                db = mk(lin.bias) if lin.bias.requires_grad else None
                 grads += [dw, db]
                 wptr.append(0 if dw is None else dw.data_ptr())
                 bptr.append(0 if db is None else db.data_ptr())
@@ -250,11 +290,15 @@ class _MultiMlpFn(torch.autograd.Function):
         dyp = (P * n)(*[d.data_ptr() for d in dys])
         dxp = None if dx is None else (P * n)(*[dx[i].data_ptr() for i in range(n)])
         wp, bp = (P * len(wptr))(*wptr), (P * len(bptr))(*bptr)
-        ws = torch.empty(lib.nrt_mlp_backward_multi_workspace_bytes(hs, n, M), dtype=torch.uint8,
-                         device=x.device)
-        _lib.call("nrt_mlp_backward_multi", hs, n, _lib.ptr(x), M, dyp, dxp, wp, bp,
-                  _lib.ptr(ws), _lib.stream())
-        return (None, None if dx is None else dx.sum(0), *grads)
+        if not zeros:
+            ws = torch.empty(lib.nrt_mlp_backward_multi_workspace_bytes(hs, n, M),
+                             dtype=torch.uint8, device=x.device)
+            _lib.call("nrt_mlp_backward_multi", hs, n, _lib.ptr(x), M, dyp, dxp, wp, bp,
+                      _lib.ptr(ws), _lib.stream())
+        dxs = None if dx is None else (dx.sum(0) if not zeros else torch.zeros_like(x))
+        if idx is not None and dxs is not None:
+            dxs = torch.zeros_like(full_x).index_copy_(0, idx, dxs)
+        return (None, dxs, *grads)
 
 
 def input_gradient(mlp, x):

@@ -92,6 +92,58 @@ def test_mlp_backward_matches_autograd(name, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dead", [0.6, 1.0])
+@pytest.mark.parametrize("name", ["sp_var_16x256_F128", "latent_4x32", "neural_bsdf_6x96_F64"])
+def test_mlp_backward_compacts_zero_gradient_rows(name, dead):
+    """A backward whose dY is zero on most rows (the missed rays of a masked training step) runs
+    on the rows with a gradient only (neural_blocks.COMPACT_MIN_DEAD); the gradients still match
+    float64 autograd over all rows, dL/dx (and dL/dlatent) is 0 on the dropped rows, and an
+    all-zero dY gives all-zero gradients.  The mixture's multi-MLP backward the same way."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer import neural_blocks as nb
+    kw = SHAPES[name]
+    M = 1500
+    ref, mine = _pair(kw, 77)
+    set_precision("fp32")
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(M, kw["in_size"], generator=g) - 0.5)
+    lat = torch.randn(M, kw["latent_size"], generator=g) if kw.get("latent_size") else None
+    dy = torch.randn(M, kw["out"], generator=g)
+    dy[torch.rand(M, generator=g) < dead] = 0.0
+    want = _grads(ref, x, lat, dy, torch.float64)
+    ref32 = _grads(ref, x, lat, dy, torch.float32)
+    xm = x.cuda().requires_grad_(True)
+    lm = lat.cuda().requires_grad_(True) if lat is not None else None
+    (mine(xm, lm) * dy.cuda()).sum().backward()
+    got = {"dx": xm.grad}
+    if lat is not None:
+        got["dlatent"] = lm.grad
+    for i, a in enumerate(mine._linears()):
+        got[f"dW[{i}]"] = a.weight.grad
+        got[f"db[{i}]"] = a.bias.grad
+    for k in want:
+        _close(got[k], want[k], ref32[k], k)
+    dead_rows = (dy == 0).all(-1)
+    assert torch.equal(xm.grad.cpu()[dead_rows], torch.zeros_like(x[dead_rows]))
+    if dead == 1.0:
+        assert all(float(v.abs().max()) == 0.0 for v in got.values())
+    if lat is None:  # the multi-MLP backward (two copies of the MLP on one input)
+        from neural_raytracing_amd.pathtracer.neural_blocks import mlp_multi
+        mine2 = _pair(kw, 78)[1]
+        xm2 = x.cuda().requires_grad_(True)
+        ys = mlp_multi([mine, mine2], xm2)
+        for q in list(mine.parameters()) + list(mine2.parameters()):
+            q.grad = None
+        (ys[0] * dy.cuda()).sum().backward()  # mine2's output unused: its dY is all zero
+        for i, a in enumerate(mine._linears()):
+            _close(a.weight.grad, want[f"dW[{i}]"], ref32[f"dW[{i}]"], f"multi dW[{i}]")
+        _close(xm2.grad, want["dx"], ref32["dx"], "multi dx")
+        for a in mine2._linears():
+            assert a.weight.grad is None or float(a.weight.grad.abs().max()) == 0.0
+    assert nb.COMPACT_MIN_DEAD < 0.6
+
+
+@pytest.mark.gpu
 def test_mlp_training_steps_reduce_loss():
     """A few Adam steps of an 8x64 SkipConnMLP fitting a smooth target on the HIP path."""
     from neural_raytracing_amd import set_precision
