@@ -27,7 +27,7 @@ fi
 if [ "$STEP" = all ] || [ "$STEP" = scenes ]; then
   rm -f gpurun_out/scenes.jsonl
   for SC in colocate dtu; do
-    for PREC in fp32 fp32-split fp16; do
+    for PREC in fp32 fp32-split mixed fp16; do
       timeout -k 10 300 python -u bench.py --scene $SC --precision $PREC --steps 3 --warmup 1 >> gpurun_out/scenes.jsonl 2> gpurun_out/scene_$SC.err
       rc=$?; echo "SCENE $SC $PREC EXIT $rc"; [ $rc -eq 0 ] || exit $rc
     done
@@ -40,9 +40,11 @@ fi
 if [ "$STEP" = all ] || [ "$STEP" = train ]; then
   timeout -k 10 300 python -u bench.py --scene train --steps 10 --warmup 2 > gpurun_out/train.jsonl 2> gpurun_out/train.err
   rc=$?; echo "TRAIN EXIT $rc"; tail -1 gpurun_out/train.jsonl; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python -u bench.py --scene train --precision mixed --steps 10 --warmup 2 >> gpurun_out/train.jsonl 2>> gpurun_out/train.err
+  rc=$?; echo "TRAIN MIXED EXIT $rc"; tail -1 gpurun_out/train.jsonl; [ $rc -eq 0 ] || exit $rc
   # the kernel trace of a training step is large (every torch op): keep only the stats
   rm -rf /tmp/prof_train
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python3 bench.py --scene train --steps 5 --warmup 1 > gpurun_out/prof_train.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python3 bench.py --scene train --precision mixed --steps 5 --warmup 1 > gpurun_out/prof_train.log 2>&1
   rc=$?; echo "PROF TRAIN EXIT $rc"; [ $rc -eq 0 ] || exit $rc
   mkdir -p gpurun_out/prof_train && find /tmp/prof_train -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_train/ \;
 fi
