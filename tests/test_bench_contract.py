@@ -8,9 +8,9 @@ import pathlib
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 # the round's final line (bench.py with the CPU baseline) and the rocprofv3 --kernel-trace --stats
 # summary of the same frame (bench.py --no-cpu-baseline --no-extra-legs)
-BENCH = ROOT / "profiles" / "r03" / "final" / "bench.json"
-STATS = ROOT / "profiles" / "r03" / "final" / "kernel_stats.csv"
-PEAK = {"fp32": 157.3, "fp16": 2500.0, "fp32-split": 2500.0}
+BENCH = ROOT / "profiles" / "r04" / "final" / "bench.json"
+STATS = ROOT / "profiles" / "r04" / "final" / "kernel_stats.csv"
+PEAK = {"fp32": 157.3, "fp16": 2500.0, "fp32-split": 2500.0, "mixed": 2500.0}
 
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
@@ -20,7 +20,7 @@ REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 def _line():
     import pytest
     if not BENCH.exists():
-        pytest.skip("the round's final bench line is not committed yet (tools/r03_final.sh)")
+        pytest.skip("the round's final bench line is not committed yet (tools/run_gpu_round.sh)")
     return json.loads(BENCH.read_text().strip().splitlines()[-1])
 
 
