@@ -94,11 +94,10 @@ def train_sdf_handle(sdf):
     (``train_handle``: re-packed on the device by nrt_mlp_refresh after each optimiser step) and,
     for a SphereSDF, a sphere table rewritten on the device (nrt_sdf_refresh_spheres) when its
     tensors change -- where ``sdf_handle`` would copy every weight to the host and pack it again
-    each step.  The FP16 ring kernels refuse refreshed handles, so FP16 keeps ``sdf_handle``."""
+    each step.  The refresh re-rounds the FP16 ring stream too (round 4), so every precision
+    marches on it."""
     from ..script_modules import resolve
     s = resolve(sdf)
-    if _lib.precision_code() == _lib.NRT_FP16:
-        return sdf_handle(sdf)
     if isinstance(s, SkipConnMLP):
         th = train_handle(s)
         cached = getattr(s, "_nrt_train_sdf", None)
