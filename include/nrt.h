@@ -159,6 +159,26 @@ int nrt_sdf_eval(const nrt_sdf* sdf, const float* p, int64_t M, float* out, int 
 /* out[M,3] = d sdf / d p  (SDF.autograd_diff, sdfs.py:184-197; f32 backward) */
 int nrt_sdf_grad(const nrt_sdf* sdf, const float* p, int64_t M, float* grad, void* stream);
 
+/* SphereSDF's smooth-min part for training (sdfs.py:37-43, utils.py:386-387; replaces the
+ * torch ops of SphereSDF.forward and of SDF.autograd_diff's create_graph=True gradient,
+ * sdfs.py:184-197, when the points carry no gradient): value[P] = -log(max(sum_i exp(-k sd_i),
+ * 1e-4)) / k with sd_i = |(I + tfs_i) p - c_i| - R_i, and grad[P,3] = d value / d p (either
+ * output may be NULL).  centers [n,3], radii [n], tfs [n,3,3] are the module's device tensors;
+ * n <= 1260. */
+int nrt_sphere_smoothmin_forward(const float* p, int64_t P, const float* centers,
+                                 const float* radii, const float* tfs, int32_t n, float k,
+                                 float* value, float* grad, void* stream);
+/* The backward of both outputs with respect to the sphere parameters (for grad: the double
+ * backward of the normal): dcenters [n,3], dradii [n], dtfs [n,3,3] (each may be NULL) are
+ * overwritten with sum_points dvalue . d value / d theta + dgrad . d grad / d theta; dvalue [P]
+ * and dgrad [P,3] may be NULL (no gradient).  Deterministic (fixed-order sums).
+ * workspace: nrt_sphere_smoothmin_workspace_bytes(P) bytes. */
+size_t nrt_sphere_smoothmin_workspace_bytes(int64_t P);
+int nrt_sphere_smoothmin_backward(const float* p, int64_t P, const float* centers,
+                                  const float* radii, const float* tfs, int32_t n, float k,
+                                  const float* dvalue, const float* dgrad, float* dcenters,
+                                  float* dradii, float* dtfs, void* workspace, void* stream);
+
 typedef struct {
   int32_t max_steps;   /* SDF.max_steps (sdfs.py:96; scripts set 32/64/256)               */
   float epsilon;       /* SDF.epsilon 1e-3                                                 */

@@ -72,6 +72,10 @@ _SIGNATURES = {
     "nrt_sdf_create_sphere_blob": (_I32, [_I32, _P, _P, _P, _F, _P, ctypes.POINTER(_P)]),
     "nrt_sdf_destroy": (_I32, [_P]),
     "nrt_sdf_refresh_spheres": (_I32, [_P, _P, _P, _P, _P]),
+    "nrt_sphere_smoothmin_forward": (_I32, [_P, _I64, _P, _P, _P, _I32, _F, _P, _P, _P]),
+    "nrt_sphere_smoothmin_workspace_bytes": (ctypes.c_size_t, [_I64]),
+    "nrt_sphere_smoothmin_backward": (_I32, [_P, _I64, _P, _P, _P, _I32, _F, _P, _P, _P, _P, _P,
+                                             _P, _P]),
     "nrt_sdf_eval": (_I32, [_P, _P, _I64, _P, _I32, _P]),
     "nrt_sdf_grad": (_I32, [_P, _P, _I64, _P, _P]),
     "nrt_intersect_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),

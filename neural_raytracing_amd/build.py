@@ -8,7 +8,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libnrt_hip.so")
 SOURCES = ["nrt_common.hip", "nrt_pack.hip", "nrt_api_mlp.hip", "nrt_api_sdf.hip",
            "nrt_api_shade.hip", "nrt_api_cam.hip", "nrt_ring_march.hip", "nrt_ring_march32.hip", "nrt_ring_march3.hip", "nrt_ring_mixed.hip", "nrt_ring_normal.hip", "nrt_prog.hip", "nrt_shade_ring.hip", "nrt_ring_normal32.hip", "nrt_callable.hip", "nrt_api_nerf.hip",
-           "nrt_api_path.hip", "nrt_api_train.hip", "nrt_refresh.hip", "nrt_sphere.hip", "nrt_api_tile.hip"]
+           "nrt_api_path.hip", "nrt_api_train.hip", "nrt_refresh.hip", "nrt_sphere.hip", "nrt_sphere_smoothmin.hip", "nrt_api_tile.hip"]
 HEADERS = ["nrt_kernels.h", "nrt_device.h", "nrt_internal.h", "nrt_launch.h", "nrt_ring3.h",
            "nrt_shade_ring.h"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nrt.h")

@@ -125,6 +125,56 @@ def needs_grad(*modules):
     return False
 
 
+SMOOTHMIN_K = 32.0  # sdfs.py:43 / utils.py:386-387
+
+
+class _SphereSmoothMinFn(torch.autograd.Function):
+    """(value, d value / d p) of SphereSDF's smooth-min on nrt_sphere_smoothmin_forward, with the
+    sphere parameters' gradients of both outputs from nrt_sphere_smoothmin_backward -- for the
+    gradient output that is the double backward of SDF.autograd_diff's create_graph=True normal
+    (sdfs.py:184-197).  The points carry no gradient (the reference's hit and scan points come
+    from the no-grad march)."""
+
+    @staticmethod
+    def forward(ctx, p, centers, radii, tfs):
+        P, n = p.shape[0], centers.shape[0]
+        value = torch.empty(P, device=p.device)
+        grad = torch.empty(P, 3, device=p.device)
+        c, r, t = (x.detach().float().contiguous() for x in (centers, radii, tfs))
+        _lib.call("nrt_sphere_smoothmin_forward", _lib.ptr(p), P, _lib.ptr(c), _lib.ptr(r),
+                  _lib.ptr(t), n, SMOOTHMIN_K, _lib.ptr(value), _lib.ptr(grad), _lib.stream())
+        ctx.save_for_backward(p, c, r, t)
+        return value, grad
+
+    @staticmethod
+    def backward(ctx, dvalue, dgrad):
+        if torch.is_grad_enabled():
+            raise _lib.NrtError("third derivatives of the SphereSDF smooth-min are not on the "
+                                "HIP path")
+        p, c, r, t = ctx.saved_tensors
+        P, n = p.shape[0], c.shape[0]
+        lib = _lib.load(require_device=True)
+        dc = torch.empty_like(c) if ctx.needs_input_grad[1] else None
+        dr = torch.empty_like(r) if ctx.needs_input_grad[2] else None
+        dt = torch.empty_like(t) if ctx.needs_input_grad[3] else None
+        dv = None if dvalue is None else dvalue.float().contiguous()
+        dg = None if dgrad is None else dgrad.float().contiguous()
+        ws = torch.empty(lib.nrt_sphere_smoothmin_workspace_bytes(P), dtype=torch.uint8,
+                         device=p.device)
+        _lib.call("nrt_sphere_smoothmin_backward", _lib.ptr(p), P, _lib.ptr(c), _lib.ptr(r),
+                  _lib.ptr(t), n, SMOOTHMIN_K, _lib.ptr(dv), _lib.ptr(dg), _lib.ptr(dc),
+                  _lib.ptr(dr), _lib.ptr(dt), _lib.ptr(ws), _lib.stream())
+        return None, dc, dr, dt
+
+
+def sphere_smoothmin(sdf, p):
+    """(value, gradient) of the smooth-min part at points p [..., 3] that carry no gradient, on
+    the fused kernels; shapes p.shape[:-1] and p.shape."""
+    flat = p.detach().reshape(-1, 3).float().contiguous()
+    v, g = _SphereSmoothMinFn.apply(flat, sdf.centers, sdf.radii, sdf.tfs)
+    return v.reshape(p.shape[:-1]), g.reshape(p.shape)
+
+
 def sphere_part(sdf, p):
     """The smooth-min of the transformed spheres of SphereSDF (sdfs.py:37-43, utils.py:386-387)."""
     flat = p.reshape(-1, 3).unsqueeze(0)
@@ -146,7 +196,10 @@ def sdf_value(sdf, p):
     if isinstance(sdf, SkipConnMLP):
         return sdf(p).reshape(p.shape[:-1])
     if _is_sphere_sdf(sdf):
-        out = sphere_part(sdf, p)
+        if p.is_cuda and not p.requires_grad:
+            out = sphere_smoothmin(sdf, p)[0]  # fused forward + parameter backward
+        else:  # points with a gradient (an SDF callable warping them): the torch restatement
+            out = sphere_part(sdf, p)
         return out + sdf.shift(p).reshape_as(out)
     raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP training path")
 
@@ -165,10 +218,13 @@ def sdf_gradient(sdf, p):
     if isinstance(sdf, SkipConnMLP):
         return input_gradient(sdf, p)
     if _is_sphere_sdf(sdf):
-        with torch.enable_grad():
-            q = p.clone().requires_grad_(True)
-            out = sphere_part(sdf, q)
-            (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+        if p.is_cuda:
+            g = sphere_smoothmin(sdf, p)[1]  # fused gradient + its double backward
+        else:
+            with torch.enable_grad():
+                q = p.clone().requires_grad_(True)
+                out = sphere_part(sdf, q)
+                (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
         return g + input_gradient(sdf.shift, p)
     raise _lib.NrtError(f"SDF callable {type(sdf).__name__} has no HIP training path")
 

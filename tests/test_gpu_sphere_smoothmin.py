@@ -1,0 +1,104 @@
+"""SphereSDF's smooth-min on the fused training kernels (nrt_sphere_smoothmin_forward / _backward,
+differentiable._SphereSmoothMinFn) against float64 torch autograd of the restatement
+(sdfs.py:37-43, utils.py:386-387): the value, the gradient d v / d p (the normal's sphere part,
+sdfs.py:184-197), and the sphere parameters' gradients of a loss on both -- for the gradient
+output that is the double backward through create_graph=True.  Includes points far from every
+sphere (the 1e-4 clamp: constant value, no gradient) and ragged point counts."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(p, c, r, t, k=32.0):
+    """value and create_graph gradient in the input dtype (torch autograd)."""
+    q = p.clone().requires_grad_(True)
+    T = t + torch.eye(3, dtype=p.dtype).unsqueeze(0)
+    qq = torch.einsum("ijk,ibk->ibj", T, q.unsqueeze(0).expand(T.shape[0], -1, -1)) - c.unsqueeze(1)
+    sd = qq.norm(p=2, dim=-1) - r.unsqueeze(-1)
+    v = -(-k * sd).exp().sum(dim=0).clamp(min=1e-4).log() / k
+    (g,) = torch.autograd.grad(v, q, torch.ones_like(v), create_graph=True)
+    return v, g
+
+
+def _params(n, seed, dtype=torch.float32):
+    g = torch.Generator().manual_seed(seed)
+    c = (0.3 * torch.rand(n, 3, generator=g) - 0.15).to(dtype)
+    r = (0.2 * torch.rand(n, generator=g) + 0.05).to(dtype)
+    t = (0.1 * torch.randn(n, 3, 3, generator=g)).to(dtype)
+    return c, r, t
+
+
+@pytest.mark.parametrize("P", [1, 77, 5000])
+@pytest.mark.parametrize("n", [1, 64, 128])
+def test_smoothmin_matches_float64_autograd(P, n):
+    from neural_raytracing_amd.pathtracer.differentiable import _SphereSmoothMinFn
+    c, r, t = _params(n, 3 + n)
+    g = torch.Generator().manual_seed(P)
+    p = 0.6 * (torch.rand(P, 3, generator=g) * 2 - 1)
+    p[: P // 10] *= 40.0  # far away: the clamp (no gradient)
+    dv = torch.randn(P, generator=g)
+    dg = torch.randn(P, 3, generator=g)
+    # float64 reference of values and of every parameter gradient of J = dv . v + dg . g
+    c64, r64, t64 = (x.double().requires_grad_(True) for x in (c, r, t))
+    v64, g64 = _ref(p.double(), c64, r64, t64)
+    (dv.double() * v64).sum().add((dg.double() * g64).sum()).backward()
+    # fp32 torch, for the tolerance scale
+    c32, r32, t32 = (x.clone().requires_grad_(True) for x in (c, r, t))
+    v32, g32 = _ref(p, c32, r32, t32)
+    (dv * v32).sum().add((dg * g32).sum()).backward()
+    # fused
+    cm, rm, tm = (x.cuda().requires_grad_(True) for x in (c, r, t))
+    v, gr = _SphereSmoothMinFn.apply(p.cuda().contiguous(), cm, rm, tm)
+    (dv.cuda() * v).sum().add((dg.cuda() * gr).sum()).backward()
+
+    def close(got, want, ref32, what):
+        scale = max(1.0, want.abs().max().item())
+        err = (got.detach().cpu().double() - want.detach()).abs().max().item()
+        e32 = (ref32.detach().double() - want.detach()).abs().max().item()
+        assert err <= max(1e-5 * scale, 4 * e32), (what, err, e32, scale)
+    close(v, v64, v32, "value")
+    close(gr, g64, g32, "grad")
+    close(cm.grad, c64.grad, c32.grad, "dcenters")
+    close(rm.grad, r64.grad, r32.grad, "dradii")
+    close(tm.grad, t64.grad, t32.grad, "dtfs")
+    far = (p.abs() > 1.0).any(-1)
+    if far.any():  # clamped points: zero gradient output
+        assert gr.detach().cpu()[far].abs().max().item() == 0.0
+
+
+def test_smoothmin_value_only_and_grad_only():
+    """A loss on one output only (the other's gradient is None / zero): same as float64."""
+    from neural_raytracing_amd.pathtracer.differentiable import _SphereSmoothMinFn
+    c, r, t = _params(32, 9)
+    p = 0.4 * (torch.rand(900, 3) * 2 - 1)
+    for which in ("value", "grad"):
+        c64, r64, t64 = (x.double().requires_grad_(True) for x in (c, r, t))
+        v64, g64 = _ref(p.double(), c64, r64, t64)
+        (v64.sum() if which == "value" else g64.square().sum()).backward()
+        cm, rm, tm = (x.cuda().requires_grad_(True) for x in (c, r, t))
+        v, gr = _SphereSmoothMinFn.apply(p.cuda().contiguous(), cm, rm, tm)
+        (v.sum() if which == "value" else gr.square().sum()).backward()
+        for got, want in ((cm.grad, c64.grad), (rm.grad, r64.grad), (tm.grad, t64.grad)):
+            err = (got.cpu().double() - want).abs().max().item()
+            assert err <= 1e-4 * max(1.0, want.abs().max().item()), (which, err)
+
+
+def test_smoothmin_deterministic_and_empty():
+    from neural_raytracing_amd.pathtracer.differentiable import _SphereSmoothMinFn
+    c, r, t = _params(128, 5)
+    p = (0.5 * (torch.rand(20000, 3) * 2 - 1)).cuda()
+    dg = torch.randn(20000, 3).cuda()
+    outs = []
+    for _ in range(2):
+        cm, rm, tm = (x.cuda().requires_grad_(True) for x in (c, r, t))
+        v, gr = _SphereSmoothMinFn.apply(p, cm, rm, tm)
+        (dg * gr).sum().backward()
+        outs.append((cm.grad.clone(), rm.grad.clone(), tm.grad.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    cm, rm, tm = (x.cuda().requires_grad_(True) for x in (c, r, t))
+    v, gr = _SphereSmoothMinFn.apply(torch.zeros(0, 3, device="cuda"), cm, rm, tm)
+    assert v.numel() == 0 and gr.shape == (0, 3)
+    (v.sum() + gr.sum()).backward()
+    assert float(cm.grad.abs().max()) == 0.0 and float(tm.grad.abs().max()) == 0.0
