@@ -381,9 +381,9 @@ def direct_sample(it, active, bsdf, lights, lead, device, shapes=None, w_isect=F
     ae = active & (pdf > 0)
     wo = it.to_local(d)
     f, _ = bsdf_eval(bsdf, it, wo, ae)
-    result = result.clone()
-    result[ae] = result[ae] + f[ae] * le[ae]
-    return result
+    # result[ae] += f[ae] le[ae] without the boolean gathers' host syncs (both are finite and
+    # zero outside ae: light_sample / bsdf_eval mask them)
+    return torch.where(ae.unsqueeze(-1), result + f * le, result)
 
 
 def path_sample(shapes, rays, bsdf, lights, max_depth, training, sampler, uniforms=None,

@@ -301,11 +301,17 @@ class SDF:
         n = torch.zeros_like(p0)
         p = p0
         raw = None
-        if bool(hit.any()):
-            raw = sdf_gradient(self.sdf, p0[hit])
+        # the march's compacted hit list, sorted (= hit-mask order, as p0[hit]): one host sync
+        # for its length instead of one per boolean-mask gather / scatter and their backwards
+        hit_idx, hit_count, _ = hits
+        cnt = int(hit_count.item())
+        if cnt > 0:
+            idx = hit_idx[:cnt].long().sort().values
+            ph = p0.index_select(0, idx)
+            raw = sdf_gradient(self.sdf, ph)
             nh = F.normalize(raw, eps=1e-6, dim=-1)
-            n = n.index_put((hit,), nh)
-            p = p0.index_put((hit,), p0[hit] + nh * self.epsilon * 5)
+            n = n.index_put((idx,), nh)
+            p = p0.index_put((idx,), ph + nh * self.epsilon * 5)
         frame = coordinate_system(n)
         si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead).squeeze(), obj=self,
                             throughput=throughput)
