@@ -249,12 +249,16 @@ def light_sample(lights, it, active):
     from .lights.lights import LightField, PointLights, RendererPointLights
     p = it.p
     if isinstance(lights, LightField):
-        # lights.py:175-195
-        v = lights.light_field_approx(p[active])
-        d = torch.zeros_like(p)
-        d[active] = F.normalize(v, eps=1e-6, dim=-1).clamp(min=1e-6, max=1)
-        le = torch.zeros_like(p)
-        le[active] = torch.linalg.norm(v, ord=2, dim=-1, keepdim=True) * lights.color.sigmoid()
+        # lights.py:175-195, on the active rows through one integer index (one host sync for
+        # its length; the boolean gather and scatters took one each, and their backwards more)
+        flat = p.reshape(-1, 3)
+        aidx = torch.nonzero(active.reshape(-1)).squeeze(1)
+        v = lights.light_field_approx(flat.index_select(0, aidx))
+        d = torch.zeros_like(flat).index_put(
+            (aidx,), F.normalize(v, eps=1e-6, dim=-1).clamp(min=1e-6, max=1)).reshape(p.shape)
+        le = torch.zeros_like(flat).index_put(
+            (aidx,), torch.linalg.norm(v, ord=2, dim=-1, keepdim=True) *
+            lights.color.sigmoid()).reshape(p.shape)
         pdf = torch.ones(p.shape[:-1], device=p.device)
         dist = None
     elif isinstance(lights, PointLights):
