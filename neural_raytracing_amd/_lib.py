@@ -183,7 +183,9 @@ def stream():
 # ---------------------------------------------------------------------------------------------
 # precision
 # ---------------------------------------------------------------------------------------------
-_precision = {"value": NRT_FP16 if os.environ.get("NRT_PRECISION", "fp32") == "fp16" else NRT_FP32}
+# NRT_PRECISION (fp32 | fp16 | fp32-split | mixed) picks the process-wide default; set_precision
+# overrides it
+_precision = {"value": _PRECISIONS.get(os.environ.get("NRT_PRECISION", "fp32"), NRT_FP32)}
 
 
 def set_precision(p):
