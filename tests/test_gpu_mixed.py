@@ -123,3 +123,18 @@ def test_mixed_frame_vs_fp32():
     assert m["maxabs_agreeing"] <= 1e-4
     assert m["pixels_over_1e-4"] <= 2 + 1e-4 * m["pixels"]
     assert m["pixels_over_1e-4"] < f["pixels_over_1e-4"]
+
+
+def test_mixed_independent_of_grid_size():
+    """The flags, the refinement list (appended in any order) and the runner-up merges are
+    per-ray facts: t / hit / p / n / throughput are bit-identical for every persistent grid
+    (option march_blocks; 0 = the occupancy-sized grid)."""
+    scene, rays = _scene_rays(crop=64)
+    outs = []
+    for blocks in (0, 1, 7, 33):
+        lib_opt("march_blocks", blocks)
+        outs.append(_intersect(scene["shape"], rays, "mixed", primary=True))
+    lib_opt("march_blocks", 0)
+    for o in outs[1:]:
+        for k in ("t", "hit", "p", "n", "thr"):
+            assert torch.equal(o[k], outs[0][k]), k
