@@ -489,7 +489,10 @@ int nrt_profile_evals(uint64_t* evals);
  *                      1e-7 units (the FP16 SDF error of the headline scene is <= 7.3e-5; slowly
  *                      converging rays need the larger bound)
  *   "mixed_restart"  1  1: a flagged ray marches again from t = 0; 0: it resumes at the flagged
- *                      step (cheaper, but keeps the FP16 drift of t: measured 1,464 step flips)
+ *                      step (cheaper, but keeps the FP16 drift of t: measured 1,464 step flips);
+ *                      2: at its first step within "mixed_zone" of a surface (zone 0.2: 18 step
+ *                      flips for 2.5 ms less; kept for A/B)
+ *   "mixed_zone"     500000  restart 2's zone, 1e-7 units
  *   "mixed_drift"    0  1: the flag bound is d * (1 + a per-ray drift estimate built from the
  *                      ratio of consecutive step values) instead of d * (1 + step/16); measured
  *                      to flag more rays for the same accuracy (152 vs 133 ms), kept for A/B

@@ -276,6 +276,7 @@ struct MarchArgs {
   //  * sdf(best) with keys2: both candidates' values merge into kbest[ray] (atomic min of the key)
   float refine_d = 0.f, refine_s = 0.f;
   int drift_model = 0;  // 1: the flag bound follows a per-ray drift estimate (option "mixed_drift")
+  float zone = 0.f;     // > 0: flagged rays resume at the first step within `zone` of a surface
   unsigned long long* amb = nullptr;
   unsigned long long* keys2 = nullptr;
   unsigned long long* kbest = nullptr;
@@ -606,6 +607,7 @@ __device__ __forceinline__ void march_body(
   unsigned long long ambs = ~0ull;  // NRT_MIXED: the first undecidable step's (i, t), or none
   float drift = 0.f, dprev = 1.f;   // NRT_MIXED: t's drift bound (units of the FP16 error)
   float mt = 0.f;                   // mode 3: the ray's distance to the light
+  unsigned long long cps = ~0ull;   // NRT_MIXED: the zone checkpoint (MarchArgs::zone)
   int64_t cursor = 0;  // wave-uniform
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
@@ -711,7 +713,7 @@ __device__ __forceinline__ void march_body(
               if (!(scan_key_value(k2) - scan_key_value(k1) <= a.refine_s)) kind = -1;
             }
           } else if (seg < 0) {
-            kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull; drift = 0.f;
+            kind = 0; t = 0.f; i = 0; hit = false; ambs = ~0ull; drift = 0.f; cps = ~0ull;
             if (mode == 3) {  // shadow rays start 100 eps out (sdfs.py:170)
               t = 0.f + 1e2f * a.eps;
               mt = a.occ_max_t[ray];
@@ -772,8 +774,12 @@ __device__ __forceinline__ void march_body(
         if (a.drift_model && i > 0) drift = drift * fabsf(d / dprev) + 1.f;
         const float bound = a.refine_d * (a.drift_model ? 1.f + drift : 1.f + 0.0625f * (float)i);
         const float tn = t + d;
+        const unsigned long long here = ((unsigned long long)(uint32_t)i << 32) | __float_as_uint(t);
+        // a.zone: the refinement resumes at the first step that came within `zone` of a surface
+        // (the drift of the far-field steps before it kept), instead of at the flagged step
+        if (a.zone > 0.f && cps == ~0ull && d < a.zone) cps = here;
         if (fabsf(d - a.eps) <= bound || (d > a.eps && fabsf(tn - a.max_t) <= bound))
-          ambs = ((unsigned long long)(uint32_t)i << 32) | __float_as_uint(t);
+          ambs = (a.zone > 0.f && cps != ~0ull) ? cps : here;
         dprev = d;
       }
       if (mode == 3) {  // sdfs.py:175-179: t advances on the hit step too, the test is strict

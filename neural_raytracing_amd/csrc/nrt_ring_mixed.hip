@@ -43,6 +43,9 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
   MarchArgs m16 = ma;
   m16.refine_d = rd;
   m16.drift_model = (int)option(OPT_MIXED_DRIFT);
+  const int64_t restart = option(OPT_MIXED_RESTART);
+  // restart 2: resume at the zone checkpoint (option "mixed_zone")
+  m16.zone = restart == 2 ? 1e-7f * (float)option(OPT_MIXED_ZONE) : 0.f;
   m16.amb = amb;
   m16.keys2 = scan ? keys2 : nullptr;
   if (int rc = ring_march16_launch(s, rays, P, m16, t, thr, keys, st, false)) return rc;
@@ -57,7 +60,7 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
   mr.count = lcount;
   // option "mixed_restart" (default): a flagged ray marches again from t = 0 -- resumed at the
   // flagged step instead, it would carry the FP16 march's drift of t into the decision
-  mr.start = option(OPT_MIXED_RESTART) ? nullptr : amb;
+  mr.start = restart == 1 ? nullptr : amb;
   if (int rc = ring3_launch(s, rays, P, mr, t, nullptr, nullptr, st, 2)) return rc;
   // 3. sdf(best) at FP32 accuracy, over both candidates where FP16 could not order them
   if (scan) {

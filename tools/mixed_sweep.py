@@ -21,6 +21,7 @@ def main():
     ss = [int(v) for v in sys.argv[3].split(",")] if len(sys.argv) > 3 else [2000]
     rs = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1]
     ms = [int(v) for v in sys.argv[5].split(",")] if len(sys.argv) > 5 else [0]
+    zs = [int(v) for v in sys.argv[6].split(",")] if len(sys.argv) > 6 else [500000]
     dev = torch.device("cuda", 0)
     _lib.load(require_device=True)
     nra.set_precision("fp32")
@@ -33,8 +34,10 @@ def main():
                      size, range(size), background=0.0, with_noise=1e-3, device=dev)
     with torch.no_grad():
         want, rhit, rt = bench._frame_state(rr, 1234)
-        for d, s, r, mdl in [(d, s, r, mdl) for mdl in ms for r in rs for d in ds for s in ss]:
+        for d, s, r, mdl, z in [(d, s, r, mdl, z) for z in zs for mdl in ms for r in rs
+                                for d in ds for s in ss]:
             if True:
+                _lib.set_option("mixed_zone", z)
                 _lib.set_option("mixed_drift", mdl)
                 _lib.set_option("mixed_restart", r)
                 _lib.set_option("mixed_refine_d", d)
@@ -48,7 +51,7 @@ def main():
                                            rt.cpu())
                 both = (hit & rhit).reshape(-1)
                 dt = (t - rt).abs().reshape(-1)[both]
-                rec = {"refine_d": d, "refine_s": s, "restart": r, "drift_model": mdl, "frame_ms": 1000 * el / 3,
+                rec = {"refine_d": d, "refine_s": s, "restart": r, "drift_model": mdl, "zone": z, "frame_ms": 1000 * el / 3,
                        **{k + "_ms": v[0] / max(v[1], 1) for k, v in ks.items()},
                        "evals": evals, "dt_q": torch.quantile(dt.float()[: 1 << 20], torch.tensor(
                            [0.5, 0.9, 0.99, 0.999], device=dt.device)).tolist(), **acc}
