@@ -493,6 +493,11 @@ int nrt_profile_evals(uint64_t* evals);
  *                      2: at its first step within "mixed_zone" of a surface (zone 0.2: 18 step
  *                      flips for 2.5 ms less; kept for A/B)
  *   "mixed_zone"     500000  restart 2's zone, 1e-7 units
+ *   "bwd_colsplit"   1  nrt_mlp_backward(_multi): 1 = the column-split kernels (a block of one
+ *                      wave per 32-column row block on the same 32 rows; the encoding in global
+ *                      tiles where that doubles the blocks per CU), 2 = the same with the encoding
+ *                      in the LDS slab unless fewer than two blocks fit, 0 = one wave per 32 rows
+ *                      (round 3).  Gradients bit-equal across values.
  *   "mixed_drift"    0  1: the flag bound is d * (1 + a per-ray drift estimate built from the
  *                      ratio of consecutive step values) instead of d * (1 + step/16); measured
  *                      to flag more rays for the same accuracy (152 vs 133 ms), kept for A/B

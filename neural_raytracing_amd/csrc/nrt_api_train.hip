@@ -262,6 +262,230 @@ __device__ __forceinline__ void mlp_backward32(
     for (int j = h; j < m.latent; j += 2) dLat[row * m.latent + j] = egrad[es * (2 * F + in + j)];
 }
 
+// ---- column-split backward: one block of CW waves per 32 rows -------------------------------
+// The per-wave variant above gives a training batch one wave per 32 rows: a ~19k-row backward is
+// ~600 waves on 1,024 SIMDs, each running every layer's full 256-column GEMM alone at one wave
+// per SIMD (round-3 PMC: MFMA busy 0.09-0.17, 0.4-1.1 resident waves per SIMD).  Here the CW
+// waves of a block share one slab (the same 32 rows) and wave w computes output row blocks
+// [w NBW, (w + 1) NBW) of every layer -- its slice of the weight fragments, the whole slab as B --
+// so the batch runs CW times the waves at NBW accumulators each (two or more waves per SIMD), and
+// every layer boundary is a block barrier (all waves have read the slab before any overwrites it).
+// Same operations per output element in the same order: results bit-equal to the per-wave kernel.
+template <int NB>
+struct ColSplit {
+  // row blocks per wave: one (two put the 256-column kernels at the 256-VGPR cap with spills,
+  // measured slower than the per-wave kernel)
+  static constexpr int NBW = 1;
+  static constexpr int CW = NB / NBW;                            // waves per block
+};
+
+template <int NB, bool TILE>
+__device__ __forceinline__ void mlp_backward_cs(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
+    float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
+    float* __restrict__ Eact, float* __restrict__ dZg, float* __restrict__ Et,
+    float* __restrict__ Gt, int RS) {
+  constexpr int NBW = ColSplit<NB>::NBW, CW = ColSplit<NB>::CW;
+  constexpr int PF = 8;
+  extern __shared__ float smem[];
+  const MlpDev& m = *mp;
+  float* X = smem;
+  const int lane = lane_id(), r = lane & 31, h = lane >> 5;
+  const int w = (int)(threadIdx.x >> 6);
+  const int rbw = w * NBW;  // this wave's first output row block
+  const int64_t grp = blockIdx.x;
+  const int64_t row0 = grp * 32;
+  if (row0 >= M) return;  // whole block exits together
+  const int64_t row = row0 + r;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  const int H = m.hidden, L = m.n_hidden, ke = m.ke, dp = m.dp, in = m.in_size;
+  EncIn e;
+  if (in <= 4) {
+    for (int i = 0; i < 4; ++i) e.x[i] = (i < in) ? x[rr * in + i] : 0.f;
+    e.xg = nullptr;
+  } else {
+    e.x[0] = e.x[1] = e.x[2] = e.x[3] = 0.f;
+    e.xg = x + rr * in;
+  }
+  e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
+  float* rowp = X + r * RS;
+  float* const et = TILE ? Et + grp * ke * 32 + r : rowp + H;
+  float* const gt = TILE ? Gt + grp * ke * 32 + r : rowp + H;
+  constexpr int es = TILE ? 32 : 1;
+  // ---- forward, saving Z_l, A_l and the encoding (the waves share the encoding's slot pairs)
+  for (int slot = 2 * h + 4 * w; slot < ke; slot += 4 * CW) {
+    float a, b;
+    enc_pair<false>(m, e, slot, a, b);
+    et[slot * es] = a;
+    et[(slot + 1) * es] = b;
+  }
+  __syncthreads();
+  if (valid)
+    for (int s = h + 2 * w; s < ke; s += 2 * CW) {
+      const int c = enc_col(m, s);
+      if (c < 0) continue;
+      const float v = et[s * es];
+      Eraw[row * dp + c] = v;
+      Eact[row * dp + c] = act_fwd<false>(v, m.act);
+    }
+  f16v acc[NBW];
+  for (int l = 0; l <= L; ++l) {
+    bias32<NBW>(acc, m.bias[l], rbw, NB, h);
+    if (l == 0) {
+      if (TILE) gemm32_tile<NBW, PF>(acc, m.w32[0], NB, rbw, ke >> 1, et - r, -1);
+      else gemm32<NBW, PF>(acc, m.w32[0], NB, rbw, ke >> 1, X, RS, H, -1);
+    } else {
+      const int i = l - 1;
+      gemm32<NBW, PF>(acc, m.w32[l], NB, rbw, H >> 1, X, RS, 0, -1);
+      if (i != L - 1 && (i % m.skip) == 0) {
+        const float* Ws = m.w32[l] + (H >> 1) * NB * 64;
+        if (TILE) gemm32_tile<NBW, PF>(acc, Ws, NB, rbw, ke >> 1, et - r, m.act);
+        else gemm32<NBW, PF>(acc, Ws, NB, rbw, ke >> 1, X, RS, H, m.act);
+      }
+    }
+    __syncthreads();  // every wave has read the layer's inputs from the slab
+#pragma unroll
+    for (int ib = 0; ib < NBW; ++ib)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int k0 = 32 * (rbw + ib) + 8 * g + 4 * h;
+        float4 zv, av;
+        float* zp = &zv.x;
+        float* ap = &av.x;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          zp[j] = acc[ib][4 * g + j];
+          ap[j] = act_fwd<false>(zp[j], m.act);
+          rowp[k0 + j] = ap[j];
+        }
+        if (valid) {
+          *reinterpret_cast<float4*>(Zg + ((int64_t)l * M + row) * H + k0) = zv;
+          *reinterpret_cast<float4*>(Ag + ((int64_t)l * M + row) * H + k0) = av;
+        }
+      }
+    __syncthreads();  // the layer's activations are in the slab
+  }
+  // ---- backward seed: dZ_L = (dY W_out) * act'(Z_L); the encoding gradient starts at zero.
+  // Slot s is accumulated by one wave and lane in every pass (its row block's owner, at the MFMA
+  // output position), so only the barrier before dL/dx orders it across waves.
+  const float* eraw_row = Eraw + rr * dp;
+  for (int s = 4 * h + 8 * w; s < ke; s += 8 * CW)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) gt[(s + j) * es] = 0.f;
+  const float* Ao = m.w32[L + 1];
+  const int out = m.out;
+  for (int k = h + 2 * w; k < H; k += 2 * CW) {
+    float g = 0.f;
+    for (int o = 0; o < out; ++o)
+      g = fmaf(dY[rr * out + o], Ao[((k >> 1) * m.ob + (o >> 5)) * 64 + (k & 1) * 32 + (o & 31)], g);
+    rowp[k] = g * act_bwd(Zg[((int64_t)L * M + rr) * H + k], m.act);
+  }
+  __syncthreads();
+  for (int l = L; l >= 0; --l) {
+    if (valid)
+      for (int k = 4 * h + 8 * w; k < H; k += 8 * CW)
+        *reinterpret_cast<float4*>(dZg + ((int64_t)l * M + row) * H + k) =
+            make_float4(rowp[k], rowp[k + 1], rowp[k + 2], rowp[k + 3]);
+    const float* At = m.wt32[l];
+    const int nrb = m.nbt[l];
+    const bool has_hidden_in = (l != 0);
+    const bool has_enc_in = (l == 0) || ((l - 1) != L - 1 && ((l - 1) % m.skip) == 0);
+    const int hid_rb = has_hidden_in ? NB : 0;
+    if (has_enc_in) {
+      const int enc_pos0 = has_hidden_in ? H : 0;
+      for (int rb0 = hid_rb + rbw; rb0 < nrb; rb0 += NB) {
+#pragma unroll
+        for (int ib = 0; ib < NBW; ++ib) acc[ib] = f16v{};
+        gemm32<NBW, PF>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+        // per row block: every load first (clamped addresses, unconditional), then the
+        // activation's branches
+#pragma unroll
+        for (int ib = 0; ib < NBW; ++ib) {
+          if (rb0 + ib >= nrb) continue;
+          float ev[16], gv[16];
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int slot = min(max(pos - enc_pos0, 0), ke - 1);
+            const int c = l != 0 ? enc_col(m, slot) : -1;
+            ev[reg] = eraw_row[c < 0 ? 0 : c];
+            gv[reg] = gt[slot * es];
+          }
+#pragma unroll
+          for (int reg = 0; reg < 16; ++reg) {
+            const int pos = 32 * (rb0 + ib) + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+            const int slot = pos - enc_pos0;
+            if (slot >= 0 && slot < ke) {
+              float v = acc[ib][reg];
+              if (l != 0) {  // skip inputs are act(enc)
+                const int c = enc_col(m, slot);
+                v = c < 0 ? 0.f : v * act_bwd(ev[reg], m.act);
+              }
+              gt[slot * es] = gv[reg] + v;
+            }
+          }
+        }
+      }
+    }
+    if (has_hidden_in) {
+#pragma unroll
+      for (int ib = 0; ib < NBW; ++ib) acc[ib] = f16v{};
+      gemm32<NBW, PF>(acc, At, nrb, rbw, H >> 1, X, RS, 0, -1);
+    }
+    __syncthreads();  // every wave has read dZ_l from the slab
+    if (has_hidden_in) {
+#pragma unroll
+      for (int ib = 0; ib < NBW; ++ib) {
+        float4 zq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          zq[q] = *reinterpret_cast<const float4*>(Zg + ((int64_t)(l - 1) * M + rr) * H + 32 * (rbw + ib) + 8 * q + 4 * h);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k0 = 32 * (rbw + ib) + 8 * q + 4 * h;
+          const float* zp = &zq[q].x;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rowp[k0 + j] = acc[ib][4 * q + j] * act_bwd(zp[j], m.act);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // ---- encoding -> inputs (every wave's slots of the encoding gradient: the barrier above)
+  const float* egrad = gt;
+  const int F = m.freqs;
+  for (int i = w; i < in; i += CW) {
+    float g = 0.f;
+    for (int q = h; q < F; q += 2) {
+      float s, c;
+      sincosf(proj<false>(m, e, q), &s, &c);
+      g = fmaf(egrad[es * (2 * q)] * c - egrad[es * (2 * q + 1)] * s, m.basis[i * F + q], g);
+    }
+    if (h == 0) g += egrad[es * (2 * F + i)];
+    g += __shfl_xor(g, 32);
+    if (dX && valid && h == 0) dX[row * in + i] = g;
+  }
+  if (dLat && valid)
+    for (int j = h + 2 * w; j < m.latent; j += 2 * CW) dLat[row * m.latent + j] = egrad[es * (2 * F + in + j)];
+}
+
+template <int NB, bool TILE>
+__global__ void __launch_bounds__(64 * ColSplit<NB>::CW, 2) k_mlp_backward32_cs(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    int64_t M, const float* __restrict__ dY, float* __restrict__ dX, float* __restrict__ dLat,
+    float* __restrict__ Zg, float* __restrict__ Ag, float* __restrict__ Eraw,
+    float* __restrict__ Eact, float* __restrict__ dZg, float* __restrict__ Et,
+    float* __restrict__ Gt, int RS) {
+  mlp_backward_cs<NB, TILE>(mp, x, lat, M, dY, dX, dLat, Zg, Ag, Eraw, Eact, dZg, Et, Gt, RS);
+}
+
+struct BwdJob;
+template <int NB, bool TILE>
+__global__ void __launch_bounds__(64 * ColSplit<NB>::CW, 2) k_mlp_backward32_multi_cs(
+    const BwdJob* __restrict__ jobs, const float* __restrict__ x, int64_t M, int RS);
+
 // below four row blocks two waves per SIMD fit (registers and slab): ask the compiler for that
 template <int NB, bool TILE>
 __global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_backward32(
@@ -288,6 +512,14 @@ __global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_backward32_multi(
   const BwdJob j = jobs[blockIdx.y];
   mlp_backward32<NB, TILE>(j.mp, x, nullptr, M, j.dY, j.dX, nullptr, j.Z, j.A, j.Eraw, j.Eact,
                            j.dZ, j.Et, j.Gt, RS, per_wave);
+}
+
+template <int NB, bool TILE>
+__global__ void __launch_bounds__(64 * ColSplit<NB>::CW, 2) k_mlp_backward32_multi_cs(
+    const BwdJob* __restrict__ jobs, const float* __restrict__ x, int64_t M, int RS) {
+  const BwdJob j = jobs[blockIdx.y];
+  mlp_backward_cs<NB, TILE>(j.mp, x, nullptr, M, j.dY, j.dX, nullptr, j.Z, j.A, j.Eraw, j.Eact,
+                            j.dZ, j.Et, j.Gt, RS);
 }
 
 // second derivative of act at pre-activation x (torch double-backward formulas:
@@ -465,6 +697,152 @@ __global__ void __launch_bounds__(256, NB <= 4 ? 2 : 1) k_mlp_grad_backward32(
           rowp[col + 32 * ib + (reg & 3) + 8 * (reg >> 2) + 4 * h] = acc[ib][reg];
       wave_lds_fence();
     }
+  }
+}
+
+// Column-split variant of k_mlp_grad_backward32 (as mlp_backward_cs): one block of NB waves per
+// 32 rows sharing one slab, wave w computing output row block w of every layer's primal and
+// tangent GEMMs (both before one barrier, then both writes).  The [a | enc | enc tangent | a
+// tangent] slab row (~53 KB a wave for the 8x128 SDF shift) held the per-wave kernel at three
+// waves per CU; here three blocks of four waves fit.  Same operations per element: bit-equal.
+template <int NB>
+__global__ void __launch_bounds__(64 * NB, 2) k_mlp_grad_backward32_cs(
+    const MlpDev* __restrict__ mp, const float* __restrict__ x, const float* __restrict__ lat,
+    const float* __restrict__ v, int64_t M, float* __restrict__ Zg, float* __restrict__ Tg,
+    float* __restrict__ Ag, float* __restrict__ E0, float* __restrict__ E1,
+    float* __restrict__ dZg, int RS) {
+  constexpr int CW = NB, PF = 8;
+  extern __shared__ float smem[];
+  const MlpDev& m = *mp;
+  float* X = smem;
+  const int lane = lane_id(), r = lane & 31, h = lane >> 5;
+  const int w = (int)(threadIdx.x >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * 32;
+  if (row0 >= M) return;  // whole block exits together
+  const int64_t row = row0 + r;
+  const bool valid = row < M;
+  const int64_t rr = valid ? row : M - 1;
+  const int H = m.hidden, L = m.n_hidden, ke = m.ke, dp = m.dp, in = m.in_size, F = m.freqs;
+  const int EE = H, ET = H + ke, PT = H + 2 * ke;
+  const int64_t M2 = 2 * M;
+  EncIn e;
+  if (in <= 4) {
+    for (int i = 0; i < 4; ++i) e.x[i] = (i < in) ? x[rr * in + i] : 0.f;
+    e.xg = nullptr;
+  } else {
+    e.x[0] = e.x[1] = e.x[2] = e.x[3] = 0.f;
+    e.xg = x + rr * in;
+  }
+  e.lat = (lat && m.latent > 0) ? lat + rr * m.latent : nullptr;
+  float* rowp = X + r * RS;
+  const float* vr = v + rr * in;
+  // ---- encoding (write_enc_slab's pairs, shared by the waves) and its tangent along v
+  for (int slot = 2 * h + 4 * w; slot < ke; slot += 4 * CW) {
+    float a, b;
+    enc_pair<false>(m, e, slot, a, b);
+    rowp[EE + slot] = a;
+    rowp[EE + slot + 1] = b;
+  }
+  for (int s = h + 2 * w; s < ke; s += 2 * CW) {
+    float tv = 0.f;
+    if (s < 2 * F) {
+      const int q = s >> 1;
+      float vb = vr[0] * m.basis[q];
+      for (int i = 1; i < in; ++i) vb = fmaf(vr[i], m.basis[i * F + q], vb);
+      float sn, cs;
+      sincosf(proj<false>(m, e, q), &sn, &cs);
+      tv = (s & 1) ? -sn * vb : cs * vb;
+    } else if (s < 2 * F + in) {
+      tv = vr[s - 2 * F];
+    }
+    rowp[ET + s] = tv;
+  }
+  __syncthreads();
+  if (valid)
+    for (int s = h + 2 * w; s < ke; s += 2 * CW) {
+      const int c = enc_col(m, s);
+      if (c < 0) continue;
+      const float ev = rowp[EE + s], tv = rowp[ET + s];
+      E0[row * dp + c] = ev;
+      E0[(M + row) * dp + c] = tv;
+      E1[row * dp + c] = act_fwd<false>(ev, m.act);
+      E1[(M + row) * dp + c] = act_bwd(ev, m.act) * tv;
+    }
+  // ---- forward: primal and tangent GEMMs of a layer, one barrier, then both writes
+  f16v acc[1], act_[1];
+  for (int l = 0; l <= L; ++l) {
+    const bool skip = l > 0 && (l - 1) != L - 1 && ((l - 1) % m.skip) == 0;
+    bias32<1>(acc, m.bias[l], w, NB, h);
+    act_[0] = f16v{};
+    if (l == 0) {
+      gemm32<1, PF>(acc, m.w32[0], NB, w, ke >> 1, X, RS, EE, -1);
+      gemm32<1, PF>(act_, m.w32[0], NB, w, ke >> 1, X, RS, ET, -1);
+    } else {
+      gemm32<1, PF>(acc, m.w32[l], NB, w, H >> 1, X, RS, 0, -1);
+      if (skip) gemm32<1, PF>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, EE, m.act);
+      gemm32<1, PF>(act_, m.w32[l], NB, w, H >> 1, X, RS, PT, -1);
+      if (skip) gemm32<1, PF>(act_, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, ET, -1);
+    }
+    __syncthreads();  // every wave has read the layer's inputs
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int k = 32 * w + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      const float z = acc[0][reg], zt = act_[0][reg];
+      const float a = act_fwd<false>(z, m.act);
+      const float at = act_bwd(valid ? z : 0.f, m.act) * zt;
+      if (valid) {
+        Zg[((int64_t)l * M + row) * H + k] = z;
+        Ag[((int64_t)l * M2 + row) * H + k] = a;
+        Tg[((int64_t)l * M + row) * H + k] = zt;
+        Ag[((int64_t)l * M2 + M + row) * H + k] = at;
+      }
+      rowp[k] = a;
+      rowp[PT + k] = at;
+    }
+    if (l == 0)  // skip layers consume act(enc): tangent act'(enc) * enc tangent
+      for (int s = h + 2 * w; s < ke; s += 2 * CW) rowp[ET + s] = act_bwd(rowp[EE + s], m.act) * rowp[ET + s];
+    __syncthreads();
+  }
+  // ---- reverse: seed a_bar_L = 0, at_bar_L = W_out^T 1
+  const float* Ao = m.w32[L + 1];
+  for (int k = h + 2 * w; k < H; k += 2 * CW) {
+    float g = 0.f;
+    for (int o = 0; o < m.out; ++o) g += Ao[((k >> 1) * m.ob + (o >> 5)) * 64 + (k & 1) * 32 + (o & 31)];
+    rowp[k] = 0.f;
+    rowp[PT + k] = g;
+  }
+  __syncthreads();
+  for (int l = L; l >= 0; --l) {
+    for (int k = h + 2 * w; k < H; k += 2 * CW) {
+      const float z = valid ? Zg[((int64_t)l * M + row) * H + k] : 0.f;
+      const float zt = valid ? Tg[((int64_t)l * M + row) * H + k] : 0.f;
+      const float d1 = act_bwd(z, m.act);
+      const float ab = rowp[k], atb = rowp[PT + k];
+      const float zb = ab * d1 + atb * act_bwd2(z, m.act) * zt;
+      const float ztb = atb * d1;
+      rowp[k] = zb;
+      rowp[PT + k] = ztb;
+      if (valid) {
+        dZg[((int64_t)l * M2 + row) * H + k] = zb;
+        dZg[((int64_t)l * M2 + M + row) * H + k] = ztb;
+      }
+    }
+    __syncthreads();
+    if (l == 0) break;
+    const float* At = m.wt32[l];
+    const int nrb = m.nbt[l];
+    acc[0] = f16v{};
+    act_[0] = f16v{};
+    gemm32<1, PF>(acc, At, nrb, w, H >> 1, X, RS, 0, -1);
+    gemm32<1, PF>(act_, At, nrb, w, H >> 1, X, RS, PT, -1);
+    __syncthreads();
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int k = 32 * w + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      rowp[k] = acc[0][reg];
+      rowp[PT + k] = act_[0][reg];
+    }
+    __syncthreads();
   }
 }
 
@@ -778,6 +1156,26 @@ LdsPlan backward_plan(const MlpDev& d, bool& tile) {
   tile = per_cu(tiled) >= 2 * per_cu(slab);
   return tile ? tiled : slab;
 }
+// the column-split kernels' plan: one slab per block of ColSplit<nb>::CW waves (same TILE rule,
+// counted in blocks per CU)
+LdsPlan backward_plan_cs(const MlpDev& d, bool& tile) {
+  auto plan = [&](bool t) {
+    LdsPlan p;
+    p.RS = (std::max(d.hidden, 32) + (t ? 0 : d.ke)) | 1;
+    p.per_wave = 32 * p.RS;
+    p.waves = 1;
+    p.bytes = (size_t)p.per_wave * 4;
+    return p;
+  };
+  const LdsPlan slab = plan(false), tiled = plan(true);
+  const auto per_cu = [](const LdsPlan& p) { return std::min(8, kLdsBytes / (p.per_wave * 4)); };
+  // the per-wave kernels' rule (TILE where it doubles the blocks per CU: the 16x256 F = 128
+  // MLP, 4 blocks of 8 waves per CU instead of 2; measured 0.5 ms a training step faster);
+  // option bwd_colsplit 2: the slab unless fewer than two blocks fit
+  tile = (option(OPT_BWD_COLSPLIT) != 2 || per_cu(slab) < 2) && per_cu(tiled) >= 2 * per_cu(slab);
+  return tile ? tiled : slab;
+}
+#define NRT_CW(NBv) (ColSplit<NBv>::CW)
 
 // one MLP's activations / gradients region of the multi-MLP workspace (carve's first seven arrays)
 size_t region_bytes(const MlpDev& d, int64_t M) {
@@ -856,14 +1254,26 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   }
   TrainWs w = carve(m, M, workspace);
   bool tile = false;
-  const LdsPlan lp = backward_plan(d, tile);
+  const bool cs = option(OPT_BWD_COLSPLIT) != 0;
+  const LdsPlan lp = cs ? backward_plan_cs(d, tile) : backward_plan(d, tile);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
   {
     ProfScope prof("k_mlp_backward32", st);
     NRT_NB_SWITCH(d.nb, {
-      if (tile) {
+      if (cs) {
+        const dim3 gcs(waves), bcs(64 * NRT_CW(NB));
+        if (tile) {
+          if (!(rc = set_lds(k_mlp_backward32_cs<NB, true>, lp.bytes)))
+            k_mlp_backward32_cs<NB, true><<<gcs, bcs, lp.bytes, st>>>(
+                m->dev, x, latent, M, dy, dx, dlatent, w.Z, w.A, w.Eraw, w.Eact, w.dZ, w.Et, w.Gt, lp.RS);
+        } else {
+          if (!(rc = set_lds(k_mlp_backward32_cs<NB, false>, lp.bytes)))
+            k_mlp_backward32_cs<NB, false><<<gcs, bcs, lp.bytes, st>>>(
+                m->dev, x, latent, M, dy, dx, dlatent, w.Z, w.A, w.Eraw, w.Eact, w.dZ, w.Et, w.Gt, lp.RS);
+        }
+      } else if (tile) {
         if (!(rc = set_lds(k_mlp_backward32<NB, true>, lp.bytes)))
           k_mlp_backward32<NB, true><<<grid, block, lp.bytes, st>>>(
               m->dev, x, latent, M, dy, dx, dlatent, w.Z, w.A, w.Eraw, w.Eact, w.dZ, w.Et, w.Gt,
@@ -947,14 +1357,24 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   float* part = (float*)p;
   NRT_HIP(hipMemcpyAsync(tj, jobs.data(), (size_t)n * sizeof(BwdJob), hipMemcpyHostToDevice, st));
   bool tile = false;
-  const LdsPlan lp = backward_plan(d, tile);
+  const bool cs = option(OPT_BWD_COLSPLIT) != 0;
+  const LdsPlan lp = cs ? backward_plan_cs(d, tile) : backward_plan(d, tile);
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves), n), block(64 * lp.waves);
   int rc = NRT_OK;
   {
     ProfScope prof("k_mlp_backward32", st);
     NRT_NB_SWITCH(d.nb, {
-      if (tile) {
+      if (cs) {
+        const dim3 gcs(waves, n), bcs(64 * NRT_CW(NB));
+        if (tile) {
+          if (!(rc = set_lds(k_mlp_backward32_multi_cs<NB, true>, lp.bytes)))
+            k_mlp_backward32_multi_cs<NB, true><<<gcs, bcs, lp.bytes, st>>>(tj, x, M, lp.RS);
+        } else {
+          if (!(rc = set_lds(k_mlp_backward32_multi_cs<NB, false>, lp.bytes)))
+            k_mlp_backward32_multi_cs<NB, false><<<gcs, bcs, lp.bytes, st>>>(tj, x, M, lp.RS);
+        }
+      } else if (tile) {
         if (!(rc = set_lds(k_mlp_backward32_multi<NB, true>, lp.bytes)))
           k_mlp_backward32_multi<NB, true><<<grid, block, lp.bytes, st>>>(tj, x, M, lp.RS, lp.per_wave);
       } else {
@@ -1041,11 +1461,17 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   if (bytes > (size_t)kLdsBytes) { set_error("nrt_mlp_grad_backward: MLP too wide for LDS"); return NRT_EINVAL; }
   const int nwaves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(nwaves, waves)), block(64 * waves);
+  const bool cs = option(OPT_BWD_COLSPLIT) != 0;
   int rc = NRT_OK;
   {
     ProfScope prof("k_mlp_grad_backward32", st);
     NRT_NB_SWITCH(d.nb, {
-      if (!(rc = set_lds(k_mlp_grad_backward32<NB>, bytes)))
+      if (cs) {
+        const size_t bcs = (size_t)per_wave * 4;
+        if (!(rc = set_lds(k_mlp_grad_backward32_cs<NB>, bcs)))
+          k_mlp_grad_backward32_cs<NB><<<dim3(nwaves), dim3(64 * NB), bcs, st>>>(
+              m->dev, x, latent, v, M, buf[0], buf[1], buf[2], buf[4], buf[5], buf[3], RS);
+      } else if (!(rc = set_lds(k_mlp_grad_backward32<NB>, bytes)))
         k_mlp_grad_backward32<NB><<<grid, block, bytes, st>>>(m->dev, x, latent, v, M, buf[0], buf[1],
                                                              buf[2], buf[4], buf[5], buf[3], RS,
                                                              per_wave);

@@ -33,6 +33,7 @@ enum Option {
   OPT_MIXED_DRIFT,     // "mixed_drift"
   OPT_RING_OCCLUSION,  // "ring_occlusion"
   OPT_MIXED_ZONE,      // "mixed_zone" (1e-7 units)
+  OPT_BWD_COLSPLIT,    // "bwd_colsplit"
   OPT_COUNT
 };
 int64_t option(Option o);

@@ -308,3 +308,58 @@ def test_mlp_backward_multi_with_frozen_biases():
     for a, b in zip(got, want):
         scale = b.abs().max().clamp_min(1e-6)
         assert ((a - b).abs().max() / scale) < 1e-5, ((a - b).abs().max(), scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_mlp_backward_column_split_bit_equal_to_per_wave(name, mode):
+    """The column-split backward kernels (option bwd_colsplit 1: encoding tiles where they double
+    the blocks per CU, 2: the slab) do the per-wave kernels' operations in the same order: every
+    gradient bit-equal to bwd_colsplit 0, on a ragged row count, single and multi-MLP launches."""
+    from neural_raytracing_amd import _lib, set_precision
+    kw = SHAPES[name]
+    _, mine = _pair(kw, 7)
+    set_precision("fp32")
+    M = 3001
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(M, kw["in_size"], generator=g) - 0.5).cuda()
+    lat = torch.randn(M, kw["latent_size"], generator=g).cuda() if kw.get("latent_size") else None
+    dy = torch.randn(M, kw["out"], generator=g).cuda()
+
+    def run(opt):
+        with _lib.options(bwd_colsplit=opt):
+            mine.zero_grad(set_to_none=True)
+            xm = x.clone().requires_grad_(True)
+            lm = lat.clone().requires_grad_(True) if lat is not None else None
+            (mine(xm, lm) * dy).sum().backward()
+            out = [xm.grad.clone()] + ([lm.grad.clone()] if lm is not None else [])
+            out += [p.grad.clone() for p in mine.parameters() if p.grad is not None]
+        return out
+
+    base = run(0)
+    got = run(mode)
+    assert len(base) == len(got) > 2
+    for i, (a, b) in enumerate(zip(base, got)):
+        assert torch.equal(a, b), (name, mode, i, (a - b).abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_mlp_backward_multi_column_split_bit_equal(mode):
+    from neural_raytracing_amd import _lib
+    from neural_raytracing_amd.pathtracer.neural_blocks import mlp_multi
+    kw = SHAPES["neural_bsdf_6x96_F64"]
+    mlps = [_pair(kw, seed)[1] for seed in (1, 2, 3)]
+    g = torch.Generator().manual_seed(11)
+    x = (torch.rand(2999, kw["in_size"], generator=g) * 2 - 1).cuda()
+    dys = [torch.randn(2999, kw["out"], generator=g).cuda() for _ in mlps]
+    params = [q for m in mlps for q in m.parameters()]
+
+    def grads(opt):
+        with _lib.options(bwd_colsplit=opt):
+            xx = x.clone().requires_grad_(True)
+            loss = sum((y * dy).sum() for y, dy in zip(mlp_multi(mlps, xx), dys))
+            return torch.autograd.grad(loss, [xx] + params)
+    for a, b in zip(grads(0), grads(mode)):
+        assert torch.equal(a, b), (a - b).abs().max().item()

@@ -96,6 +96,32 @@ def test_mlp_grad_backward_matches_autograd(name, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_mlp_grad_backward_column_split_bit_equal(name):
+    """k_mlp_grad_backward32_cs (option bwd_colsplit != 0) against the per-wave kernel
+    (bwd_colsplit 0): the same operations per element, every parameter gradient bit-equal, on a
+    ragged row count."""
+    from neural_raytracing_amd import _lib, set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import input_gradient
+    kw = SHAPES[name]
+    _, mine = _pair(kw, 3)
+    set_precision("fp32")
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand(2011, 3, generator=g) - 0.5).cuda()
+    v = torch.randn(2011, 3, generator=g).cuda()
+
+    def run(opt):
+        with _lib.options(bwd_colsplit=opt):
+            mine.zero_grad(set_to_none=True)
+            (input_gradient(mine, x) * v).sum().backward()
+            return [p.grad.clone() for p in mine.parameters() if p.grad is not None]
+    base, got = run(0), run(1)
+    assert len(base) == len(got) > 2
+    for i, (a, b) in enumerate(zip(base, got)):
+        assert torch.equal(a, b), (name, i, (a - b).abs().max().item())
+
+
+@pytest.mark.gpu
 def test_mlp_grad_backward_empty_and_refusals():
     from neural_raytracing_amd import NrtError
     from neural_raytracing_amd.pathtracer.neural_blocks import input_gradient
