@@ -1,5 +1,5 @@
 # GPU round script: tests, smoke, bench, rocprof, PMC traffic (each step time-limited; stop at
-# the first failure).  bash tools/run_gpu_round.sh [all|tests|bench|prof|pmc|scenes]
+# the first failure).  bash tools/run_gpu_round.sh [all|tests|bench|prof|pmc|scenes|train|trainpmc]
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -47,4 +47,14 @@ if [ "$STEP" = all ] || [ "$STEP" = train ]; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_train -o run --output-format csv -- python3 bench.py --scene train --precision mixed --steps 5 --warmup 1 > gpurun_out/prof_train.log 2>&1
   rc=$?; echo "PROF TRAIN EXIT $rc"; [ $rc -eq 0 ] || exit $rc
   mkdir -p gpurun_out/prof_train && find /tmp/prof_train -name "*kernel_stats.csv" -exec cp {} gpurun_out/prof_train/ \;
+fi
+if [ "$STEP" = trainpmc ]; then
+  # the training backward's PMC (column-split vs per-wave kernels) and the option A/B of the step
+  bash tools/pmc_train.sh || exit 1
+  python tools/pmc_train_summary.py > gpurun_out/pmc_train/summary.json || exit 1
+  rm -f gpurun_out/train_ab.jsonl
+  for OPT in 0 1 2; do
+    timeout -k 10 300 python -u bench.py --scene train --precision mixed --steps 10 --warmup 2 --nrt-option bwd_colsplit=$OPT >> gpurun_out/train_ab.jsonl 2>> gpurun_out/train_ab.err
+    rc=$?; echo "TRAIN bwd_colsplit=$OPT EXIT $rc"; [ $rc -eq 0 ] || exit $rc
+  done
 fi
