@@ -271,6 +271,54 @@ __device__ __forceinline__ void mlp_backward32(
 // so the batch runs CW times the waves at NBW accumulators each (two or more waves per SIMD), and
 // every layer boundary is a block barrier (all waves have read the slab before any overwrites it).
 // Same operations per output element in the same order: results bit-equal to the per-wave kernel.
+// gemm32 with the slab's B operand prefetched PF - 1 k-steps ahead too (rotating registers, as
+// the A fragments): the column-split kernels run one row block per wave, one MFMA per k-step,
+// where gemm32's in-step ds_read left the LDS latency exposed at ~1 wave per SIMD.  Same MFMAs
+// on the same values in the same order.
+template <int NB, int PF>
+__device__ __forceinline__ void gemm32_pb(f16v (&acc)[NB], const float* __restrict__ A, int nrb,
+                                          int rb0, int nks, const float* X, int RS, int kcol,
+                                          int act_in) {
+  using gptr = const __attribute__((address_space(1))) float*;
+  if (nks <= 0) return;
+  const int lane = lane_id();
+  const int r = lane & 31, h = lane >> 5;
+  const float* xr = X + r * RS + kcol + h;
+  const gptr Ag = (gptr)(A + (size_t)rb0 * 64 + lane);
+  const int stride = nrb * 64;
+  int off[NB];
+#pragma unroll
+  for (int ib = 0; ib < NB; ++ib) off[ib] = (rb0 + ib < nrb ? ib : nrb - 1 - rb0) * 64;
+  float a[PF][NB], bq[PF];
+#pragma unroll
+  for (int p = 0; p < PF; ++p) {
+    const int sp = p < nks ? p : nks - 1;
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)sp * stride + off[ib]];
+    bq[p] = xr[2 * sp];
+  }
+  auto step = [&](const float (&av)[NB], float b) {
+    if (act_in >= 0) b = act_fwd<false>(b, act_in);
+#pragma unroll
+    for (int ib = 0; ib < NB; ++ib)
+      if (rb0 + ib < nrb) acc[ib] = mfma32(av[ib], b, acc[ib]);
+  };
+  int s = 0;
+  for (; s + PF <= nks; s += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      step(a[p], bq[p]);
+      const int sn = s + p + PF < nks ? s + p + PF : nks - 1;
+#pragma unroll
+      for (int ib = 0; ib < NB; ++ib) a[p][ib] = Ag[(size_t)sn * stride + off[ib]];
+      bq[p] = xr[2 * sn];
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (s + p < nks) step(a[p], bq[p]);
+}
+
 template <int NB>
 struct ColSplit {
   // row blocks per wave: one (two put the 256-column kernels at the 256-VGPR cap with spills,
@@ -335,14 +383,14 @@ __device__ __forceinline__ void mlp_backward_cs(
     bias32<NBW>(acc, m.bias[l], rbw, NB, h);
     if (l == 0) {
       if (TILE) gemm32_tile<NBW, PF>(acc, m.w32[0], NB, rbw, ke >> 1, et - r, -1);
-      else gemm32<NBW, PF>(acc, m.w32[0], NB, rbw, ke >> 1, X, RS, H, -1);
+      else gemm32_pb<NBW, PF>(acc, m.w32[0], NB, rbw, ke >> 1, X, RS, H, -1);
     } else {
       const int i = l - 1;
-      gemm32<NBW, PF>(acc, m.w32[l], NB, rbw, H >> 1, X, RS, 0, -1);
+      gemm32_pb<NBW, PF>(acc, m.w32[l], NB, rbw, H >> 1, X, RS, 0, -1);
       if (i != L - 1 && (i % m.skip) == 0) {
         const float* Ws = m.w32[l] + (H >> 1) * NB * 64;
         if (TILE) gemm32_tile<NBW, PF>(acc, Ws, NB, rbw, ke >> 1, et - r, m.act);
-        else gemm32<NBW, PF>(acc, Ws, NB, rbw, ke >> 1, X, RS, H, m.act);
+        else gemm32_pb<NBW, PF>(acc, Ws, NB, rbw, ke >> 1, X, RS, H, m.act);
       }
     }
     __syncthreads();  // every wave has read the layer's inputs from the slab
@@ -398,7 +446,7 @@ __device__ __forceinline__ void mlp_backward_cs(
       for (int rb0 = hid_rb + rbw; rb0 < nrb; rb0 += NB) {
 #pragma unroll
         for (int ib = 0; ib < NBW; ++ib) acc[ib] = f16v{};
-        gemm32<NBW, PF>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
+        gemm32_pb<NBW, PF>(acc, At, nrb, rb0, H >> 1, X, RS, 0, -1);
         // per row block: every load first (clamped addresses, unconditional), then the
         // activation's branches
 #pragma unroll
@@ -432,7 +480,7 @@ __device__ __forceinline__ void mlp_backward_cs(
     if (has_hidden_in) {
 #pragma unroll
       for (int ib = 0; ib < NBW; ++ib) acc[ib] = f16v{};
-      gemm32<NBW, PF>(acc, At, nrb, rbw, H >> 1, X, RS, 0, -1);
+      gemm32_pb<NBW, PF>(acc, At, nrb, rbw, H >> 1, X, RS, 0, -1);
     }
     __syncthreads();  // every wave has read dZ_l from the slab
     if (has_hidden_in) {
@@ -775,13 +823,13 @@ __global__ void __launch_bounds__(64 * NB, 2) k_mlp_grad_backward32_cs(
     bias32<1>(acc, m.bias[l], w, NB, h);
     act_[0] = f16v{};
     if (l == 0) {
-      gemm32<1, PF>(acc, m.w32[0], NB, w, ke >> 1, X, RS, EE, -1);
-      gemm32<1, PF>(act_, m.w32[0], NB, w, ke >> 1, X, RS, ET, -1);
+      gemm32_pb<1, PF>(acc, m.w32[0], NB, w, ke >> 1, X, RS, EE, -1);
+      gemm32_pb<1, PF>(act_, m.w32[0], NB, w, ke >> 1, X, RS, ET, -1);
     } else {
-      gemm32<1, PF>(acc, m.w32[l], NB, w, H >> 1, X, RS, 0, -1);
-      if (skip) gemm32<1, PF>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, EE, m.act);
-      gemm32<1, PF>(act_, m.w32[l], NB, w, H >> 1, X, RS, PT, -1);
-      if (skip) gemm32<1, PF>(act_, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, ET, -1);
+      gemm32_pb<1, PF>(acc, m.w32[l], NB, w, H >> 1, X, RS, 0, -1);
+      if (skip) gemm32_pb<1, PF>(acc, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, EE, m.act);
+      gemm32_pb<1, PF>(act_, m.w32[l], NB, w, H >> 1, X, RS, PT, -1);
+      if (skip) gemm32_pb<1, PF>(act_, m.w32[l] + (H >> 1) * NB * 64, NB, w, ke >> 1, X, RS, ET, -1);
     }
     __syncthreads();  // every wave has read the layer's inputs
 #pragma unroll
@@ -833,8 +881,8 @@ __global__ void __launch_bounds__(64 * NB, 2) k_mlp_grad_backward32_cs(
     const int nrb = m.nbt[l];
     acc[0] = f16v{};
     act_[0] = f16v{};
-    gemm32<1, PF>(acc, At, nrb, w, H >> 1, X, RS, 0, -1);
-    gemm32<1, PF>(act_, At, nrb, w, H >> 1, X, RS, PT, -1);
+    gemm32_pb<1, PF>(acc, At, nrb, w, H >> 1, X, RS, 0, -1);
+    gemm32_pb<1, PF>(act_, At, nrb, w, H >> 1, X, RS, PT, -1);
     __syncthreads();
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
