@@ -308,6 +308,10 @@ def main():
                 extra["mixed"] = fp16_leg(rr, args, rows, size, precision="mixed")
             extra.update(extra_legs(scene, cameras, size, args, rows))
             extra["api_paths"] = api_path_legs(scene, args)
+            # the training step (training_utils.py:246-285) at the reference's
+            # arithmetic and with the mixed march, each with its backward roofline
+            extra["train"] = {p: train_leg(p, 10, 2, cpu=(p == "fp32" and not args.no_cpu_baseline))
+                              for p in ("fp32", "mixed")}
         if not args.no_cpu_baseline:
             extra.update(cpu_baseline(scene, size, args))
 
@@ -457,8 +461,17 @@ def fp16_leg(rr, args, rows, size, steps=5, warmup=2, precision="fp16"):
         if ks[k][1]:
             roof[k + "_ms"] = ks[k][0] / ks[k][1]
     if precision == "mixed":
-        roof["note"] = ("the evaluations counted include the split refinement's; the FP16 peak "
-                        "prices them all, so the fraction is a lower bound")
+        # the evaluation count includes the split refinement's (k_refine3 / k_best3), so the
+        # executed rate divides it by the time of all three kernels; each split evaluation is
+        # priced at one product although it issues three, so this is a lower bound
+        k_ms = sum(ks[k][0] for k in ("k_march16", "k_refine3", "k_best3")) / max(ks["k_march16"][1], 1)
+        roof["executed_achieved"] = roof["executed_flop_per_launch"] / (k_ms * 1e-3) / 1e12
+        roof["executed_frac"] = roof["executed_achieved"] / roof["peak"]
+        roof["executed_ms_per_launch"] = k_ms
+        roof["note"] = ("executed_*: every counted evaluation (the FP16 march's and the split "
+                        "refinement's, each priced at one product) over the time of k_march16 + "
+                        "k_refine3 + k_best3 -- a lower bound, as a split evaluation issues three "
+                        "products; frac / achieved: the algorithmic count over k_march16 alone")
     return {"value": frame_rays * args.samples * steps / el, "unit": "ray-samples/s",
             "ms_per_step": 1000 * el / steps, "steps": steps, "dtype": precision,
             "roofline": roof,
@@ -844,11 +857,59 @@ def colocate_valu_roofline(size, args, kernel_ms):
 
 
 def bench_train(args):
+    """`--scene train`: one JSON line of the training step (train_leg)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+        raise SystemExit("--scene train runs on one GPU")
+    device = torch.device("cuda", 0)
+    torch.cuda.set_device(device)
+    from neural_raytracing_amd import _lib
+    _lib.load(require_device=True)
+    # --precision fp16 / mixed / fp32-split: the gradient-free march (and, fp16, the MLP
+    # forwards) at that precision, every backward FP32 (default fp32: the reference's arithmetic)
+    prec = args.precision if args.precision_set else "fp32"
+    line = train_leg(prec, args.steps, args.warmup, size=args.size, crop=args.crop,
+                     views=args.views, samples=args.samples, cpu=not args.no_cpu_baseline,
+                     torch_profile=args.torch_profile)
+    print(json.dumps(line), flush=True)
+
+
+TRAIN_KERNELS = ("k_mlp_backward32", "k_wgrad", "k_mlp_grad_backward32")
+
+
+def train_roofline(steps):
+    """Roofline of the training step's backward launches over the timed steps: per kernel the
+    algorithmic FLOP the library recorded (nrt_profile_flop: the MLP backward's forward recompute
+    + input-gradient chain, the split-K weight gradients, the SDF normal's double backward, at
+    the layers' real widths) over its HIP-event time, against the 157.3 TF FP32 matrix peak; the
+    headline entry is the kernel with the most time."""
+    from neural_raytracing_amd import _lib
+    per = {}
+    for k in TRAIN_KERNELS:
+        ms, n = _lib.profile_read(k)
+        flop = _lib.profile_flop(k)
+        ach = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        per[k] = {"ms_per_step": ms / steps, "launches_per_step": n / steps,
+                  "flop_per_step": flop / steps, "achieved": ach,
+                  "frac": ach / PEAK_TFLOPS["fp32"]}
+    top = max(per, key=lambda k: per[k]["ms_per_step"])
+    return {"bound": "mfma", "kernel": top, "achieved": per[top]["achieved"],
+            "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s", "frac": per[top]["frac"],
+            "traffic": None, "flop_basis": "algorithmic: 2 FLOP per multiply-add of every layer "
+                                           "product at its real width (include/nrt.h "
+                                           "nrt_profile_flop)",
+            "kernels": per}
+
+
+def train_leg(prec, steps, warmup, size=256, crop=80, views=6, samples=64, cpu=True,
+              torch_profile=None):
     """One-GPU training-step line: the nerf_synthetic training iteration of
     training_utils.py:246-285 / scripts/nerf_synthetic.py:61-116 -- N=6 views, an 80x80 crop of
     a 256^2 frame, SDF(SphereSDF(n=128), max_steps=64), 8 NeuralBSDF(Softplus) +
     ComposeSpatialVarying, LightField, NeRFIntegrator(Direct); loss = MSE + eikonal(raw_normals);
-    backward through the fused path; AdamW with the script's three learning rates.  FP32."""
+    backward through the fused path; AdamW with the script's three learning rates.  `prec` sets
+    the gradient-free march's arithmetic (fp32 = the reference's; mixed = FP16 march with its
+    undecidable steps at FP32 accuracy); every MLP forward and backward is FP32 except under
+    fp16.  The process precision is restored afterwards."""
     from neural_raytracing_amd import _lib
     import neural_raytracing_amd as nra
     import neural_raytracing_amd.pathtracer as pt
@@ -856,14 +917,8 @@ def bench_train(args):
     from neural_raytracing_amd.pathtracer.integrators import Direct, NeRFIntegrator
     from neural_raytracing_amd.pathtracer.lights import LightField
     from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--scene train runs on one GPU")
-    device = torch.device("cuda", 0)
-    torch.cuda.set_device(device)
-    _lib.load(require_device=True)
-    # --precision fp16: mixed precision -- the gradient-free march / scan and the MLP forwards on
-    # the FP16 kernels, every backward in FP32 (default fp32: the reference's arithmetic)
-    prec = args.precision if args.precision_set else "fp32"
+    device = torch.device("cuda", torch.cuda.current_device())
+    old_prec = nra.get_precision()
     nra.set_precision(prec)
     torch.manual_seed(0)
     random.seed(0)
@@ -872,7 +927,7 @@ def bench_train(args):
         for a in [sdf.shift.init, *sdf.shift.layers]:
             a.weight.normal_(0.0, 0.02)
         sdf.shift.out.weight.normal_(0.0, 0.002)
-    shape = SDF(sdf=sdf.to(device), device=device, max_steps=args.samples)
+    shape = SDF(sdf=sdf.to(device), device=device, max_steps=samples)
     bsdf = ComposeSpatialVarying([NeuralBSDF(activation=torch.nn.Softplus(), device="cpu")
                                   for _ in range(8)], device="cpu")
     for b in bsdf.bsdfs:
@@ -885,7 +940,7 @@ def bench_train(args):
         {"params": list(bsdf.parameters()), "lr": 8e-4},
         {"params": list(lights.parameters()), "lr": 8e-5},
     ], lr=8e-5, weight_decay=0)
-    size, crop, N = args.size, args.crop, args.views
+    N = views
     focal = float(0.5 * size / math.tan(0.5 * 0.6911))
     c2w = torch.stack([view_c2w(i, N) for i in range(N)]).to(device)
     cameras = pt.cameras.NeRFCamera(cam_to_world=c2w, focal=focal, device=device)
@@ -908,60 +963,31 @@ def bench_train(args):
         opt.step()
         return loss
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
-    if args.torch_profile:
-        # op counts of one step by Python call site (tools: where the launches come from)
-        from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
-            step(10_000)
-            torch.cuda.synchronize()
-        # host synchronisations of one step by call site (torch.cuda sync debug mode)
-        import collections
-        import traceback
-        import warnings
-        sites = collections.Counter()
-
-        def show(message, category, filename, lineno, file=None, line=None):
-            stack = [f for f in traceback.extract_stack()[:-1]
-                     if "site-packages" not in f.filename and "warnings" not in f.filename]
-            sites[" <- ".join(f"{f.filename.split('/')[-1]}:{f.lineno}" for f in stack[-4:])] += 1
-        old_show = warnings.showwarning
-        warnings.showwarning = show
-        torch.cuda.set_sync_debug_mode("warn")
-        try:
-            with warnings.catch_warnings():
-                warnings.simplefilter("always")
-                warnings.showwarning = show
-                step(10_001)
-                torch.cuda.synchronize()
-        finally:
-            torch.cuda.set_sync_debug_mode(0)
-            warnings.showwarning = old_show
-        with open(args.torch_profile, "w") as f:
-            f.write(prof.key_averages().table(sort_by="count", row_limit=120,
-                                              max_name_column_width=40))
-            f.write("\n\nhost syncs by call site (one step)\n")
-            for site, n in sites.most_common():
-                f.write(f"{n:6d}  {site}\n")
-    _lib.profile_reset()
-    _lib.profile_enable(True)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(args.warmup + i)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    _lib.profile_enable(False)
-    kms = {k: _lib.profile_read(k)[0] / args.steps
-           for k in ("k_intersect", "k_mlp_backward32", "k_mlp_grad_backward32", "k_wgrad")}
+    try:
+        for i in range(warmup):
+            step(i)
+        torch.cuda.synchronize()
+        if torch_profile:
+            train_torch_profile(step, torch_profile)
+        _lib.profile_reset()
+        _lib.profile_enable(True)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            loss = step(warmup + i)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        _lib.profile_enable(False)
+        roof = train_roofline(steps)
+        kms = {k: _lib.profile_read(k)[0] / steps for k in ("k_intersect",) + TRAIN_KERNELS}
+    finally:
+        nra.set_precision(old_prec)
     rays = N * crop * crop
     line = {
         "metric": f"training ray-samples/sec/GPU (nerf_synthetic step, {N}x{crop}x{crop} crop "
-                  f"of {size}^2, {args.samples} march steps)",
-        "value": rays * args.samples * args.steps / elapsed, "unit": "ray-samples/s",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True,
+                  f"of {size}^2, {samples} march steps)",
+        "value": rays * samples * steps / elapsed, "unit": "ray-samples/s",
+        "n_gpus": 1, "steps": steps, "warmup": warmup,
+        "ms_per_step": 1000 * elapsed / steps, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {"fp32": "fp32", "fp16": "fp16 forward / fp32 backward",
                   "fp32-split": "fp32-split forward (f16 hi/lo MFMA) / fp32 backward",
@@ -971,15 +997,53 @@ def bench_train(args):
         "config": {"workload": "forward (fused march + scan) + backward (MLP backward, SDF-normal "
                                "double backward, shading autograd) + AdamW",
                    "views": N, "crop": crop, "image": [size, size],
-                   "samples_per_ray": args.samples, "precision": prec},
+                   "samples_per_ray": samples, "precision": prec},
+        "roofline": roof,
         "kernel_ms_per_step": kms, "final_loss": float(loss),
     }
-    if not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_train_baseline(sdf, bsdf, lights, size, focal, args)
-    print(json.dumps(line), flush=True)
+    if cpu:
+        line["cpu_baseline"] = cpu_train_baseline(sdf, bsdf, lights, size, focal, samples)
+    return line
 
 
-def cpu_train_baseline(sdf, bsdf, lights, size, focal, args, crop=48):
+def train_torch_profile(step, path):
+    """Op counts of one training step by Python call site and its host synchronisations (tools:
+    where the launches come from), written to `path`."""
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+        step(10_000)
+        torch.cuda.synchronize()
+    # host synchronisations of one step by call site (torch.cuda sync debug mode)
+    import collections
+    import traceback
+    import warnings
+    sites = collections.Counter()
+
+    def show(message, category, filename, lineno, file=None, line=None):
+        stack = [f for f in traceback.extract_stack()[:-1]
+                 if "site-packages" not in f.filename and "warnings" not in f.filename]
+        sites[" <- ".join(f"{f.filename.split('/')[-1]}:{f.lineno}" for f in stack[-4:])] += 1
+    old_show = warnings.showwarning
+    warnings.showwarning = show
+    torch.cuda.set_sync_debug_mode("warn")
+    try:
+        with warnings.catch_warnings():
+            warnings.simplefilter("always")
+            warnings.showwarning = show
+            step(10_001)
+            torch.cuda.synchronize()
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+        warnings.showwarning = old_show
+    with open(path, "w") as f:
+        f.write(prof.key_averages().table(sort_by="count", row_limit=120,
+                                          max_name_column_width=40))
+        f.write("\n\nhost syncs by call site (one step)\n")
+        for site, n in sites.most_common():
+            f.write(f"{n:6d}  {site}\n")
+
+
+def cpu_train_baseline(sdf, bsdf, lights, size, focal, samples, crop=48):
     """The oracle (torch-CPU restatement, 'port') running the same training step -- forward,
     create_graph normals, loss = MSE + eikonal, backward -- on one view's crop x crop window, on
     this host's threads; rate in training ray-samples/s like the GPU line."""
@@ -990,7 +1054,7 @@ def cpu_train_baseline(sdf, bsdf, lights, size, focal, args, crop=48):
         blob.radii.copy_(sdf.radii.cpu())
         blob.tfs.copy_(sdf.tfs.cpu())
     _copy_to_oracle(blob.shift, sdf.shift)
-    shape = R.MarchedSDF(sdf=blob, max_steps=args.samples, create_graph=True)
+    shape = R.MarchedSDF(sdf=blob, max_steps=samples, create_graph=True)
     parts = [R.NeuralBSDFRef(activation="softplus") for _ in bsdf.bsdfs]
     for a, b in zip(parts, bsdf.bsdfs):
         _copy_to_oracle(a.mlp, b.mlp)
@@ -1015,9 +1079,9 @@ def cpu_train_baseline(sdf, bsdf, lights, size, focal, args, crop=48):
     loss = F.mse_loss(img[..., :3], target) + (raw.norm(dim=-1) - 1).square().mean()
     loss.backward()
     cpu_s = time.perf_counter() - t0
-    return {"value": crop * crop * args.samples / cpu_s, "unit": "ray-samples/s",
+    return {"value": crop * crop * samples / cpu_s, "unit": "ray-samples/s",
             "cores": torch.get_num_threads(), **host_cpu(), "kind": "port",
-            "sample": f"one view, {crop}x{crop} crop, {args.samples} march steps + scan, forward + "
+            "sample": f"one view, {crop}x{crop} crop, {samples} march steps + scan, forward + "
                       f"backward (oracle/pathtracer_ref.py autograd), {cpu_s:.1f} s"}
 
 

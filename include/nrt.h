@@ -457,6 +457,11 @@ int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
  * executed work behind the algorithmic count (every ray at every march step and scan point,
  * sdfs.py:119-131, 232-249), which the lane-level job lists lower.  Synchronises. */
 int nrt_profile_evals(uint64_t* evals);
+/* Algorithmic FLOP of the timed launches of kernel `name` since the last nrt_profile_reset, as
+ * the entries that launch it count them (the MLP backward and weight-gradient launches of the
+ * training path: every multiply-add of the layers' products at their real widths, 2 FLOP each);
+ * 0 for launches that record none.  With nrt_profile_read's time it gives a roofline fraction. */
+int nrt_profile_flop(const char* name, double* flop);
 
 /* ---------------------------------------------------------------------------------------
  * Runtime options (no reference counterpart: the reference has one eager implementation).

@@ -124,6 +124,7 @@ _SIGNATURES = {
     "nrt_profile_read": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_I64)]),
     "nrt_profile_evals": (_I32, [ctypes.POINTER(ctypes.c_uint64)]),
+    "nrt_profile_flop": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "nrt_set_option": (_I32, [ctypes.c_char_p, _I64]),
     "nrt_get_option": (_I32, [ctypes.c_char_p, ctypes.POINTER(_I64)]),
     "nrt_reset_options": (_I32, []),
@@ -263,3 +264,11 @@ def profile_read(name):
     check(load().nrt_profile_read(name.encode(), ctypes.byref(tot), ctypes.byref(n)),
           "nrt_profile_read")
     return tot.value, n.value
+
+
+def profile_flop(name):
+    """Algorithmic FLOP the library recorded for the timed launches of kernel `name` since the
+    last reset (the training path's MLP backward / weight-gradient launches; 0 for others)."""
+    v = ctypes.c_double()
+    check(load().nrt_profile_flop(name.encode(), ctypes.byref(v)), "nrt_profile_flop")
+    return v.value

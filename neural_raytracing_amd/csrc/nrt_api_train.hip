@@ -904,6 +904,24 @@ __global__ void k_fill(float* __restrict__ p, int64_t n, float v) {
 namespace {
 size_t a256(size_t v) { return (v + 255) & ~(size_t)255; }
 
+// Algorithmic FLOP per row (2 per multiply-add, real widths) for nrt_profile_flop: a forward
+// through the layers below the out layer (init, hidden, skip parts); the backward kernel is that
+// recompute plus the input gradient of every one of those layers and the out layer's seed; the
+// double backward runs the primal and tangent forwards and the two hidden reverse chains.
+double fwd_row_flop(const MlpDev& d) {
+  const int L = d.n_hidden, H = d.hidden;
+  double f = 2.0 * d.dp * H;
+  for (int i = 0; i < L; ++i) {
+    const bool skip = i != L - 1 && (i % d.skip) == 0;
+    f += 2.0 * H * (H + (skip ? d.dp : 0));
+  }
+  return f;
+}
+double bwd_row_flop(const MlpDev& d) { return 2.0 * fwd_row_flop(d) + 2.0 * d.out * d.hidden; }
+double grad_bwd_row_flop(const MlpDev& d) {
+  return 2.0 * fwd_row_flop(d) + 4.0 * d.hidden * d.hidden * d.n_hidden;
+}
+
 constexpr size_t kWgradTableBytes = 16384;  // device copy of a WgradBatch's job table
 
 struct TrainWs {
@@ -1143,8 +1161,10 @@ struct WgradBatch {
     for (auto& j : jobs) { blocks += (int64_t)j.n_tiles * S; total += (int64_t)j.R * j.C; }
     NRT_HIP(hipMemcpyAsync(table, jobs.data(), jobs.size() * sizeof(WgradJob), hipMemcpyHostToDevice, st));
     const WgradJob* tj = (const WgradJob*)table;
+    double flop = 0.0;
+    for (auto& j : jobs) flop += 2.0 * j.R * j.C * (double)j.M;
     {
-      ProfScope prof("k_wgrad", st);
+      ProfScope prof("k_wgrad", st, flop);
       k_wgrad_batch<><<<dim3((unsigned)blocks), dim3(64 * kWgradWaves), 0, st>>>(tj, (int)jobs.size(), S, part);
       if (int rc = check_launch("k_wgrad_batch")) return rc;
     }
@@ -1308,7 +1328,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
   {
-    ProfScope prof("k_mlp_backward32", st);
+    ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M);
     NRT_NB_SWITCH(d.nb, {
       if (cs) {
         const dim3 gcs(waves), bcs(64 * NRT_CW(NB));
@@ -1411,7 +1431,7 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   dim3 grid(ceil_div64(waves, lp.waves), n), block(64 * lp.waves);
   int rc = NRT_OK;
   {
-    ProfScope prof("k_mlp_backward32", st);
+    ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M * n);
     NRT_NB_SWITCH(d.nb, {
       if (cs) {
         const dim3 gcs(waves, n), bcs(64 * NRT_CW(NB));
@@ -1512,7 +1532,7 @@ int nrt_mlp_grad_backward(const nrt_mlp* m, const float* x, const float* latent,
   const bool cs = option(OPT_BWD_COLSPLIT) != 0;
   int rc = NRT_OK;
   {
-    ProfScope prof("k_mlp_grad_backward32", st);
+    ProfScope prof("k_mlp_grad_backward32", st, grad_bwd_row_flop(d) * (double)M);
     NRT_NB_SWITCH(d.nb, {
       if (cs) {
         const size_t bcs = (size_t)per_wave * 4;

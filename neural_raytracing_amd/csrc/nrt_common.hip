@@ -45,12 +45,13 @@ static int option_index(const char* name) {
 struct ProfRec {
   std::string name;
   hipEvent_t a, b;
+  double flop;
 };
 static bool g_prof = false;        // NRT_PROF_TIMING: hipEvents around the profiled launches
 static bool g_prof_evals = false;  // NRT_PROF_EVALS: the ring marches' evaluation counter
 static std::vector<ProfRec> g_recs;
 
-ProfScope::ProfScope(const char* n, hipStream_t s) : name(n), stream(s) {
+ProfScope::ProfScope(const char* n, hipStream_t s, double f) : name(n), stream(s), flop(f) {
   if (!g_prof) return;
   if (hipEventCreate(&start) != hipSuccess) { start = nullptr; return; }
   (void)hipEventRecord(start, stream);
@@ -61,7 +62,7 @@ ProfScope::~ProfScope() {
   hipEvent_t stop;
   if (hipEventCreate(&stop) != hipSuccess) return;
   (void)hipEventRecord(stop, stream);
-  g_recs.push_back({name, start, stop});
+  g_recs.push_back({name, start, stop, flop});
 }
 
 static unsigned long long* g_evals[64] = {};
@@ -122,6 +123,15 @@ int nrt_profile_read(const char* name, double* total_ms, int64_t* launches) {
   }
   if (total_ms) *total_ms = tot;
   if (launches) *launches = n;
+  return NRT_OK;
+}
+
+int nrt_profile_flop(const char* name, double* flop) {
+  if (!flop) { set_error("nrt_profile_flop: null argument"); return NRT_EINVAL; }
+  double tot = 0.0;
+  for (auto& r : nrt::g_recs)
+    if (!name || r.name == name) tot += r.flop;
+  *flop = tot;
   return NRT_OK;
 }
 

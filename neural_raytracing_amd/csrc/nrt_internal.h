@@ -124,7 +124,8 @@ struct ProfScope {
   const char* name;
   hipStream_t stream;
   hipEvent_t start = nullptr;
-  ProfScope(const char* n, hipStream_t s);
+  double flop = 0.0;  // algorithmic FLOP of the bracketed launches (nrt_profile_flop)
+  ProfScope(const char* n, hipStream_t s, double flop = 0.0);
   ~ProfScope();
 };
 void set_error(const std::string& msg);

@@ -22,6 +22,15 @@ namespace {
 
 constexpr int kSphF = 13;  // T (9, row-major), c (3), R
 constexpr int kSmBlock = 256;
+constexpr int kMaxSpheres = 64 * 1024 / (kSphF * 4);  // the LDS table's capacity (1,260)
+constexpr int64_t kSliceMin = 4096;                    // points per backward slice at least
+constexpr int kMaxSlices = 32;
+
+// point slices of the sphere-parameter backward: the grid is spheres x slices, each block sums
+// its slice, k_smoothmin_reduce adds the slices in order (deterministic)
+int bwd_slices(int64_t P) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSlices, (P + kSliceMin - 1) / kSliceMin));
+}
 
 // sphere table into LDS: [n][13]
 __device__ __forceinline__ void stage_spheres(float* ls, const float* __restrict__ centers,
@@ -115,15 +124,18 @@ __global__ void __launch_bounds__(kSmBlock) k_smoothmin_pre(
   }
 }
 
-// one block per sphere: the 13 parameter gradients summed over the points in a fixed order
+// block (sphere j, slice s): the 13 parameter gradients summed over the slice's points in a fixed
+// order, into part[(j S + s) 13 + f]
 __global__ void __launch_bounds__(kSmBlock) k_smoothmin_bwd(
     const float* __restrict__ p, int64_t P, const float* __restrict__ centers,
     const float* __restrict__ radii, const float* __restrict__ tfs, int n, float k,
     const float* __restrict__ dvalue, const float* __restrict__ dgrad,
-    const float2* __restrict__ pre, float* __restrict__ dcenters, float* __restrict__ dradii,
-    float* __restrict__ dtfs) {
+    const float2* __restrict__ pre, float* __restrict__ part) {
   __shared__ float red[kSphF][kSmBlock];
   const int j = blockIdx.x;
+  const int S = (int)gridDim.y;
+  const int64_t per = (P + S - 1) / S;
+  const int64_t i0 = (int64_t)blockIdx.y * per, i1 = std::min<int64_t>(P, i0 + per);
   float s[kSphF];
   for (int f = 0; f < 9; ++f) s[f] = tfs[j * 9 + f] + ((f == 0 || f == 4 || f == 8) ? 1.f : 0.f);
   for (int f = 0; f < 3; ++f) s[9 + f] = centers[j * 3 + f];
@@ -131,7 +143,7 @@ __global__ void __launch_bounds__(kSmBlock) k_smoothmin_bwd(
   float acc[kSphF];
 #pragma unroll
   for (int f = 0; f < kSphF; ++f) acc[f] = 0.f;
-  for (int64_t i = threadIdx.x; i < P; i += blockDim.x) {
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const float2 pr = pre[i];
     if (pr.x == 0.f) continue;  // clamped: v constant, g = 0
     const float x = p[i * 3], y = p[i * 3 + 1], z = p[i * 3 + 2];
@@ -178,13 +190,21 @@ __global__ void __launch_bounds__(kSmBlock) k_smoothmin_bwd(
       for (int f = 0; f < kSphF; ++f) red[f][threadIdx.x] += red[f][threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x < kSphF) {
-    const int f = threadIdx.x;
-    const float r = red[f][0];
-    if (f < 9) { if (dtfs) dtfs[j * 9 + f] = r; }
-    else if (f < 12) { if (dcenters) dcenters[j * 3 + (f - 9)] = r; }
-    else if (dradii) dradii[j] = r;
-  }
+  if (threadIdx.x < kSphF) part[((int64_t)j * S + blockIdx.y) * kSphF + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// (sphere j, field f): the slices' partial sums in slice order
+__global__ void k_smoothmin_reduce(const float* __restrict__ part, int n, int S,
+                                   float* __restrict__ dcenters, float* __restrict__ dradii,
+                                   float* __restrict__ dtfs) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * kSphF) return;
+  const int j = e / kSphF, f = e % kSphF;
+  float r = 0.f;
+  for (int s = 0; s < S; ++s) r += part[((int64_t)j * S + s) * kSphF + f];
+  if (f < 9) { if (dtfs) dtfs[j * 9 + f] = r; }
+  else if (f < 12) { if (dcenters) dcenters[j * 3 + (f - 9)] = r; }
+  else if (dradii) dradii[j] = r;
 }
 
 int grid_for(int64_t P) {
@@ -199,7 +219,8 @@ using namespace nrt;
 extern "C" {
 
 size_t nrt_sphere_smoothmin_workspace_bytes(int64_t P) {
-  return (size_t)std::max<int64_t>(P, 1) * sizeof(float2);
+  const size_t pre = ((size_t)std::max<int64_t>(P, 1) * sizeof(float2) + 255) & ~(size_t)255;
+  return pre + (size_t)kMaxSpheres * bwd_slices(P) * kSphF * sizeof(float);
 }
 
 int nrt_sphere_smoothmin_forward(const float* p, int64_t P, const float* centers,
@@ -237,12 +258,17 @@ int nrt_sphere_smoothmin_backward(const float* p, int64_t P, const float* center
   const size_t lds = (size_t)n * kSphF * sizeof(float);
   if (lds > 64 * 1024) { set_error("nrt_sphere_smoothmin_backward: too many spheres"); return NRT_EINVAL; }
   float2* pre = (float2*)workspace;
+  float* part = (float*)((char*)workspace + (((size_t)P * sizeof(float2) + 255) & ~(size_t)255));
+  const int S = bwd_slices(P);
   k_smoothmin_pre<<<dim3(grid_for(P)), dim3(kSmBlock), lds, st>>>(p, P, centers, radii, tfs, n,
                                                                   k, dgrad, pre);
   if (int rc = check_launch("k_smoothmin_pre")) return rc;
-  k_smoothmin_bwd<<<dim3(n), dim3(kSmBlock), 0, st>>>(p, P, centers, radii, tfs, n, k, dvalue,
-                                                     dgrad, pre, dcenters, dradii, dtfs);
-  return check_launch("k_smoothmin_bwd");
+  k_smoothmin_bwd<<<dim3(n, S), dim3(kSmBlock), 0, st>>>(p, P, centers, radii, tfs, n, k, dvalue,
+                                                        dgrad, pre, part);
+  if (int rc = check_launch("k_smoothmin_bwd")) return rc;
+  k_smoothmin_reduce<<<dim3((n * kSphF + 255) / 256), dim3(256), 0, st>>>(part, n, S, dcenters,
+                                                                         dradii, dtfs);
+  return check_launch("k_smoothmin_reduce");
 }
 
 }  // extern "C"

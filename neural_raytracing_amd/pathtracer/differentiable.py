@@ -126,6 +126,13 @@ def needs_grad(*modules):
 
 
 SMOOTHMIN_K = 32.0  # sdfs.py:43 / utils.py:386-387
+# nrt_sphere_smoothmin_* stage the sphere table (13 floats a sphere) in 64 KB of LDS: larger
+# SphereSDFs train on the torch restatement (sphere_part under autograd)
+SMOOTHMIN_MAX_SPHERES = 64 * 1024 // (13 * 4)
+
+
+def _fused_smoothmin(sdf, p):
+    return p.is_cuda and sdf.centers.shape[0] <= SMOOTHMIN_MAX_SPHERES
 
 
 class _SphereSmoothMinFn(torch.autograd.Function):
@@ -196,7 +203,7 @@ def sdf_value(sdf, p):
     if isinstance(sdf, SkipConnMLP):
         return sdf(p).reshape(p.shape[:-1])
     if _is_sphere_sdf(sdf):
-        if p.is_cuda and not p.requires_grad:
+        if _fused_smoothmin(sdf, p) and not p.requires_grad:
             out = sphere_smoothmin(sdf, p)[0]  # fused forward + parameter backward
         else:  # points with a gradient (an SDF callable warping them): the torch restatement
             out = sphere_part(sdf, p)
@@ -218,7 +225,7 @@ def sdf_gradient(sdf, p):
     if isinstance(sdf, SkipConnMLP):
         return input_gradient(sdf, p)
     if _is_sphere_sdf(sdf):
-        if p.is_cuda:
+        if _fused_smoothmin(sdf, p):
             g = sphere_smoothmin(sdf, p)[1]  # fused gradient + its double backward
         else:
             with torch.enable_grad():

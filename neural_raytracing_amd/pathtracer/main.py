@@ -8,8 +8,10 @@ import random
 
 import torch
 
+from .. import _lib
 from .differentiable import needs_grad
-from .render import fused_integrator, render_tiles
+from . import render as _render
+from .render import fused_integrator
 from .shapes.sdfs import is_hip_sdf
 from .samplers import Sampler
 
@@ -63,9 +65,18 @@ def _fused(integrator, cameras, w_isect, addition):
 def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=None, height=None,
               chunk_size=32, bundle_size=4, background=1, addition=nothing, sampler=Sampler(),
               silent=False, trim=0, device="cuda", squeeze_first=True, w_isect=False,
-              with_noise=1e-3):
+              with_noise=1e-3, shard=None, group=None):
     """main.py:13-93.  trim > 0 renders each tile with a trim-pixel border of extra rays
-    (main.py:67-68) and keeps the tile's interior (see _composite)."""
+    (main.py:67-68) and keeps the tile's interior (see _composite).
+
+    Multi-GPU (the parallelism TODO of main.py:60): under an initialised torch.distributed
+    process group of several ranks that all ask for the same frame, the fused tile path renders
+    only this rank's bands of tile rows (band j of chunk_size rows when j % world == rank) and
+    one all-gather assembles the frame on every rank; the frame is the single-process frame (every
+    tile's camera and scan jitter is drawn in the reference's order on every rank).  shard: None =
+    automatic, False = render the whole frame on every rank, True = require sharding (render.
+    shard_of); group: the process group.  The scene's weights must be equal on the ranks
+    (render.broadcast_module replicates them)."""
     if trim < 0:
         raise ValueError("trim must be >= 0")
     batch_dims = len(cameras)
@@ -81,8 +92,10 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     ys = list(range(0, height, chunk_size))
     it = None
     fused = _fused(integrator, cameras, w_isect, addition) if trim == 0 else None
-    if needs_grad(shapes, bsdf, lights):
-        fused = None  # training: integrator.sample carries the gradients
+    if needs_grad(shapes, bsdf, lights, w_isect):
+        # training (a learned occlusion MLP included, as Direct.sample checks it):
+        # integrator.sample carries the gradients
+        fused = None
     if not hasattr(shapes, "sdf") or not is_hip_sdf(shapes.sdf):
         # an SDF callable (SDF.intersect evaluates it between the HIP march steps) or another
         # shape (the analytic Sphere): integrator.sample on its own intersect, tile by tile
@@ -95,8 +108,18 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
         for ij in range(len(xs) * len(ys)):
             i, j = divmod(ij, len(ys))
             tiles.append((xs[j], ys[i]))
-        render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk_size, size,
-                     with_noise, background)
+        sh = _render.shard_of(cameras, size, width, chunk_size, background, group, shard)
+        keep = None
+        if sh is not None:
+            rank, world = sh
+            keep = lambda k: (k % len(ys)) % world == rank  # noqa: E731  (band j = k % len(ys))
+        _render.render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk_size, size,
+                             with_noise, background, keep=keep)
+        if sh is not None:
+            _render.gather_tile_rows(out, chunk_size, sh[0], sh[1], group)
+    elif shard:
+        raise _lib.NrtError("pathtrace(shard=True) renders on the fused tile path only "
+                            "(Direct / NeRFIntegrator(Direct), no addition hook, a packed SDF)")
     for ij in range(len(xs) * len(ys) if fused is None else 0):
         i, j = divmod(ij, len(ys))
         x0, y0 = xs[j], ys[i]

@@ -170,21 +170,23 @@ class _MlpFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        import ctypes
         _check_versions(ctx)
         if torch.is_grad_enabled():
-            # create_graph=True through SkipConnMLP.forward (e.g. autograd normals of an SDF
-            # callable that wraps the MLP, under training): the HIP backward has no graph, and a
-            # silently non-differentiable gradient would drop the eikonal term's contribution
-            raise _lib.NrtError("second derivatives through SkipConnMLP.forward are not on the HIP "
-                                "path (the SDF normal of a packed SDF uses nrt_mlp_grad_backward; "
-                                "an SDF callable wrapping an MLP trains without create_graph)")
+            return _MlpFn._backward_create_graph(ctx, dy)
+        dx, dlat, grads = _MlpFn._first_order(ctx, dy)
+        return (None, dx, dlat, *grads)
+
+    @staticmethod
+    def _first_order(ctx, dy):
+        """dL/dx, dL/dlatent and the nn.Linear gradients from nrt_mlp_backward (no graph)."""
+        import ctypes
         x, lat = ctx.saved_tensors
-        lat = lat if ctx.has_lat else None
+        x = x.detach()
+        lat = lat.detach() if ctx.has_lat else None
         mlp = ctx.mlp
         lib = _lib.load(require_device=True)
         M = x.shape[0]
-        dy = dy.float().contiguous()
+        dy = dy.detach().float().contiguous()
         lins = mlp._linears()
         idx = _live_rows([dy], M)
         if idx is not None:  # the rows with a gradient only (COMPACT_MIN_DEAD)
@@ -211,8 +213,55 @@ class _MlpFn(torch.autograd.Function):
                 dx = torch.zeros_like(full_x).index_copy_(0, idx, dx)
             if dlat is not None:
                 dlat = torch.zeros_like(full_lat).index_copy_(0, idx, dlat)
-        grads = [g for pair in zip(dws, dbs) for g in pair]
+        return dx, dlat, [g for pair in zip(dws, dbs) for g in pair]
+
+    @staticmethod
+    def _backward_create_graph(ctx, dy):
+        """backward under create_graph=True -- SDF.autograd_diff (sdfs.py:184-197) through an SDF
+        callable that wraps a trainable SkipConnMLP (edit_dtu.py:86-100: bend / disp): the input
+        gradient as a differentiable function of the weights.  For a one-output MLP,
+        dL/dx = dy * g(x) with g = d y / d x (input_gradient: nrt_mlp_backward forward,
+        nrt_mlp_grad_backward for its weight gradients) and dy a differentiable tensor too.  The
+        second derivative with respect to x itself is not formed: the points come from the no-grad
+        march, and a graph from x back to a trainable parameter raises.  The nn.Linear gradients
+        returned beside it carry no graph (autograd_diff asks for the points' gradient only)."""
+        x, lat = ctx.saved_tensors
+        mlp = ctx.mlp
+        if ctx.has_lat:
+            raise _lib.NrtError("second derivatives through a latent SkipConnMLP are not on the "
+                                "HIP path")
+        if mlp.out.out_features != 1:
+            raise _lib.NrtError("second derivatives through SkipConnMLP.forward are on the HIP "
+                                "path for one-output MLPs (an SDF) only")
+        if _parameters_upstream(x):
+            raise _lib.NrtError("second derivatives with respect to the MLP's inputs are not on "
+                                "the HIP path: the SDF callable's points depend on a trainable "
+                                "parameter")
+        with torch.no_grad():
+            _, dlat, grads = _MlpFn._first_order(ctx, dy)
+        dx = None
+        if ctx.needs_input_grad[1]:
+            g = input_gradient(mlp, x.detach())
+            dx = dy.reshape(-1, 1).to(g.dtype) * g
         return (None, dx, dlat, *grads)
+
+
+def _parameters_upstream(t, limit=20000):
+    """True when the autograd graph of `t` reaches an nn.Parameter (a leaf that trains)."""
+    fn = t.grad_fn
+    if fn is None:
+        return isinstance(t, nn.Parameter)
+    seen, stack = set(), [fn]
+    while stack and len(seen) < limit:
+        f = stack.pop()
+        if f is None or f in seen:
+            continue
+        seen.add(f)
+        var = getattr(f, "variable", None)
+        if isinstance(var, nn.Parameter):
+            return True
+        stack.extend(n for n, _ in getattr(f, "next_functions", ()))
+    return False
 
 
 def _shape_key(m):

@@ -56,10 +56,13 @@ def _buffers(P, nb, device):
     return b
 
 
-def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None, w_isect=False):
+def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None, w_isect=False,
+                   scan_draws=None):
     """Run intersect + shade on flat rays [P,6]; returns the buffer set (rgb zero on misses).
     scan_groups: for batched tiles, the number of tiles G; ray r belongs to tile r // (P // G)
     and each tile draws its own scan jitter (random.random(), sdfs.py:236), in tile order.
+    scan_draws: those G uniforms already drawn by the caller (render_tiles draws every tile's,
+    the ones a rank does not render included, so the frame does not depend on the world size).
     w_isect: Direct's emitter sample with a shadow ray (True) or a learned occlusion MLP, as
     Direct.sample picks it (integrators.py:161-166)."""
     P = rays_flat.shape[0]
@@ -76,10 +79,12 @@ def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None, w_
     groups = None
     if primary:
         dist = getattr(shapes, "dist", 2.2)
+        if scan_draws is None:
+            scan_draws = [random.random() for _ in range(scan_groups or 1)]
         if scan_groups is None:
-            scan_max_t = dist + random.random() * (2 / 128)
+            scan_max_t = dist + scan_draws[0] * (2 / 128)
         else:
-            groups = torch.tensor([dist + random.random() * (2 / 128) for _ in range(scan_groups)],
+            groups = torch.tensor([dist + u * (2 / 128) for u in scan_draws],
                                   dtype=torch.float64).to(dev, non_blocking=True)
     mp = _lib.MarchParams(int(shapes.max_steps), float(shapes.epsilon), 10.0, int(primary),
                           float(scan_max_t), _lib.precision_code())
@@ -133,32 +138,121 @@ MAX_BATCH_RAYS = 1 << 22
 
 
 def render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk, size, with_noise,
-                 background, ox=0, oy=0):
+                 background, ox=0, oy=0, keep=None):
     """pathtrace's fused tile loop (main.py:63-90) as few launch chains as possible: the rays of
     consecutive tiles are generated tile by tile (same camera-jitter draws, same order), marched,
     scanned and shaded in one nrt_sdf_intersect + nrt_shade_direct over all of them -- each tile
     keeps its own scan jitter (nrt_march_params.scan_max_t_groups) -- and composited tile by
     tile.  Equal to rendering the tiles one at a time; the GPU sees up to MAX_BATCH_RAYS rays per
-    launch instead of chunk_size^2."""
+    launch instead of chunk_size^2.
+    keep: predicate on the tile index -- only those tiles are rendered (a rank's row-tile shard,
+    pathtrace under torch.distributed); every tile's camera jitter and scan jitter are still
+    drawn, in the reference's tile order, so each rendered tile sees the numbers it would see in
+    a single-process render."""
     direct, with_alpha = fused[:2]
     w_isect = fused[2] if len(fused) > 2 else False  # pathtrace's w_isect (main.py _fused)
     N = len(cameras)
     per_tile = N * chunk * chunk
     dev = out.device
     step = max(1, MAX_BATCH_RAYS // per_tile)
-    for t0 in range(0, len(tiles), step):
-        batch = tiles[t0:t0 + step]
+    primary = bool(direct.training)
+    mine = [k for k in range(len(tiles)) if keep is None or keep(k)]
+    # the scan jitter of every tile (sdfs.py:236) in tile order: python's RNG, independent of the
+    # camera's torch draws, so drawing them up front leaves both sequences as the per-tile loop
+    scan = [random.random() for _ in tiles] if primary else None
+    pos = 0  # next tile whose camera jitter is to be drawn
+    for t0 in range(0, len(mine), step):
+        batch = mine[t0:t0 + step]
         rays = torch.empty(len(batch), per_tile, 6, device=dev)
-        for k, (x0, y0) in enumerate(batch):
+        for k, ti in enumerate(batch):
+            while pos < ti:  # tiles of other ranks: draw their jitter, render nothing
+                _draw_tile_noise(cameras, tiles[pos], chunk, size, with_noise)
+                pos += 1
+            x0, y0 = tiles[ti]
             rays[k] = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise).reshape(-1, 6)
+            pos = ti + 1
         b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights,
-                           scan_groups=len(batch) if len(batch) > 1 else None, w_isect=w_isect)
-        for k, (x0, y0) in enumerate(batch):
-            sl = slice(k * per_tile, (k + 1) * per_tile)
-            _lib.call("nrt_composite", _lib.ptr(b.rgb[sl]), _lib.ptr(b.thr[sl]), _lib.ptr(b.hit[sl]),
-                      N, chunk, chunk, int(with_alpha), int(not with_alpha), float(background),
-                      _lib.ptr(out), out.shape[1], out.shape[2], out.shape[3], int(x0 - ox),
-                      int(y0 - oy), _lib.stream())
+                           scan_groups=len(batch) if len(batch) > 1 else None, w_isect=w_isect,
+                           scan_draws=[scan[ti] for ti in batch] if primary else None)
+        for k, ti in enumerate(batch):
+            x0, y0 = tiles[ti]
+            composite_slice(b, slice(k * per_tile, (k + 1) * per_tile), N, chunk, with_alpha,
+                            background, out, x0 - ox, y0 - oy)
+    while pos < len(tiles):  # the jitter of the trailing tiles of other ranks
+        _draw_tile_noise(cameras, tiles[pos], chunk, size, with_noise)
+        pos += 1
+
+
+def composite_slice(b, sl, N, chunk, with_alpha, background, out, X0, Y0):
+    """composite() of the rays sl of a batched buffer set (one chunk x chunk tile)."""
+    _lib.call("nrt_composite", _lib.ptr(b.rgb[sl]), _lib.ptr(b.thr[sl]), _lib.ptr(b.hit[sl]),
+              N, chunk, chunk, int(with_alpha), int(not with_alpha), float(background),
+              _lib.ptr(out), out.shape[1], out.shape[2], out.shape[3], int(X0), int(Y0),
+              _lib.stream())
+
+
+def _draw_tile_noise(cameras, tile, chunk, size, with_noise):
+    """Consume the camera-jitter draw of a tile this rank does not render (cameras.rays_tile's
+    torch.rand, cameras.py:45-48 in the reference): the same RNG state afterwards as a render of
+    that tile."""
+    if with_noise:
+        draw = getattr(cameras, "tile_noise", None)
+        if draw is not None:
+            draw(chunk, chunk)
+        else:
+            cameras.rays_tile(tile[0], tile[1], chunk, chunk, size, with_noise)
+
+
+def shard_of(cameras, size, width, chunk, background, group=None, shard=None):
+    """(rank, world) when pathtrace should render a row-tile shard (images shard by
+    pixel-row tiles, one all-gather at frame end), else None.  shard: None = automatic (a
+    process group of more than one rank, and every rank asks for the same frame -- checked with
+    one small all-gather of the cameras' corner rays and the frame parameters, so ranks that
+    render different views each keep rendering their own full frame), False = never, True =
+    always (an error if the ranks' frames differ)."""
+    if shard is False:
+        return None
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return None
+    if not (dist.is_available() and dist.is_initialized()):
+        if shard:
+            raise _lib.NrtError("pathtrace(shard=True) needs an initialised torch.distributed "
+                                "process group")
+        return None
+    world = dist.get_world_size(group)
+    if (world <= 1 and not shard) or width % chunk:
+        return None  # (shard=True at one rank runs the sharded path: the RCCL test's case)
+    rank = dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    # a fixed-length fingerprint (the collective needs equal shapes on every rank): the frame
+    # parameters and three moments of the cameras' corner rays
+    corners = torch.cat([cameras.rays_tile(x, y, 1, 1, size, False).reshape(-1).double().cpu()
+                         for x, y in ((0, 0), (width - 1, size - 1))])
+    w = torch.arange(1, corners.numel() + 1, dtype=torch.float64)
+    key = torch.tensor([float(len(cameras)), float(size), float(width), float(chunk),
+                        float(background), float(corners.sum()), float((corners * w).sum()),
+                        float((corners * corners).sum())], dtype=torch.float64).to(dev)
+    keys = [torch.empty_like(key) for _ in range(world)]
+    dist.all_gather(keys, key, group=group)
+    same = all(torch.equal(k, keys[0]) for k in keys)
+    if not same:
+        if shard:
+            raise _lib.NrtError("pathtrace(shard=True): the ranks asked for different frames")
+        return None
+    return rank, world
+
+
+def gather_tile_rows(out, chunk, rank, world, group=None):
+    """After each rank rendered its row-tile shard into `out` [N, width, height, C] (the rows of
+    tile band j when j % world == rank), every rank's rows into every rank's `out` by one
+    all-gather (RowGather)."""
+    rows = row_shard(out.shape[1], rank, world, chunk)
+    idx = torch.tensor(rows, dtype=torch.long, device=out.device)
+    local = out.index_select(1, idx)
+    return gather_rows(local, out.shape[1], rank, world, chunk, out=out, group=group)
 
 
 def row_shard(size, rank, world, tile_rows=16):

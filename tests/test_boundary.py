@@ -288,3 +288,114 @@ def test_runtime_options_roundtrip():
     src = open(os.path.join(os.path.dirname(_lib.HERE), "include", "nrt.h")).read()
     for n in names:
         assert f'"{n}"' in src
+
+
+class _StubCameras:
+    """A camera batch for the sharding tests: rays_tile gives [N, W, H, 1, 6] rays whose
+    components encode (view, row, column) plus the torch.rand jitter the NeRF camera draws
+    (cameras.py:45-48), so a frame shows whether each tile saw its single-process draws."""
+
+    def __init__(self, n=2):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def rays_tile(self, x0, y0, W, H, size, with_noise=False, positions=None):
+        v = torch.arange(self.n).view(-1, 1, 1).float().expand(self.n, W, H)
+        r = (x0 + torch.arange(W)).view(1, -1, 1).float().expand(self.n, W, H)
+        c = (y0 + torch.arange(H)).view(1, 1, -1).float().expand(self.n, W, H)
+        jit = torch.rand(2, W, H) if with_noise else torch.zeros(2, W, H)
+        rays = torch.stack([v, r, c, jit[0].expand(self.n, W, H), jit[1].expand(self.n, W, H),
+                            torch.zeros(self.n, W, H)], dim=-1)
+        return rays.reshape(self.n, W, H, 1, 6)
+
+
+def _stub_fused_path(monkeypatch, rendered):
+    """Replace the HIP launches of pathtrace's fused tile path (render.direct_kernels and the
+    tile composite) by torch stand-ins: a ray's colour is (view + 1000 scan jitter, row + u,
+    column + v) -- what the real kernels would make of these rays is beside the point; the
+    test checks which tiles each rank renders and that every tile sees its own draws."""
+    import types
+    from neural_raytracing_amd.pathtracer import main, render
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+
+    def direct_kernels(direct, shapes, rays_flat, bsdf, lights, scan_groups=None, w_isect=False,
+                       scan_draws=None):
+        G = scan_groups or 1
+        per = rays_flat.shape[0] // G
+        scan = torch.tensor(scan_draws).repeat_interleave(per).view(-1, 1)
+        rgb = rays_flat[:, :3] + rays_flat[:, 3:6] * torch.tensor([0.0, 1.0, 1.0]) + \
+            1000 * scan * torch.tensor([1.0, 0.0, 0.0])
+        rendered.extend(sorted(set(rays_flat[:, 1].long().tolist())))
+        return types.SimpleNamespace(rgb=rgb)
+
+    def composite_slice(b, sl, N, chunk, with_alpha, background, out, X0, Y0):
+        out[:, X0:X0 + chunk, Y0:Y0 + chunk, :3] = b.rgb[sl].view(N, chunk, chunk, 3)
+
+    monkeypatch.setattr(render, "direct_kernels", direct_kernels)
+    monkeypatch.setattr(render, "composite_slice", composite_slice)
+    monkeypatch.setattr(main, "is_hip_sdf", lambda sdf: True)
+    shapes = types.SimpleNamespace(sdf=object(), dist=2.2)
+    direct = Direct()
+    direct.training = True  # primary rays: every tile draws its scan jitter
+    return main, shapes, direct
+
+
+def _pathtrace_frame(main, shapes, direct, seed, views=2, **kw):
+    import random
+    torch.manual_seed(seed)
+    random.seed(seed)
+    out, _ = main.pathtrace(shapes, None, _StubCameras(views), direct, bsdf=None, size=48,
+                            chunk_size=8, bundle_size=1, background=0.25, silent=True,
+                            device="cpu", with_noise=1e-3, **kw)
+    return out, random.random(), torch.rand(1)  # the RNG states after the frame
+
+
+def _pathtrace_shard_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from _pytest.monkeypatch import MonkeyPatch
+    mpatch = MonkeyPatch()
+    rendered = []
+    main, shapes, direct = _stub_fused_path(mpatch, rendered)
+    want = _pathtrace_frame(main, shapes, direct, 5, shard=False)  # before any process group
+    n_single = len(rendered)
+    rendered.clear()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    got = _pathtrace_frame(main, shapes, direct, 5)  # automatic: sharded
+    from neural_raytracing_amd.pathtracer.render import row_shard
+    mine = sorted(set(rendered))
+    # ranks asking for different frames (here: different camera counts) each render their own
+    rendered.clear()
+    own = _pathtrace_frame(main, shapes, direct, 6, views=2 + rank)
+    n_own = len(set(rendered))
+    q.put((rank, (bool(torch.equal(got[0], want[0])), got[1] == want[1],
+                  bool(torch.equal(got[2], want[2])), mine == row_shard(48, rank, world, 8),
+                  n_single, n_own, tuple(own[0].shape))))
+    dist.destroy_process_group()
+    mpatch.undo()
+
+
+def test_pathtrace_row_tile_shard_gloo_world2():
+    """pathtrace under a 2-rank process group (gloo): each rank renders the rows of its tile
+    bands only (render.row_shard with chunk_size rows), the all-gather assembles the frame, and
+    the frame and both RNG states afterwards equal the single-process render's (main.py:54-90,
+    the parallelism TODO at :60)."""
+    res = _spawn(_pathtrace_shard_worker, 2)
+    for rank in (0, 1):
+        frame_eq, py_rng_eq, torch_rng_eq, rows_ok, n_single, n_own, shape = res[rank]
+        assert frame_eq and py_rng_eq and torch_rng_eq and rows_ok, res
+        assert n_single == 48  # unsharded: every row
+        assert n_own == 48 and shape == (2 + rank, 48, 48, 3)  # different frames: not sharded
+
+
+def test_pathtrace_shard_off_without_process_group(monkeypatch):
+    """No process group: the whole frame, and shard=True is an error."""
+    from neural_raytracing_amd import NrtError
+    rendered = []
+    main, shapes, direct = _stub_fused_path(monkeypatch, rendered)
+    out, _, _ = _pathtrace_frame(main, shapes, direct, 3)
+    assert sorted(set(rendered)) == list(range(48)) and out.shape == (2, 48, 48, 3)
+    with pytest.raises(NrtError):
+        _pathtrace_frame(main, shapes, direct, 3, shard=True)

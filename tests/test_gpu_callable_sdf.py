@@ -258,15 +258,84 @@ def test_callable_training_gradients_match_oracle():
     assert max(rel) < 1e-4, rel
 
 
-def test_callable_training_through_an_mlp_raises():
-    """Under training, the normals of a callable that wraps a HIP SkipConnMLP would need the MLP's
-    second derivative through autograd: NrtError rather than a gradient missing its eikonal term."""
-    from neural_raytracing_amd import _lib
+def _oracle_callable_grads(ref, kind, p, w, dtype):
+    """Oracle autograd of <w, f(p)> + eikonal(autograd normal of f at p) for the callable f
+    around a copy of the oracle blob in ``dtype``; every parameter's gradient."""
+    import copy
+    m = copy.deepcopy(ref).to(dtype)
+    for sub in m.modules():
+        if hasattr(sub, "basis_p"):
+            sub.basis_p = sub.basis_p.to(dtype)
+    f = bend(m) if kind == "bend" else disp(m)
+    q = p.detach().clone().to(dtype).requires_grad_(True)
+    out = f(q).reshape(-1)
+    (n,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+    loss = (out * w.to(dtype)).sum() + ((n.norm(dim=-1) - 1) ** 2).mean()
+    loss.backward()
+    return {k: v.grad.detach().double() for k, v in m.named_parameters()}
+
+
+@pytest.mark.parametrize("kind", ["bend", "disp"])
+def test_callable_training_through_a_hip_mlp(kind):
+    """Training through an SDF callable that wraps a trainable HIP SkipConnMLP (edit_dtu.py:86-100
+    around a SphereSDF with its 8x128 shift): SDF.autograd_diff's create_graph normal (sdfs.py:
+    184-197) differentiates the MLP's input gradient through _MlpFn's create_graph backward
+    (input_gradient: nrt_mlp_backward + nrt_mlp_grad_backward).  A loss of the callable's
+    values and the eikonal term of its normals at fixed points near the surface; every
+    parameter's gradient against float64 oracle autograd: max|HIP - f64| <= max(2e-3 max|f64|,
+    4 max|oracle f32 - f64|)."""
+    ref, mine = _blob(128, 128, 32, "softplus")
+    g = torch.Generator().manual_seed(4)
+    d = torch.nn.functional.normalize(torch.randn(600, 3, generator=g), dim=-1)
+    p = d * (0.3 + 0.1 * torch.rand(600, 1, generator=g))
+    w = torch.randn(600, generator=g) * 0.1
+    f = bend(mine) if kind == "bend" else disp(mine)
+    q = p.cuda().requires_grad_(True)
+    out = f(q).reshape(-1)
+    (n,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+    loss = (out * w.cuda()).sum() + ((n.norm(dim=-1) - 1) ** 2).mean()
+    names = dict(mine.named_parameters())
+    grads = torch.autograd.grad(loss, list(names.values()), allow_unused=True)
+    got = {k: (torch.zeros_like(v) if gr is None else gr).detach().cpu().double()
+           for (k, v), gr in zip(names.items(), grads)}
+    want = _oracle_callable_grads(ref, kind, p, w, torch.float64)
+    w32 = _oracle_callable_grads(ref, kind, p, w, torch.float32)
+    # product names (init / layers / out of shift, centers / radii / tfs) equal the oracle's
+    worst = 0.0
+    for k, g64 in want.items():
+        err = (got[k] - g64).abs().max().item()
+        e32 = (w32[k] - g64).abs().max().item()
+        tol = max(2e-3 * g64.abs().max().item(), 4 * e32, 1e-9)
+        worst = max(worst, err / tol)
+        assert err <= tol, f"{k}: {err:.3g} > {tol:.3g}"
+    report(f"callable_hip_mlp_training[{kind}]", params=len(want), worst_err_over_tol=worst)
+    # the eikonal term reaches the shift MLP's weights through the double backward
+    assert want["shift.layers.3.weight"].abs().max() > 0
+
+
+def test_callable_training_step_through_a_hip_mlp():
+    """One optimiser step of SDF.intersect's training outputs (throughput = -1000 sdf(best_pos)
+    and the create_graph normals) through disp(HIP SphereSDF): finite, nonzero gradients for the
+    shift MLP and the spheres, and the loss moves."""
     from neural_raytracing_amd.pathtracer.shapes import SDF
-    _, f_mine = _pair("bend")
-    rays = _rays(16, 6, eye=(0.0, 0.2, 1.1)).cuda()
-    with pytest.raises(_lib.NrtError):
-        SDF(sdf=f_mine, max_steps=32).intersect(rays)
+    _, mine = _blob(128, 128, 32, "softplus")
+    f = disp(mine)
+    rays = _rays(24, 5, eye=(0.0, 0.2, 1.1)).cuda()
+    opt = torch.optim.Adam(mine.parameters(), lr=1e-3)
+    losses = []
+    for _ in range(2):
+        random.seed(3)
+        opt.zero_grad()
+        it, hit = SDF(sdf=f, max_steps=48).intersect(rays)
+        loss = torch.nn.functional.softplus(-it.throughput.reshape(-1) / 1000.0).mean() + \
+            ((it.raw_normals.norm(dim=-1) - 1) ** 2).mean()
+        loss.backward()
+        losses.append(float(loss))
+        gs = [q.grad for q in mine.shift.parameters()]
+        assert all(g is not None and torch.isfinite(g).all() for g in gs)
+        assert any(float(g.abs().max()) > 0 for g in gs)
+        opt.step()
+    assert losses[0] != losses[1] and all(math.isfinite(x) for x in losses)
 
 
 def test_callable_over_frozen_mlp_with_grad_mode_on():

@@ -102,7 +102,9 @@ def test_bare_mlp_sdf_march_matches_oracle(prec):
            thr_maxabs=thr.max().item(), thr_over_0p1=int((thr > 0.1).sum()))
     assert 0.15 < rhit.float().mean() < 0.85
     if prec != "fp16":  # fp32, and mixed (FP16 march refined where FP16 cannot decide): FP32 bar
-        assert flips + int(step.sum()) <= 0.005 * hit.numel()
+        # measured (round 4, 1,600 rays): 0 hit / 0 step flips at fp32 and mixed; 2 allowed (a
+        # ray whose SDF value sits within rounding of eps at some step, sdfs.py:122)
+        assert flips + int(step.sum()) <= 2
         assert t_err <= 1e-4 and p_err <= 1e-4 and n_err <= 1e-4
         # throughput = -1000 sdf(best): 1e-4 abs on sdf is 0.1 here
         assert (thr <= 0.1).float().mean() >= 0.995
@@ -129,7 +131,8 @@ def test_bare_mlp_sdf_scan_free_matches_oracle():
     m = (hit & rhit) & ~step
     report("bare_mlp_sdf_scan_free[fp32]", rays=hit.numel(), flips=int((hit != rhit).sum()),
            step_flips=int(step.sum()))
-    assert int((hit != rhit).sum()) + int(step.sum()) <= 0.005 * hit.numel()
+    # measured (round 4): 0 hit / 0 step flips of 1,024 rays; 2 allowed
+    assert int((hit != rhit).sum()) + int(step.sum()) <= 2
     assert (t[m] - rt[m]).abs().max().item() <= 1e-4
 
 
@@ -193,7 +196,8 @@ def test_metric_config_crop_matches_oracle(prec):
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.95
     if prec != "fp16":  # fp32 and mixed: the FP32 bar
-        assert int((~agree).sum()) <= 0.005 * crop * crop
+        # measured (round 4, 64^2 crop): 0 hit / 0 step flips at fp32 and mixed; 2 allowed
+        assert int((~agree).sum()) <= 2
         assert err[agree].max().item() <= 1e-4
     else:  # measured: 90.5 dB, 4.3e-5 max on agreeing pixels, 60 step flips
         assert psnr > 75, psnr
@@ -263,7 +267,8 @@ def test_dtu_like_render_matches_oracle(prec):
            pixels_over_1e4=int((err > 1e-4).sum()), psnr=psnr)
     assert 0.1 < rh.float().mean() < 0.9, rh.float().mean()
     if prec != "fp16":  # fp32, fp32-split and mixed: the FP32 bar
-        assert int((~agree).sum()) <= 0.005 * crop * crop
+        # measured (round 4, 48^2 crop): 0 hit / 0 step flips at every FP32-bar precision
+        assert int((~agree).sum()) <= 2
         assert err[agree].max().item() <= 1e-4
     else:  # measured: 50.9 dB (2 hit flips), 1.0e-4 max on agreeing pixels
         assert psnr > 45, psnr

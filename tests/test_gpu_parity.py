@@ -14,6 +14,10 @@ from tests.report import report
 
 pytestmark = pytest.mark.gpu
 
+# FP16 render bars (PSNR against the oracle, dB): the measured level minus about 5 dB
+PSNR_FP16_RENDER = 40.0
+PSNR_FP16_PROGRAM = 40.0
+
 MLP_CASES = [
     # name, ctor kwargs, activation, init
     ("sdf_8x256_softplus", dict(num_layers=8, hidden_size=256, out=1, freqs=16), "softplus", None),
@@ -230,7 +234,9 @@ def test_render_fp16_psnr():
                                      background=0, with_noise=0.0, device="cuda")
     mse = ((got.cpu().clamp(0, 1) - want.clamp(0, 1)) ** 2).mean()
     psnr = -10 * math.log10(max(mse.item(), 1e-12))
-    assert psnr > 40, psnr
+    report("render_fp16_psnr", pixels=64 * 64, psnr=psnr,
+           maxabs=float((got.cpu() - want).abs().max()))
+    assert psnr > PSNR_FP16_RENDER, psnr
 
 
 def test_nerf_raygen_matches_oracle():
@@ -434,7 +440,9 @@ def test_program_shading_nerf_synthetic_scene(monkeypatch):
     assert hit is None or (prog[..., :3].abs().sum() > 0)
     mse = ((prog.clamp(0, 1) - want.clamp(0, 1)) ** 2).mean().item()
     psnr = -10 * math.log10(max(mse, 1e-12))
-    assert psnr > 40, psnr
+    report("program_shading_fp16_psnr", pixels=crop * crop, psnr=psnr,
+           program_vs_per_component=float((prog - regs).abs().max()))
+    assert psnr > PSNR_FP16_PROGRAM, psnr
 
 
 def _ring_blob(hidden, freqs, seed, zero_out=False):
@@ -762,12 +770,13 @@ def test_colocate_fov_render_matches_oracle(prec):
     report(f"colocate_fov_render[{prec}]", pixels=err.numel(), hits=int(rh.sum()), flips=flips,
            step_flips=steps, over_1e4=int((err > 1e-4).sum()),
            over_1e4_on_agreeing=int((err[agree] > 1e-4).sum()), maxabs=err.max().item())
-    assert int((~agree).sum()) <= 0.005 * err.numel()
+    # measured (round 4, 64^2): 0 hit / 0 step flips at every precision; 2 allowed
+    assert int((~agree).sum()) <= 2
     if prec != "fp16":  # fp32, fp32-split, mixed: the FP32 bar on every ray whose march agrees
         assert int((err[agree] > 1e-4).sum()) == 0, err[agree].max()
-    else:  # measured 4.9e-4 max (FP16 SDF / shading MLP error), 299 of 4096 pixels > 1e-4
+    else:  # measured 4.9e-4 max (FP16 SDF / shading MLP error), 298 of 4096 pixels (7.3 %) > 1e-4
         assert err[agree].max().item() <= 2e-3, err[agree].max()
-        assert int((err > 1e-4).sum()) <= 0.15 * err.numel()
+        assert int((err > 1e-4).sum()) <= 0.09 * err.numel()
 
 
 def _nerfle_pair(seed=19, envmap=False):

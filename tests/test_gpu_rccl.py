@@ -94,3 +94,35 @@ def test_rccl_row_gather_of_uneven_shards(nccl_group):
     rows = row_shard(size, 0, 1, tile)
     got = gather_rows(full[:, rows].contiguous(), size, 0, 1, tile)
     assert torch.equal(got, full)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [32, 64])
+def test_rccl_pathtrace_sharded_equals_unsharded(nccl_group, chunk):
+    """pathtrace through its row-tile shard path (shard=True: the frame fingerprint all-gather,
+    the tile-band deal, every tile's jitter drawn in order, the RowGather all-gather of the
+    bands) on the nccl group is bit-equal to the unsharded call (shard=False) with the same seeds
+    -- test_nerf's call (training_utils.py:323-329, size 128 here)."""
+    import bench
+    from neural_raytracing_amd import set_precision
+    dev = nccl_group
+    set_precision("fp32")
+    size = 128
+    scene = bench.build_scene(dev, 24, light_gain=bench.LIGHT_GAIN)
+    pt = scene["pt"]
+    focal = float(0.5 * size / torch.tan(torch.tensor(0.5 * 0.6911)).item())
+    cameras = pt.cameras.NeRFCamera(cam_to_world=bench.view_c2w(0, 1)[None].to(dev), focal=focal,
+                                    device=dev)
+    outs = []
+    for shard in (False, True):
+        torch.manual_seed(3)
+        random.seed(3)
+        with torch.no_grad():
+            img, _ = pt.pathtrace(scene["shape"], scene["lights"], cameras, scene["integrator"],
+                                  bsdf=scene["bsdf"], size=size, chunk_size=chunk, bundle_size=1,
+                                  background=0, silent=True, device=dev, shard=shard)
+        outs.append((img.clone(), random.random(), torch.rand(1, device=dev).item()))
+    torch.cuda.synchronize()
+    (a, ra, ta), (b, rb, tb) = outs
+    assert torch.equal(a, b) and ra == rb and ta == tb
+    assert float((a[..., 3] > 0.5).float().mean()) > 0.05

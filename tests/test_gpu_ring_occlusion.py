@@ -144,3 +144,35 @@ def test_fused_shadowed_tiles_match_integrator_path(prec, mode):
     report(f"fused_shadowed_tiles[{prec},{mode}]", pixels=fused[..., 0].numel(), maxabs=err)
     assert fused.shape == plain.shape
     assert err <= 1e-6, err
+
+
+@pytest.mark.gpu
+def test_pathtrace_trainable_occlusion_mlp_keeps_its_gradients():
+    """pathtrace under autograd with a trainable learned-occlusion MLP (w_isect = SkipConnMLP,
+    scene.py:313-318) must not take the gradient-free fused tile path: the occlusion weights get
+    the gradients of the per-tile integrator path (forced by an `addition` hook)."""
+    import random
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.integrators import Direct
+    from tests.test_gpu_parity import _occ_pair, _shadow_scene
+    _, mine = _shadow_scene()
+    for key in ("shape", "bsdf", "lights"):  # only the occlusion MLP trains
+        for q in getattr(mine[key], "parameters", lambda: [])():
+            q.requires_grad_(False)
+    occ = _occ_pair(1)[1]
+    for q in occ.parameters():
+        q.requires_grad_(True)
+    grads = []
+    for hook in (None, lambda it: None):
+        random.seed(21)
+        kw = {} if hook is None else {"addition": hook}
+        occ.zero_grad()
+        img, _ = pt.pathtrace(mine["shape"], mine["lights"], mine["camera"], Direct(),
+                              bsdf=mine["bsdf"], size=32, chunk_size=32, bundle_size=1,
+                              background=0.5, with_noise=0.0, w_isect=occ, **kw)
+        img.sum().backward()
+        grads.append([q.grad.detach().clone() for q in occ.parameters()])
+    for a, b in zip(*grads):
+        assert a is not None and torch.isfinite(a).all()
+        assert torch.equal(a, b)
+    assert any(float(g.abs().max()) > 0 for g in grads[0])

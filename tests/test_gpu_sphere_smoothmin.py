@@ -29,7 +29,7 @@ def _params(n, seed, dtype=torch.float32):
     return c, r, t
 
 
-@pytest.mark.parametrize("P", [1, 77, 5000])
+@pytest.mark.parametrize("P", [1, 77, 5000, 20000])  # 20,000: five point slices in the backward
 @pytest.mark.parametrize("n", [1, 64, 128])
 def test_smoothmin_matches_float64_autograd(P, n):
     from neural_raytracing_amd.pathtracer.differentiable import _SphereSmoothMinFn
@@ -102,3 +102,27 @@ def test_smoothmin_deterministic_and_empty():
     assert v.numel() == 0 and gr.shape == (0, 3)
     (v.sum() + gr.sum()).backward()
     assert float(cm.grad.abs().max()) == 0.0 and float(tm.grad.abs().max()) == 0.0
+
+
+def test_smoothmin_beyond_the_lds_table_trains_on_torch():
+    """a SphereSDF with more spheres than the fused kernels' 64 KB LDS table (1,260)
+    trains on the torch restatement instead of raising; its gradients equal the restatement's."""
+    from neural_raytracing_amd.pathtracer.differentiable import (SMOOTHMIN_MAX_SPHERES,
+                                                                 sdf_gradient, sphere_part)
+    from neural_raytracing_amd.pathtracer.shapes import SphereSDF
+    n = SMOOTHMIN_MAX_SPHERES + 40
+    sdf = SphereSDF(n=n, device="cpu")
+    with torch.no_grad():
+        sdf.radii.add_(0.1)
+    sdf = sdf.cuda()
+    p = 0.3 * torch.rand(50, 3, device="cuda")
+    g = sdf_gradient(sdf, p)
+    g.square().sum().backward()
+    got = sdf.radii.grad.clone()
+    sdf.zero_grad()
+    q = p.clone().requires_grad_(True)
+    out = sphere_part(sdf, q)
+    (gs,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=True)
+    from neural_raytracing_amd.pathtracer.neural_blocks import input_gradient
+    (gs + input_gradient(sdf.shift, p)).square().sum().backward()
+    assert torch.allclose(got, sdf.radii.grad, rtol=1e-5, atol=1e-7)
