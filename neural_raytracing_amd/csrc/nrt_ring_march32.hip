@@ -3,6 +3,11 @@
 // FP16 ring march (nrt_ring_march.hip), 16-ray tiles, torch-exact transcendentals.
 #include "nrt_launch.h"
 
+// waves per block of the 128-wide SDFs' FP32 ring march (timing experiments: -DNRT_R32_SMALL_WV)
+#ifndef NRT_R32_SMALL_WV
+#define NRT_R32_SMALL_WV 8
+#endif
+
 namespace nrt {
 
 // which = 0: march + scan (k_march32, then k_scan_best32 when primary); 1: k_scan_best32 alone
@@ -19,7 +24,7 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
   const bool scan = ma.primary != 0;
   if (scan && which == 0) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   auto run = [&]<int KH, int KE, int ACT>() -> int {
-    constexpr int WV = kRing32Waves;
+    constexpr int WV = KH <= 32 ? NRT_R32_SMALL_WV : kRing32Waves;
     auto launch = [&](auto kern, const char* name) -> int {
       const size_t lds = ring32::Engine<KH, KE, WV>::RING_BYTES + extra;
       if (int rc = set_lds(kern, lds)) return rc;

@@ -200,7 +200,7 @@ def test_metric_config_crop_matches_oracle(prec):
         assert int((~agree).sum()) <= 2
         assert err[agree].max().item() <= 1e-4
     else:  # measured: 90.5 dB, 4.3e-5 max on agreeing pixels, 60 step flips
-        assert psnr > 75, psnr
+        assert psnr > 85, psnr
         assert err[agree].max().item() <= 2e-4
 
 
@@ -271,7 +271,7 @@ def test_dtu_like_render_matches_oracle(prec):
         assert int((~agree).sum()) <= 2
         assert err[agree].max().item() <= 1e-4
     else:  # measured: 50.9 dB (2 hit flips), 1.0e-4 max on agreeing pixels
-        assert psnr > 45, psnr
+        assert psnr > 46, psnr
         assert err[agree].max().item() <= 5e-4
 
 

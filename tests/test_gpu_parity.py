@@ -15,8 +15,9 @@ from tests.report import report
 pytestmark = pytest.mark.gpu
 
 # FP16 render bars (PSNR against the oracle, dB): the measured level minus about 5 dB
-PSNR_FP16_RENDER = 40.0
-PSNR_FP16_PROGRAM = 40.0
+# (round 5: render 106.2 dB, program shading 98.5 dB)
+PSNR_FP16_RENDER = 101.0
+PSNR_FP16_PROGRAM = 93.0
 
 MLP_CASES = [
     # name, ctor kwargs, activation, init
