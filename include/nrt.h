@@ -503,6 +503,12 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      tiles where that doubles the blocks per CU), 2 = the same with the encoding
  *                      in the LDS slab unless fewer than two blocks fit, 0 = one wave per 32 rows
  *                      (round 3).  Gradients bit-equal across values.
+ *   "bwd_ring"       1  nrt_mlp_backward(_multi) of the shading MLPs' shapes (LightField 10x256
+ *                      F=16, spatial weights 16x256 F=128, NeuralBSDF 6x96 F=64: leaky_relu, 3
+ *                      inputs, no latent) on the FP32 ring engine (16-row tiles, the weights and
+ *                      the transposed weights streamed through a block-shared LDS ring, dZ kept in
+ *                      registers between layers); 0: the bwd_colsplit kernels.  Same gradients to
+ *                      FP32 rounding (different summation order), both held to float64 autograd
  *   "mixed_drift"    0  1: the flag bound is d * (1 + a per-ray drift estimate built from the
  *                      ratio of consecutive step values) instead of d * (1 + step/16); measured
  *                      to flag more rays for the same accuracy (152 vs 133 ms), kept for A/B

@@ -1327,7 +1327,13 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves)), block(64 * lp.waves);
   int rc = NRT_OK;
-  {
+  // the shading MLPs' shapes: the ring backward (nrt_train_ring.h), its job table in the
+  // workspace's weight-gradient table region (the weight gradients copy theirs after it ran)
+  if (!latent && ring_backward_ok(&m, 1) && ring_backward_table_bytes(1) <= kWgradTableBytes) {
+    ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M);
+    if ((rc = ring_backward(&m, 1, x, M, &dy, &dx, &w.A, &w.dZ, &w.Eraw, &w.Eact, w.part, st)))
+      return rc;
+  } else {
     ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M);
     NRT_NB_SWITCH(d.nb, {
       if (cs) {
@@ -1430,7 +1436,15 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   const int waves = ceil_div64(M, 32);
   dim3 grid(ceil_div64(waves, lp.waves), n), block(64 * lp.waves);
   int rc = NRT_OK;
-  {
+  if (ring_backward_ok(mlps, n) && ring_backward_table_bytes(n) <= (size_t)n * kWgradTableBytes) {
+    // the ring backward (nrt_train_ring.h), blockIdx.y = MLP; its job table in the weight-gradient
+    // table region
+    std::vector<float*> A(n), dZ(n), Er(n), Ea(n);
+    for (int i = 0; i < n; ++i) { A[i] = ws[i].A; dZ[i] = ws[i].dZ; Er[i] = ws[i].Eraw; Ea[i] = ws[i].Eact; }
+    ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M * n);
+    if ((rc = ring_backward(mlps, n, x, M, dy, dx, A.data(), dZ.data(), Er.data(), Ea.data(), table, st)))
+      return rc;
+  } else {
     ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M * n);
     NRT_NB_SWITCH(d.nb, {
       if (cs) {

@@ -53,6 +53,10 @@ struct nrt_mlp {
   // nrt_mlp_refresh gathers its stream and bias table too once it exists
   mutable nrt_rprog solo32;
   bool solo_in_refresh = false;  // the refresh maps cover solo32
+  // [forward | transposed] FP32 row program of the ring backward (nrt_train_ring.h), built on
+  // first use; nrt_mlp_refresh gathers it too once it is in the maps
+  mutable nrt_rprog bwd32;
+  bool bwd_in_refresh = false;
   ~nrt_mlp();
 };
 

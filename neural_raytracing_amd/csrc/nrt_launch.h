@@ -34,6 +34,7 @@ enum Option {
   OPT_RING_OCCLUSION,  // "ring_occlusion"
   OPT_MIXED_ZONE,      // "mixed_zone" (1e-7 units)
   OPT_BWD_COLSPLIT,    // "bwd_colsplit"
+  OPT_BWD_RING,        // "bwd_ring"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -246,12 +247,24 @@ int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const f
                   const float* lscale, float* rgb, float* weights_out, hipStream_t st);
 
 // ---- FP32 / fp32-split shading on the row-program ring engines (nrt_shade_ring.hip) ----
-int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out);
+int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out, int mode = 0);
 int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st);
 bool solo_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
                        void*& stream_dst, void*& bias_dst);
 int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
                const float* wi, const int32_t* hit_idx, const int32_t* hit_count, int64_t P,
                const float* lscale, float* rgb, float* weights_out, int precision, hipStream_t st);
+// ---- the MLP backward on the ring engine (nrt_train_ring.h, launched from nrt_shade_ring.hip) --
+// the bytes of the device job table ring_backward needs for n MLPs
+size_t ring_backward_table_bytes(int n);
+// true when every MLP has a ring-backward shape (and, refreshed, a refreshed backward program)
+bool ring_backward_ok(const nrt_mlp* const* mlps, int n);
+// per MLP k: dy[k] [M][out], dx[k] [M][3] or null, A[k] / dZ[k] [L+1][M][H], Eraw[k] / Eact[k]
+// [M][dp]; table: ring_backward_table_bytes(n) bytes of device memory
+int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                  const float* const* dy, float* const* dx, float* const* A, float* const* dZ,
+                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st);
+bool bwd_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
+                      void*& stream_dst, void*& bias_dst);
 
 }  // namespace nrt

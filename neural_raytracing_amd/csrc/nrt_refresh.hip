@@ -112,8 +112,9 @@ struct Section {
 // The fragment layouts of nrt_pack.hip, as source indices into [W_0 .. W_{L+1} | b_0 .. b_{L+1}]
 // (row-major nn.Linear weights), -1 for padding.
 void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& secs,
-                int64_t& n_src, bool& solo) {
+                int64_t& n_src, bool& solo, bool& bwd) {
   solo = false;
+  bwd = false;
   const nrt_mlp_desc& d = m->desc;
   const MlpDev& md = m->host_dev;
   const int in = d.in_size, H = d.hidden, L = d.num_layers, O = d.out, F = d.freqs;
@@ -286,6 +287,20 @@ void build_maps(const nrt_mlp* m, std::vector<int>& map, std::vector<Section>& s
       solo = true;
     }
   }
+  // the ring backward's program (nrt_train_ring.h): the forward part and the transposed layers
+  {
+    std::vector<int> smap, bmap;
+    void *sdst = nullptr, *bdst = nullptr;
+    if (bwd_refresh_maps(m, smap, bmap, sdst, bdst)) {
+      begin(sdst, SEC_F32);
+      map.insert(map.end(), smap.begin(), smap.end());
+      end();
+      begin(bdst, SEC_F32);
+      map.insert(map.end(), bmap.begin(), bmap.end());
+      end();
+      bwd = true;
+    }
+  }
 }
 
 }  // namespace
@@ -300,9 +315,10 @@ extern "C" int nrt_mlp_refresh(nrt_mlp* m, const float* const* weights, const fl
   if (!m->gather_map) {
     std::vector<int> map;
     std::vector<Section> secs;
-    bool solo = false;
-    build_maps(m, map, secs, m->n_src, solo);
+    bool solo = false, bwd = false;
+    build_maps(m, map, secs, m->n_src, solo, bwd);
     m->solo_in_refresh = solo;
+    m->bwd_in_refresh = bwd;
     if (map.size() > (size_t)INT32_MAX) { set_error("nrt_mlp_refresh: MLP too large"); return NRT_EINVAL; }
     NRT_HIP(hipMalloc(&m->gather_map, map.size() * sizeof(int)));
     NRT_HIP(hipMemcpy(m->gather_map, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice));

@@ -8,6 +8,7 @@
 // else keeps the per-wave k_shade_direct.
 #include "nrt_launch.h"
 #include "nrt_shade_ring.h"
+#include "nrt_train_ring.h"
 
 namespace nrt {
 
@@ -57,7 +58,8 @@ struct Walker {
   void chunk_end() { chunks->back() = (int)pieces() - chunks->at(chunks->size() - 2); }
 };
 
-int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
+// with_out = false: the backward program's forward part (no out layer)
+int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale, bool with_out = true) {
   const nrt_mlp_desc& d = m->desc;
   const int H = d.hidden, L = d.num_layers, F = d.freqs, in = 3;
   const int dp = in + 2 * F;
@@ -175,16 +177,84 @@ int walk_mlp(const nrt_mlp* m, Walker& w, std::vector<float>& lscale) {
     for (int ib = 0; ib < NC; ++ib) hidden_chunk(1 + i, ib, 2);
     if (enc[1 + i]) enc_part(1 + i);
   }
-  hidden_chunk(L + 1, 0, 1);
+  if (with_out) hidden_chunk(L + 1, 0, 1);
+  return NRT_OK;
+}
+
+// The transposed layers of the ring backward (nrt_train_ring.h bwd32), FP32, in the order it
+// consumes them: T-out (one chunk [sb][lane][t]: lane (g, i) = W_out[4 g + t][16 sb + i], the
+// outputs padded to 16), then for l = L .. 1 the T-enc chunks of a skip layer and the T-hidden
+// chunks of layer l, then the init layer's T-enc chunks.  A T chunk is 32 output rows (inputs j of
+// layer l: hidden features, or encoding slots 32 c + 16 b + i) x the layer's H outputs in the
+// ring32 k order: quad u, sub-block b, lane (g, i), t -> W_l[16 u + 4 g + t][j].
+int walk_mlp_bwd(const nrt_mlp* m, Walker& w) {
+  const nrt_mlp_desc& d = m->desc;
+  const int H = d.hidden, L = d.num_layers, F = d.freqs, in = 3;
+  const int dp = in + 2 * F, NSB = H / 16, NC = H / 32, QH = H / 16;
+  const int CEN = (dp + 31) / 32;
+  const int nl = L + 2;
+  std::vector<int> R(nl), C(nl);
+  std::vector<char> hid(nl), enc(nl);
+  for (int l = 0; l < nl; ++l) {
+    const bool skip = l >= 1 && l <= L && (l - 1) != L - 1 && ((l - 1) % d.skip) == 0;
+    hid[l] = l >= 1;
+    enc[l] = l == 0 || skip;
+    R[l] = l == nl - 1 ? d.out : H;
+    C[l] = (hid[l] ? H : 0) + (enc[l] ? dp : 0);
+    if ((int64_t)m->host_w[l].size() != (int64_t)R[l] * C[l]) {
+      set_error("backward program: weight shape mismatch");
+      return NRT_EINVAL;
+    }
+  }
+  std::vector<int64_t> woff(nl + 1, 0);
+  for (int l = 0; l < nl; ++l) woff[l + 1] = woff[l] + (int64_t)R[l] * C[l];
+  auto slot_col = [&](int s) -> int {
+    if (s < 2 * F) return (s & 1) ? in + F + (s >> 1) : in + (s >> 1);
+    if (s < 2 * F + in) return s - 2 * F;
+    return -1;
+  };
+  auto put32 = [&](int l, int row, int col) {
+    const bool ok = row < R[l] && col >= 0 && col < C[l];
+    if (w.map) w.map->push_back(ok ? (int)(woff[l] + (int64_t)row * C[l] + col) : -1);
+    else w.s32->push_back(ok ? m->host_w[l][(size_t)row * C[l] + col] : 0.f);
+  };
+  // T-out
+  w.chunk_begin();
+  for (int sb = 0; sb < NSB; ++sb)
+    for (int lane = 0; lane < 64; ++lane)
+      for (int t = 0; t < 4; ++t) put32(L + 1, 4 * (lane >> 4) + t, 16 * sb + (lane & 15));
+  w.chunk_end();
+  // one T chunk of layer l: output rows j = col(32 c + 16 b + i)
+  auto t_chunk = [&](int l, int c, auto&& col) {
+    w.chunk_begin();
+    for (int u = 0; u < QH; ++u)
+      for (int b = 0; b < 2; ++b)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int t = 0; t < 4; ++t)
+            put32(l, 16 * u + 4 * (lane >> 4) + t, col(32 * c + 16 * b + (lane & 15)));
+    w.chunk_end();
+  };
+  auto t_enc = [&](int l) {
+    for (int c = 0; c < CEN; ++c)
+      t_chunk(l, c, [&](int s) { const int cc = slot_col(s); return cc < 0 ? -1 : (hid[l] ? H + cc : cc); });
+  };
+  for (int l = L; l >= 1; --l) {
+    if (enc[l]) t_enc(l);
+    for (int c = 0; c < NC; ++c) t_chunk(l, c, [](int j) { return j; });
+  }
+  t_enc(0);
   return NRT_OK;
 }
 
 }  // namespace
 
-int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out) {
+// mode 0: the MLPs' forward evaluation; mode 1 (one FP32 MLP): the ring backward's program,
+// the forward without the out layer, then the transposed layers (walk_mlp_bwd)
+int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out, int mode) {
   out.built = true;
   out.ok = false;
   if (mlps.empty() || (int)mlps.size() > kMaxProgMlp) return NRT_OK;
+  if (mode == 1 && (split || mlps.size() != 1)) return NRT_OK;
   RProgDev& d = out.d;
   std::memset(&d, 0, sizeof(d));
   std::vector<float> s32;
@@ -197,7 +267,9 @@ int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& 
     const nrt_mlp* m = mlps[k];
     const nrt_mlp_desc& md = m->desc;
     std::vector<float> lscale;
-    if (int rc = walk_mlp(m, w, lscale)) return rc;
+    if (int rc = walk_mlp(m, w, lscale, mode == 0)) return rc;
+    if (mode == 1)
+      if (int rc = walk_mlp_bwd(m, w)) return rc;
     RProgMlp& pm = d.mlp[k];
     pm.L = md.num_layers; pm.skip = md.skip; pm.F = md.freqs; pm.out = md.out;
     pm.bstride = md.hidden;  // >= 16 rows of the out layer's sub-block
@@ -400,6 +472,79 @@ bool solo_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vect
   stream_dst = const_cast<void*>(sp.d.stream);
   bias_dst = const_cast<float*>(sp.d.tables);  // biases first (scales follow, 1 in FP32)
   return true;
+}
+
+// the backward program's refresh maps (as solo_refresh_maps, for m->bwd32)
+bool bwd_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
+                      void*& stream_dst, void*& bias_dst) {
+  if (!solo_shape(m)) return false;
+  nrt_rprog& bp = m->bwd32;
+  if (!bp.built && build_rprog({m}, false, bp, 1) != NRT_OK) return false;
+  if (!bp.ok) return false;
+  std::vector<int> chunks;
+  std::vector<float> lscale;
+  Walker w{false, nullptr, nullptr, &chunks, &stream_map};
+  if (walk_mlp(m, w, lscale, false) != NRT_OK || walk_mlp_bwd(m, w) != NRT_OK) return false;
+  const nrt_mlp_desc& d = m->desc;
+  int64_t wtot = 0;
+  for (const auto& v : m->host_w) wtot += (int64_t)v.size();
+  int64_t boff = wtot;
+  for (int l = 0; l < d.num_layers + 2; ++l) {
+    const int rows = l == d.num_layers + 1 ? d.out : d.hidden;
+    for (int r = 0; r < d.hidden; ++r) bias_map.push_back(r < rows ? (int)(boff + r) : -1);
+    boff += rows;
+  }
+  if ((int64_t)stream_map.size() * 4 != bp.d.stream_bytes) return false;
+  stream_dst = const_cast<void*>(bp.d.stream);
+  bias_dst = const_cast<float*>(bp.d.tables);
+  return true;
+}
+
+size_t ring_backward_table_bytes(int n) { return (size_t)std::max(n, 1) * sizeof(rprog::BwdRingJob); }
+
+bool ring_backward_ok(const nrt_mlp* const* mlps, int n) {
+  if (option(OPT_BWD_RING) == 0 || n < 1) return false;
+  const int shape = solo_shape(mlps[0]);
+  if (!shape) return false;
+  for (int k = 0; k < n; ++k) {
+    const nrt_mlp* m = mlps[k];
+    if (solo_shape(m) != shape) return false;
+    if (m->refreshed && !m->bwd_in_refresh) return false;
+    if (!m->bwd32.built && build_rprog({m}, false, m->bwd32, 1) != NRT_OK) return false;
+    if (!m->bwd32.ok) return false;
+  }
+  return true;
+}
+
+int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                  const float* const* dy, float* const* dx, float* const* A, float* const* dZ,
+                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st) {
+  if (!ring_backward_ok(mlps, n)) return NRT_EUNSUPPORTED;
+  std::vector<rprog::BwdRingJob> jobs(n);
+  for (int k = 0; k < n; ++k)
+    jobs[k] = rprog::BwdRingJob{mlps[k]->bwd32.d, dy[k], dx ? dx[k] : nullptr, A[k], dZ[k],
+                                Eraw[k], Eact[k]};
+  NRT_HIP(hipMemcpyAsync(table, jobs.data(), (size_t)n * sizeof(rprog::BwdRingJob),
+                         hipMemcpyHostToDevice, st));
+  const auto* tj = (const rprog::BwdRingJob*)table;
+  constexpr int WV = kRWaves;
+  const int64_t want = ceil_div64(M, 16 * WV);
+  const RProgDev& d0 = mlps[0]->bwd32.d;  // the same shape: the same LDS plan for every MLP
+  auto run = [&](auto sh) -> int {
+    using S = decltype(sh);
+    return with_depth<0, WV>(d0, [&](auto dd) -> int {
+      constexpr int D = decltype(dd)::value;
+      auto kern = rprog::k_mlp_bwd_ring<D, WV, S>;
+      const size_t lds = rprog::Engine<D, WV>::lds_bytes(d0);
+      if (int r = set_lds(kern, lds)) return r;
+      kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want), n), dim3(64 * WV), lds, st>>>(tj, x, M);
+      return check_launch("k_mlp_bwd_ring");
+    });
+  };
+  const int shape = solo_shape(mlps[0]);
+  if (shape == 1) return run(rprog::LightShape{});
+  if (shape == 2) return run(rprog::SpatialShape{});
+  return run(rprog::BsdfShape{});
 }
 
 // NRT_EUNSUPPORTED when the MLP has no compiled ring shape (or a refreshed handle whose solo
