@@ -980,6 +980,7 @@ struct WgradJob {
   float* dW;
   int64_t M, slice_rows, part_off, out0;
   int R, C, ldi, ldw, c0, tiles_c, n_tiles, block0;
+  int bias;  // 1: db = the column sums of dZ (In unused)
 };
 
 template <int = 0>
@@ -1079,6 +1080,147 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
     }
 }
 
+// ---- LDS-staged weight gradients (default; NRT_WGRAD_V1 builds the kernel above) -----------
+// k_wgrad_batch fed each MFMA from 4-byte global loads in the MFMA's lane order (round-4 PMC:
+// 65-75 % of wave time waiting at ~0.5 MFMA busy) and, with 64 x 64 tiles, read a 256 x 256
+// layer's dZ and In slices four times each.  Here one block of 8 waves computes a whole 256 x 256
+// output tile over its slice of the batch -- a layer's operands are read once per slice (64 FLOP
+// per byte) -- and the rows stream through three LDS stages of 16 rows ([16][256 + 1] floats of
+// dZ and of In: coalesced 1 KiB row segments, loaded two stages ahead into registers so ~8k cycles
+// of MFMA cover each load).  Wave (wr, wc) takes rows 128 wr .., columns 64 wc .. of the tile as
+// 4 x 2 v_mfma_f32_32x32x2_f32 accumulators with operands read from LDS.  Exact f32, each output's
+// products in row order within the slice (deterministic).  A bias job (the product against a
+// column of ones) is a column sum of dZ on the VALU.
+constexpr int kWgT = 256;   // tile side
+constexpr int kWgKS = 16;   // rows per LDS stage
+constexpr int kWgNS = 3;    // stages
+constexpr int kWgLd = kWgT + 1;
+
+template <int = 0>
+__global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restrict__ jobs, int n_jobs,
+                                                       int S, float* __restrict__ part) {
+  typedef float f16v_ __attribute__((ext_vector_type(16)));
+  extern __shared__ float wsm[];  // [kWgNS][2][kWgKS][kWgLd]
+  int j = 0;
+  while (j + 1 < n_jobs && (int)blockIdx.x >= jobs[j + 1].block0) ++j;
+  const WgradJob& jb = jobs[j];
+  const int b = (int)blockIdx.x - jb.block0;
+  const int tile = b % jb.n_tiles, slice = b / jb.n_tiles;
+  const float* __restrict__ dZ = jb.dZ;
+  const float* __restrict__ In = jb.In;
+  const int R = jb.R, C = jb.C, ldi = jb.ldi;
+  const int64_t m0 = (int64_t)slice * jb.slice_rows;
+  const int64_t m1 = std::min<int64_t>(jb.M, m0 + jb.slice_rows);
+  const int t = threadIdx.x;
+  float* out = part + jb.part_off + (size_t)slice * R * C;
+  if (jb.bias) {  // bias: column sums over the slice, in row order
+    for (int r = t; r < R; r += 512) {
+      float acc = 0.f;
+      int64_t m = m0;
+      for (; m + 8 <= m1; m += 8) {  // eight loads in flight, added in row order
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = dZ[(m + k) * R + r];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc += v[k];
+      }
+      for (; m < m1; ++m) acc += dZ[m * R + r];
+      out[r] = acc;
+    }
+    return;
+  }
+  const int r0 = (tile / jb.tiles_c) * kWgT, c0 = (tile % jb.tiles_c) * kWgT;
+  const int w = t >> 6, lane = t & 63, i = lane & 31, h = lane >> 5;
+  const int wr = w >> 2, wc = w & 3;
+  // this wave's row blocks / column blocks that hold any output (the rest of its tile is padding)
+  const bool live = r0 + 128 * wr < R && c0 + 64 * wc < C;
+  // staging: thread t loads column (t & 255) of rows (t >> 8) + 2 k, k < 8, of both operands
+  const int lc = t & 255, lr = t >> 8;
+  const bool rok = r0 + lc < R, cok = c0 + lc < C;
+  // through global-address-space pointers: flat loads would also count in lgkmcnt, so every LDS
+  // read's wait would drain the staging loads in flight
+  using gptr = const __attribute__((address_space(1))) float*;
+  const gptr zcol = (gptr)(dZ + (rok ? r0 + lc : 0));
+  const gptr icol = (gptr)(In + (cok ? c0 + lc : 0));
+  auto sA = [&](int st, int row, int col) -> float& { return wsm[((st * 2) * kWgKS + row) * kWgLd + col]; };
+  auto sB = [&](int st, int row, int col) -> float& { return wsm[((st * 2 + 1) * kWgKS + row) * kWgLd + col]; };
+  float za[2][kWgKS / 2], ia[2][kWgKS / 2];
+  // raw loads (clamped rows); the masking waits for the stash, so no load is consumed early
+  auto load = [&](int q, int64_t ms) {
+#pragma unroll
+    for (int k = 0; k < kWgKS / 2; ++k) {
+      const int64_t m = ms + lr + 2 * k;
+      const int64_t mm = m < m1 ? m : m0;
+      za[q][k] = zcol[mm * R];
+      ia[q][k] = icol[mm * ldi];
+    }
+  };
+  auto stash = [&](int q, int st, int64_t ms) {
+#pragma unroll
+    for (int k = 0; k < kWgKS / 2; ++k) {
+      const bool ok = ms + lr + 2 * k < m1;
+      sA(st, lr + 2 * k, lc) = ok && rok ? za[q][k] : 0.f;
+      sB(st, lr + 2 * k, lc) = ok && cok ? ia[q][k] : 0.f;
+    }
+  };
+  f16v_ acc[4][2] = {};
+  const int64_t nst = (m1 - m0 + kWgKS - 1) / kWgKS;  // stages of the slice
+  // prologue: stage 0 into LDS, stage 1 into registers
+  if (nst > 0) { load(0, m0); stash(0, 0, m0); }
+  if (nst > 1) load(1, m0 + kWgKS);
+  __syncthreads();
+  // stage s: LDS slot s % kWgNS; register set Q = s & 1 (compile-time in each half of the loop
+  // body: a runtime index would put the sets in scratch memory)
+  auto body = [&](int64_t s, auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    const int st = (int)(s % kWgNS);
+    // stage s + 1 waits in set Q ^ 1; stage s + 2 goes into set Q (its stage s is in LDS since
+    // the last barrier)
+    // unconditional (rows past the slice load as zeros): a load under a branch makes the
+    // compiler's wait-count analysis drain every load at the stash below
+    load(Q, m0 + (s + 2) * kWgKS);
+    if (live) {
+#pragma unroll
+      for (int ks = 0; ks < kWgKS / 2; ++ks) {
+        const int row = 2 * ks + h;
+        float a[4], bv[2];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) a[x] = sA(st, row, 128 * wr + 32 * x + i);
+#pragma unroll
+        for (int y = 0; y < 2; ++y) bv[y] = sB(st, row, 64 * wc + 32 * y + i);
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], bv[y], acc[x][y], 0, 0, 0);
+      }
+    }
+    // stage s + 1 (registers) into its slot: the slot of stage s - 2, read two barriers ago
+    stash(Q ^ 1, (int)((s + 1) % kWgNS), m0 + (s + 1) * kWgKS);
+    __syncthreads();
+  };
+  for (int64_t s = 0; s < nst; s += 2) {
+    body(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nst) body(s + 1, std::integral_constant<int, 1>{});
+  }
+  if (!live) return;
+  // accumulator (x, y) register q: row 128 wr + 32 x + (q & 3) + 8 (q >> 2) + 4 h, column
+  // 64 wc + 32 y + i of the tile
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const int cc = c0 + 64 * wc + 32 * y + i;
+      if (cc >= C) continue;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int rr = r0 + 128 * wr + 32 * x + (q & 3) + 8 * (q >> 2) + 4 * h;
+        if (rr < R) out[(size_t)rr * C + cc] = acc[x][y][q];
+      }
+    }
+}
+constexpr size_t kWgLdsBytes = (size_t)kWgNS * 2 * kWgKS * kWgLd * sizeof(float);
+
 // element e of the concatenated outputs (job j owns [out0, out0 + R C)): the sum over slices in
 // slice order
 template <int = 0>
@@ -1104,7 +1246,11 @@ static_assert(kMaxWgradJobs * sizeof(WgradJob) <= kWgradTableBytes, "job table")
 // the slice count of a batch: about 3 blocks (12 waves, the kernel's occupancy) per CU over all
 // the batch's tiles, at least kSliceRows rows per slice
 int batch_slices(int64_t total_tiles, int64_t M) {
+#ifdef NRT_WGRAD_V1
   int64_t S = std::max<int64_t>(1, (256 * 3 + total_tiles - 1) / total_tiles);
+#else
+  int64_t S = std::max<int64_t>(1, (256 + total_tiles - 1) / total_tiles);  // a block per CU
+#endif
   S = std::min<int64_t>(S, kSplitMax);
   S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
   return (int)S;
@@ -1125,14 +1271,21 @@ struct WgradBatch {
   void bias(const float* dZ, int R, int64_t M, float* db) {
     WgradJob j{};
     j.dZ = dZ; j.In = nullptr; j.dW = db; j.M = M; j.R = R; j.C = 1; j.ldi = 1; j.ldw = 1; j.c0 = 0;
+    j.bias = 1;
     jobs.push_back(j);
   }
   // lay out tiles, slices and partial offsets; returns the partial floats needed
   size_t plan(int& S) {
     int64_t tiles = 0, Mmax = 1;
     for (auto& j : jobs) {
+#ifdef NRT_WGRAD_V1
       j.tiles_c = (j.C + 63) / 64;
       j.n_tiles = ((j.R + 63) / 64) * j.tiles_c;
+#else
+      // k_wgrad_tile: 128 x 128 tiles; a bias job is one block per slice
+      j.tiles_c = j.bias ? 1 : (j.C + kWgT - 1) / kWgT;
+      j.n_tiles = j.bias ? 1 : ((j.R + kWgT - 1) / kWgT) * j.tiles_c;
+#endif
       tiles += j.n_tiles;
       Mmax = std::max(Mmax, j.M);
     }
@@ -1165,8 +1318,14 @@ struct WgradBatch {
     for (auto& j : jobs) flop += 2.0 * j.R * j.C * (double)j.M;
     {
       ProfScope prof("k_wgrad", st, flop);
+#ifdef NRT_WGRAD_V1
       k_wgrad_batch<><<<dim3((unsigned)blocks), dim3(64 * kWgradWaves), 0, st>>>(tj, (int)jobs.size(), S, part);
       if (int rc = check_launch("k_wgrad_batch")) return rc;
+#else
+      if (int rc = set_lds(k_wgrad_tile<>, kWgLdsBytes)) return rc;
+      k_wgrad_tile<><<<dim3((unsigned)blocks), dim3(512), kWgLdsBytes, st>>>(tj, (int)jobs.size(), S, part);
+      if (int rc = check_launch("k_wgrad_tile")) return rc;
+#endif
     }
     k_split_reduce_batch<><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
         tj, (int)jobs.size(), S, total, part);

@@ -167,6 +167,21 @@ __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// F.softplus (beta 1, threshold 20) in FP32 on the hardware transcendentals: max(x, 0) +
+// log1p(e), e = exp(-|x|) in (0, 1], with log1p(e) = log(u) e / (u - 1), u = fl(1 + e) -- the
+// classic compensation of the rounding of 1 + e (Goldberg), accurate to a few ulp with the ~1-ulp
+// v_exp / v_log / v_rcp.  ~12 VALU against ~100 for ocml's log1pf(expf(x)) (double-float
+// arithmetic), which left the FP32 march VALU-bound (one chunk's activations cost as much issue
+// time as its 128 MFMAs) and most of the SDF shift backward's issue time.
+__device__ __forceinline__ float softplus_exact(float x) {
+  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+  const float u = 1.f + e;
+  const float d = u - 1.f;
+  const float l1p = d == 0.f ? e : (__builtin_amdgcn_logf(u) * kLn2) * (e * __builtin_amdgcn_rcpf(d));
+  return x > 20.f ? x : fmaxf(x, 0.f) + l1p;
+}
+
 // torch semantics: F.leaky_relu (slope 0.01), F.softplus (beta 1, threshold 20), sigmoid, relu
 template <bool FAST>
 __device__ __forceinline__ float act_fwd(float x, int act) {
@@ -174,7 +189,7 @@ __device__ __forceinline__ float act_fwd(float x, int act) {
     case ACT_LEAKY: return x > 0.f ? x : x * 0.01f;
     case ACT_SOFTPLUS:
       if (FAST) return x > 20.f ? x : __logf(1.f + __expf(x));
-      return x > 20.f ? x : log1pf(expf(x));
+      return softplus_exact(x);
     case ACT_SIGMOID:
       return FAST ? 1.f / (1.f + __expf(-x)) : 1.f / (1.f + expf(-x));
     case ACT_RELU: return x > 0.f ? x : 0.f;
@@ -1459,11 +1474,18 @@ __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// 16-row sub-blocks per chunk: 64 output rows (four independent MFMA chains) between barriers.
+// Round 4 ran 32-row chunks; the headline march's PMC showed 28 % of wave time parked at the
+// per-chunk barrier (MFMA busy 0.76), so a chunk now carries twice the MFMAs per barrier.  A skip
+// layer's encoding part is a chunk of its own (64 rows x the encoding quads), which keeps the
+// largest chunk (and the 2-slot ring) at 64 KiB for H = 256.
+constexpr int kSub = 4;
+
 // KH = H / 4 hidden k-steps, KE = ke / 4 encoding k-steps (ke = encoding slots padded to 16)
 template <int KH, int KE, int WV>
 struct Engine {
   static constexpr int QH = KH / 4, QE = KE / 4;        // quads per sub-block
-  static constexpr int MAXQ = 2 * (QH + QE);            // largest chunk (a skip layer's), KiB
+  static constexpr int MAXQ = kSub * (QH > QE ? QH : QE);  // largest chunk, KiB
   static constexpr int MAXL = (MAXQ + WV - 1) / WV;     // DMA pieces per wave per chunk
   static constexpr int SLOTQ = MAXL * WV;
   static constexpr int RING_BYTES = 2 * SLOTQ * 1024;
@@ -1559,20 +1581,8 @@ struct Engine {
   }
 };
 
-// F.softplus (beta 1, threshold 20) in FP32 on the hardware transcendentals: max(x, 0) +
-// log1p(e), e = exp(-|x|) in (0, 1], with log1p(e) = log(u) e / (u - 1), u = fl(1 + e) -- the
-// classic compensation of the rounding of 1 + e (Goldberg), accurate to a few ulp with the ~1-ulp
-// v_exp / v_log / v_rcp.  ~12 VALU against ~100 for ocml's log1pf(expf(x)) (double-float
-// arithmetic), which left the FP32 march VALU-bound: one chunk's activations (8 per lane) cost as
-// much issue time as its 128 MFMAs.
-__device__ __forceinline__ float softplus_f32(float x) {
-  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
-  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
-  const float u = 1.f + e;
-  const float d = u - 1.f;
-  const float l1p = d == 0.f ? e : (__builtin_amdgcn_logf(u) * kLn2) * (e * __builtin_amdgcn_rcpf(d));
-  return x > 20.f ? x : fmaxf(x, 0.f) + l1p;
-}
+// the FP32 ring engine's softplus (softplus_exact, above)
+__device__ __forceinline__ float softplus_f32(float x) { return softplus_exact(x); }
 
 // the MLP activation with the code a template argument (torch semantics, FP32)
 template <int ACT>
@@ -1608,6 +1618,33 @@ __device__ __forceinline__ void seg2(const float4* A, const float (&B)[NBV], f4v
   seg2<NQ, P0, BO>(A, B, a0, a1, [](int) {});
 }
 
+// seg2 for a four-sub-block chunk: NQ quads at ring positions P0 + 4u + b, four chains a[b];
+// each quad's four LDS reads issued one quad ahead of its MFMAs, side(u) before them
+template <int NQ, int P0, int BO, int NBV, class Side>
+__device__ __forceinline__ void seg4(const float4* A, const float (&B)[NBV], f4v (&a)[kSub],
+                                     Side&& side) {
+  float4 w[kSub];
+#pragma unroll
+  for (int b = 0; b < kSub; ++b) w[b] = A[(P0 + b) * 64];
+#pragma unroll
+  for (int u = 0; u < NQ; ++u) {
+    side(u);
+    float4 n[kSub];
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) n[b] = (u + 1 < NQ) ? A[(P0 + kSub * (u + 1) + b) * 64] : w[b];
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) a[b] = mfma4(w[b].x, B[BO + 4 * u], a[b]);
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) a[b] = mfma4(w[b].y, B[BO + 4 * u + 1], a[b]);
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) a[b] = mfma4(w[b].z, B[BO + 4 * u + 2], a[b]);
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) a[b] = mfma4(w[b].w, B[BO + 4 * u + 3], a[b]);
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) w[b] = n[b];
+  }
+}
+
 // forward-mode activation (TAN): the lane's column is 4 ray + comp, comp 0 the value
 // pre-activation z, comps 1..3 the tangent dz/dx_{comp-1}; every lane takes its ray's z from the
 // quad leader and returns act(z) (comp 0) or act'(z) dz (torch's backward formulas, act_bwd)
@@ -1626,8 +1663,8 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
                                       float x2) {
   using En = Engine<KH, KE, WV>;
   constexpr int QH = En::QH, QE = En::QE;
-  constexpr int NC = KH / 8;  // 32-row chunks per layer
-  static_assert(QH >= 8, "hidden chunks must have a quad per pending activation");
+  constexpr int NC = KH / (4 * kSub);  // 64-row chunks per layer
+  static_assert(QH >= 8 && KH % (4 * kSub) == 0, "hidden chunks must spread the pending activations");
   const int g = E.lane >> 4;
   const int comp = TAN ? (E.lane & 3) : 0;
   const bool value = comp == 0;
@@ -1675,34 +1712,36 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
     if (TAN) b *= bmask;
     return b;
   };
-  auto chunk_q = [&](int i) {  // quads of hidden layer i's chunks (i == L: the out layer)
-    if (i >= L) return QH;
-    return 2 * QH + ((i != L - 1 && i % SK == 0) ? 2 * QE : 0);
-  };
+  constexpr int CH = kSub * QH, CE = kSub * QE;  // KiB of a hidden-part / encoding-part chunk
+  // the first chunk of hidden layer i (i == L: the out layer)
+  auto first_q = [&](int i) { return i >= L ? QH : CH; };
   float src[KH], dst[KH];
-  f4v pend0, pend1;
+  f4v pend[kSub];
   // activation of chunk ib's accumulators into dst.  The empty asm pins each result inside the
   // chunk that computes it: dst is read only by the next layer, so the compiler would otherwise
   // sink every chunk's activations to the end of the layer, out of the MFMA gaps.
-  auto retire1 = [&](int ib, int k) {  // element k (< 8) of chunk ib
+  auto retire1 = [&](int ib, int k) {  // element k (< 4 kSub) of chunk ib
     const int r = k & 3;
-    float& d = dst[8 * ib + k];
-    if (TAN) d = act_tan32<ACT>(k < 4 ? pend0[r] : pend1[r], value);
-    else d = act<ACT>(k < 4 ? pend0[r] : pend1[r]);
+    float& d = dst[4 * kSub * ib + k];
+    if (TAN) d = act_tan32<ACT>(pend[k >> 2][r], value);
+    else d = act<ACT>(pend[k >> 2][r]);
     asm volatile("" : "+v"(d));
   };
   auto retire = [&](int ib) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) retire1(ib, k);
+    for (int k = 0; k < 4 * kSub; ++k) retire1(ib, k);
   };
   // init layer (neural_blocks.py:80): raw encoding in
 #pragma unroll
   for (int ib = 0; ib < NC; ++ib) {
-    const float4* A = E.begin(2 * QE, ib + 1 < NC ? 2 * QE : chunk_q(0), false);
-    f4v a0 = bias(0, 2 * ib), a1 = bias(0, 2 * ib + 1);
+    const float4* A = E.begin(CE, ib + 1 < NC ? CE : first_q(0), false);
+    f4v a[kSub];
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) a[b] = bias(0, kSub * ib + b);
     if (ib > 0) retire(ib - 1);
-    seg2<QE, 0, 0>(A, eraw, a0, a1);
-    pend0 = a0; pend1 = a1;
+    seg4<QE, 0, 0>(A, eraw, a, [](int) {});
+#pragma unroll
+    for (int b = 0; b < kSub; ++b) pend[b] = a[b];
     E.end();
   }
   retire(NC - 1);
@@ -1711,24 +1750,33 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
 #pragma unroll
     for (int k = 0; k < KH; ++k) src[k] = dst[k];
     const bool skip = i != L - 1 && i % SK == 0;
-    const int nq = chunk_q(i);
 #pragma unroll
     for (int ib = 0; ib < NC; ++ib) {
-      const float4* A = E.begin(nq, ib + 1 < NC ? nq : chunk_q(i + 1), false);
-      f4v a0 = bias(1 + i, 2 * ib), a1 = bias(1 + i, 2 * ib + 1);
-      // the previous chunk's activations: one per quad over the first 8 quads (QH >= 8)
-      seg2<QH, 0, 0>(A, src, a0, a1, [&](int u) {
-        if (ib > 0 && u < 8) retire1(ib - 1, u);
+      const int after = ib + 1 < NC ? CH : first_q(i + 1);  // the chunk after this row block
+      const float4* A = E.begin(CH, skip ? CE : after, false);
+      f4v a[kSub];
+#pragma unroll
+      for (int b = 0; b < kSub; ++b) a[b] = bias(1 + i, kSub * ib + b);
+      // the previous chunk's 4 kSub activations spread over this chunk's QH quads
+      seg4<QH, 0, 0>(A, src, a, [&](int u) {
+        if (ib > 0)
+#pragma unroll
+          for (int k = (u * 4 * kSub) / QH; k < ((u + 1) * 4 * kSub) / QH; ++k) retire1(ib - 1, k);
       });
-      if (skip) seg2<QE, 2 * QH, 0>(A, eact, a0, a1);
-      pend0 = a0; pend1 = a1;
       E.end();
+      if (skip) {  // the encoding part: a chunk of its own
+        const float4* B = E.begin(CE, after, false);
+        seg4<QE, 0, 0>(B, eact, a, [](int) {});
+        E.end();
+      }
+#pragma unroll
+      for (int b = 0; b < kSub; ++b) pend[b] = a[b];
     }
     retire(NC - 1);
   }
   // out layer (neural_blocks.py:86): one 16-row sub-block, two half chains (k-steps of even /
   // odd quads) so consecutive MFMAs are independent; row 0 of ray j sits in register 0 of lane j
-  const float4* A = E.begin(QH, 2 * QE, true);
+  const float4* A = E.begin(QH, CE, true);
   f4v o0 = bias(L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
   {
     float4 w0 = A[0], w1 = A[64];

@@ -144,9 +144,10 @@ unsigned long long* profile_eval_counter();
 // refresh map (source indices, nrt_refresh.hip).  f(layer, row, pos) is called once per stream
 // float, in order; pos is the layer input: hidden feature k in [0, H) or H + encoding slot; rows
 // past the layer's R are padding.
-//   chunk = 32 output rows (2 sub-blocks of 16) of one layer; the out layer is one chunk of one
-//   sub-block (rows 0..15).  A chunk is quads u = 0 .. qh + qe - 1 (qh = H / 16 hidden, qe =
-//   ke / 16 encoding quads), each quad [sub-block b][lane][t] = 1 KiB per sub-block: lane (g =
+//   chunk = 64 output rows (ring32::kSub = 4 sub-blocks of 16) of one layer; the out layer is one
+//   chunk of one sub-block (rows 0..15).  A chunk is quads u = 0 .. qh + qe - 1 (qh = H / 16
+//   hidden, qe = ke / 16 encoding quads; the eval takes a skip layer's encoding quads as a chunk of
+//   their own), each quad [sub-block b][lane][t] = 1 KiB per sub-block: lane (g =
 //   lane >> 4, i = lane & 15) holds A[row 16 b + i][k = g] of k-steps 4u + t.  Hidden k-step s
 //   takes feature 16 (s >> 2) + 4 g + (s & 3) in lane group g -- register s & 3 of sub-block s >> 2
 //   of the previous layer's 16x16 accumulator -- and encoding k-step e takes slot 4 e + g.
@@ -156,9 +157,10 @@ struct Ring32Layer {
 };
 template <class F>
 inline void ring32_walk(const std::vector<Ring32Layer>& ls, int H, int ke, F&& f) {
+  constexpr int S = ring32::kSub;  // sub-blocks per chunk (64 output rows)
   for (size_t l = 0; l < ls.size(); ++l) {
     const bool out = l + 1 == ls.size();
-    const int nsub = out ? 1 : 2, nch = out ? 1 : (ls[l].R + 31) / 32;
+    const int nsub = out ? 1 : S, nch = out ? 1 : (ls[l].R + 16 * S - 1) / (16 * S);
     const int qh = ls[l].hid ? H / 16 : 0, qe = ls[l].enc ? ke / 16 : 0;
     for (int c = 0; c < nch; ++c)
       for (int u = 0; u < qh + qe; ++u)

@@ -518,7 +518,7 @@ struct RingPol32 {
   using Eng = ring32::Engine<KH, KE, WV>;
   __device__ __forceinline__ static void init(Eng& E, const SdfDev& s, const MlpDev& m, char* lds,
                                               const MarchArgs&) {
-    E.init(m, s, lds, 2 * Eng::QE);
+    E.init(m, s, lds, ring32::kSub * Eng::QE);
   }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;

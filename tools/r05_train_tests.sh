@@ -18,3 +18,9 @@ for l in open("gpurun_out/r05/train.jsonl"):
     print(d["config"]["precision"], round(d["ms_per_step"], 2), d["final_loss"],
           {k: (round(v["ms_per_step"], 2), round(v["frac"], 3)) for k, v in r["kernels"].items()})
 PY
+# the FP16 march's persistent grid on a small batch: every CU (option march_blocks) vs the default
+for MB in 256; do
+  timeout -k 10 300 python -u bench.py --scene train --precision mixed --steps 10 --warmup 2 --no-cpu-baseline --nrt-option march_blocks=$MB > gpurun_out/r05/train_mb$MB.json 2> gpurun_out/r05/train_mb.err
+  rc=$?; echo "TRAIN mixed march_blocks=$MB EXIT $rc"; [ $rc -eq 0 ] || exit $rc
+  python -c "import json; d=json.load(open('gpurun_out/r05/train_mb$MB.json')); print('march_blocks=$MB', round(d['ms_per_step'],2), d['final_loss'], round(d['kernel_ms_per_step']['k_intersect'],2))"
+done
