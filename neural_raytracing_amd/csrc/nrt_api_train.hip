@@ -963,6 +963,9 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
 // dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row segments per half-wave -- then the waves'
 // accumulators are summed in wave order through LDS and the slice partials in slice order
 // (deterministic).  S is chosen from the shapes alone (same inputs, same bits).
+#ifndef NRT_WGRAD_TILE
+#define NRT_WGRAD_V1 1
+#endif
 constexpr int kSplitMax = 64;
 constexpr int64_t kSliceRows = 256;  // batch rows per slice at least
 constexpr int kWgradWaves = 4;        // waves per block
@@ -1080,7 +1083,12 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
     }
 }
 
-// ---- LDS-staged weight gradients (default; NRT_WGRAD_V1 builds the kernel above) -----------
+// ---- LDS-staged weight gradients (NRT_WGRAD_TILE builds it in place of k_wgrad_batch) --------
+// Measured slower than k_wgrad_batch on the training step's batches (7.0 vs 3.3 ms a step): one
+// 8-wave block per CU leaves ~1 wave per SIMD once the slices are dealt (29 weight tiles x 6
+// slices for the spatial MLP's 47 jobs), the 96-row NeuralBSDF tiles fill 37 % of a 256 x 256
+// tile, and the bias jobs' column sums are latency chains.  Kept for the next attempt (smaller
+// tiles, more blocks).
 // k_wgrad_batch fed each MFMA from 4-byte global loads in the MFMA's lane order (round-4 PMC:
 // 65-75 % of wave time waiting at ~0.5 MFMA busy) and, with 64 x 64 tiles, read a 256 x 256
 // layer's dZ and In slices four times each.  Here one block of 8 waves computes a whole 256 x 256

@@ -169,7 +169,7 @@ inline void ring32_walk(const std::vector<Ring32Layer>& ls, int H, int ke, F&& f
             for (int t = 0; t < 4; ++t) {
               const int s = 4 * u + t, g = lane >> 4;
               const int pos = u < qh ? 16 * (s >> 2) + 4 * g + (s & 3) : H + 4 * (s - 4 * qh) + g;
-              f((int)l, 32 * c + 16 * b + (lane & 15), pos);
+              f((int)l, 16 * S * c + 16 * b + (lane & 15), pos);
             }
   }
 }
