@@ -502,7 +502,10 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      wave per 32-column row block on the same 32 rows; the encoding in global
  *                      tiles where that doubles the blocks per CU), 2 = the same with the encoding
  *                      in the LDS slab unless fewer than two blocks fit, 0 = one wave per 32 rows
- *                      (round 3).  Gradients bit-equal across values.
+ *                      (round 3).  Gradients bit-equal across values.  nrt_mlp_grad_backward
+ *                      follows the option too: any nonzero value selects its column-split
+ *                      kernel (k_mlp_grad_backward32_cs, the slab in LDS; 1 and 2 run the same
+ *                      kernel there), 0 the per-wave kernel.
  *   "bwd_ring"       1  nrt_mlp_backward(_multi) of the shading MLPs' shapes (LightField 10x256
  *                      F=16, spatial weights 16x256 F=128, NeuralBSDF 6x96 F=64: leaky_relu, 3
  *                      inputs, no latent) on the FP32 ring engine (16-row tiles, the weights and
