@@ -96,6 +96,21 @@ int nrt_mlp_refresh(nrt_mlp* mlp, const float* const* device_weights,
 /* y[M, out] = SkipConnMLP(x[M, in], latent[M, latent]) -- neural_blocks.py:75-86 */
 int nrt_mlp_forward(const nrt_mlp* mlp, const float* x, const float* latent, int64_t M,
                     float* y, int precision, void* stream);
+/* y[k][M, out] = mlps[k](x) for n same-shape MLPs without latent on one input: the NeuralBSDF
+ * components of a spatially varying mixture on the shared Rusinkiewicz features (bsdfs.py:
+ * 634-637, called per component there).  At FP32 the shading MLP shapes run as one launch on
+ * the ring engine (n x the row blocks, up to 16 MLPs a launch); other shapes and precisions are
+ * n nrt_mlp_forward calls.  Each y[k] equals nrt_mlp_forward(mlps[k], ...) bit for bit.
+ * save (training; NULL for none): one device buffer of nrt_mlp_save_bytes(mlps[k], M) bytes per
+ * MLP; the forward also stores the activations the backward needs (every hidden layer's and the
+ * Fourier encoding), so nrt_mlp_backward_saved does not evaluate the forward again -- the torch
+ * autograd contract (the forward saves, the backward reads).  FP32 only; NRT_EUNSUPPORTED for
+ * MLPs whose nrt_mlp_save_bytes is 0. */
+int nrt_mlp_forward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                          float* const* y, void* const* save, int precision, void* stream);
+/* Bytes of one MLP's saved activations for M rows; 0 when the MLP has no saving forward (the
+ * shading shapes of the ring backward only: see option "bwd_ring"). */
+size_t nrt_mlp_save_bytes(const nrt_mlp* mlp, int64_t M);
 
 /* Backward of nrt_mlp_forward in FP32 (torch autograd through
  * SkipConnMLP.forward, neural_blocks.py:75-86): given dy [M, out] = dL/dy, writes
@@ -118,6 +133,15 @@ int nrt_mlp_backward(const nrt_mlp* mlp, const float* x, const float* latent, in
  * workspace: nrt_mlp_backward_multi_workspace_bytes(mlps, n, M) bytes. */
 size_t nrt_mlp_backward_multi_workspace_bytes(const nrt_mlp* const* mlps, int n, int64_t M);
 int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                           const float* const* dy, float* const* dx, float* const* dweights,
+                           float* const* dbiases, void* workspace, void* stream);
+/* nrt_mlp_backward_multi from the activations nrt_mlp_forward_multi saved (saved[i], Ms rows):
+ * the backward chain and the weight gradients only.  Row i of this call (x [M, in], dy[i]) is
+ * saved row rows[i] (int32 [M]; NULL: M == Ms and row i) -- the rows with a gradient, compacted
+ * by the caller.  Same gradients as nrt_mlp_backward_multi on those rows, bit for bit.
+ * workspace: nrt_mlp_backward_multi_workspace_bytes(mlps, n, M) bytes. */
+int nrt_mlp_backward_saved(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                           const int32_t* rows, const void* const* saved, int64_t Ms,
                            const float* const* dy, float* const* dx, float* const* dweights,
                            float* const* dbiases, void* workspace, void* stream);
 
@@ -512,6 +536,9 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      the transposed weights streamed through a block-shared LDS ring, dZ kept in
  *                      registers between layers); 0: the bwd_colsplit kernels.  Same gradients to
  *                      FP32 rounding (different summation order), both held to float64 autograd
+ *   "train_save"     1  nrt_mlp_save_bytes > 0 for the ring backward's shapes (the training
+ *                      forward saves its activations, nrt_mlp_backward_saved skips the forward
+ *                      evaluation); 0: nrt_mlp_save_bytes returns 0 (the backward recomputes)
  *   "mixed_drift"    0  1: the flag bound is d * (1 + a per-ray drift estimate built from the
  *                      ratio of consecutive step values) instead of d * (1 + step/16); measured
  *                      to flag more rays for the same accuracy (152 vs 133 ms), kept for A/B
@@ -520,6 +547,12 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      per-wave k_occlusion; same visibility bar either way
  *   "mixed_refine_s" 2000 NRT_MIXED: sdf(best) re-evaluates the scan's runner-up when the FP16
  *                      minimum and runner-up lie within s (1e-7 units)
+ *   "march_queue"    2  nrt_sdf_intersect's ring marches: 1 = one launch-wide job queue (waves
+ *                      take 16 jobs at a time from [every ray's march][every ray's scan
+ *                      segments] through a device counter) instead of per-wave job lists, 0 =
+ *                      the lists, 2 = the queue for batches of >= 131,072 rays (64 a resident
+ *                      wave; the 800^2 frame 1 % faster, the 38,400-ray training march 1-5 %
+ *                      slower on it); same results (a ray's values do not depend on the schedule)
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
 int nrt_set_option(const char* name, int64_t value);

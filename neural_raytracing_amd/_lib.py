@@ -67,6 +67,8 @@ _SIGNATURES = {
     "nrt_mlp_destroy": (_I32, [_P]),
     "nrt_mlp_refresh": (_I32, [_P, _P, _P, _P]),
     "nrt_mlp_forward": (_I32, [_P, _P, _P, _I64, _P, _I32, _P]),
+    "nrt_mlp_forward_multi": (_I32, [_P, _I32, _P, _I64, _P, _P, _I32, _P]),
+    "nrt_mlp_save_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_sdf_create_unit_sphere": (_I32, [ctypes.POINTER(_P)]),
     "nrt_sdf_create_mlp": (_I32, [_P, ctypes.POINTER(_P)]),
     "nrt_sdf_create_sphere_blob": (_I32, [_I32, _P, _P, _P, _F, _P, ctypes.POINTER(_P)]),
@@ -116,6 +118,7 @@ _SIGNATURES = {
     "nrt_mlp_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _P]),
     "nrt_mlp_backward_multi_workspace_bytes": (ctypes.c_size_t, [_P, _I32, _I64]),
     "nrt_mlp_backward_multi": (_I32, [_P, _I32, _P, _I64, _P, _P, _P, _P, _P, _P]),
+    "nrt_mlp_backward_saved": (_I32, [_P, _I32, _P, _I64, _P, _P, _I64, _P, _P, _P, _P, _P, _P]),
     "nrt_mlp_grad_backward_workspace_bytes": (ctypes.c_size_t, [_P, _I64]),
     "nrt_mlp_grad_backward": (_I32, [_P, _P, _P, _I64, _P, _P, _P, _P, _P]),
     "nrt_frames": (_I32, [_P, _P, _I64, _P, _P, _P]),

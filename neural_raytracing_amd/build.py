@@ -10,7 +10,7 @@ SOURCES = ["nrt_common.hip", "nrt_pack.hip", "nrt_api_mlp.hip", "nrt_api_sdf.hip
            "nrt_api_shade.hip", "nrt_api_cam.hip", "nrt_ring_march.hip", "nrt_ring_march32.hip", "nrt_ring_march3.hip", "nrt_ring_mixed.hip", "nrt_ring_normal.hip", "nrt_prog.hip", "nrt_shade_ring.hip", "nrt_ring_normal32.hip", "nrt_callable.hip", "nrt_api_nerf.hip",
            "nrt_api_path.hip", "nrt_api_train.hip", "nrt_refresh.hip", "nrt_sphere.hip", "nrt_sphere_smoothmin.hip", "nrt_api_tile.hip"]
 HEADERS = ["nrt_kernels.h", "nrt_device.h", "nrt_internal.h", "nrt_launch.h", "nrt_ring3.h",
-           "nrt_shade_ring.h"]
+           "nrt_shade_ring.h", "nrt_train_ring.h"]
 HEADER = os.path.join(os.path.dirname(HERE), "include", "nrt.h")
 
 # -ffp-contract=off: elementwise math rounds like the reference's eager torch ops (no silent FMA
@@ -27,9 +27,17 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _obj(src):
+    return os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+
+
 def needs_build():
+    """Any object older than its source or a header (an edit made while a build ran leaves the
+    .so newer than the edit but its object stale), or the .so older than an object."""
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [HEADER]
-    return _stale(OUT, [os.path.join(CSRC, s) for s in SOURCES] + hdrs)
+    if any(_stale(_obj(s), [os.path.join(CSRC, s)] + hdrs) for s in SOURCES):
+        return True
+    return _stale(OUT, [_obj(s) for s in SOURCES])
 
 
 def build(force=False, verbose=True, jobs=None):
@@ -42,7 +50,7 @@ def build(force=False, verbose=True, jobs=None):
     hdrs = [os.path.join(CSRC, h) for h in HEADERS] + [HEADER]
 
     def compile_one(src):
-        obj = os.path.join(OBJDIR, os.path.splitext(src)[0] + ".o")
+        obj = _obj(src)
         path = os.path.join(CSRC, src)
         if force or _stale(obj, [path] + hdrs):
             cmd = [hipcc, *FLAGS, "-c", path, "-o", obj]

@@ -1652,6 +1652,84 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   return batch.run(table, part, cap, st);
 }
 
+int nrt_mlp_backward_saved(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                           const int32_t* rows, const void* const* saved, int64_t Ms,
+                           const float* const* dy, float* const* dx, float* const* dweights,
+                           float* const* dbiases, void* workspace, void* stream) {
+  if (!mlps || n <= 0 || M < 0 || !dy || !saved || Ms < 0 || (!rows && M != Ms) ||
+      (M > 0 && (!x || !workspace))) {
+    set_error("nrt_mlp_backward_saved: bad argument");
+    return NRT_EINVAL;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (!mlps[i] || !saved[i] || !same_shape(mlps[0], mlps[i])) {
+      set_error("nrt_mlp_backward_saved: the MLPs must share one shape, each with its saved activations");
+      return NRT_EINVAL;
+    }
+  }
+  const MlpDev& d = mlps[0]->host_dev;
+  if (M > INT32_MAX || Ms > INT32_MAX) { set_error("nrt_mlp_backward_saved: at most 2^31-1 rows per call"); return NRT_EINVAL; }
+#ifdef NRT_WGRAD_TILE
+  set_error("nrt_mlp_backward_saved: not with the NRT_WGRAD_TILE weight-gradient kernel");
+  return NRT_EUNSUPPORTED;
+#endif
+  if (!ring_backward_ok(mlps, n)) {
+    set_error("nrt_mlp_backward_saved: no ring backward for these MLPs (nrt_mlp_save_bytes is 0)");
+    return NRT_EUNSUPPORTED;
+  }
+  const int L = d.n_hidden, H = d.hidden, NL = L + 2;
+  if (M == 0)
+    return nrt_mlp_backward_multi(mlps, n, x, 0, dy, dx, dweights, dbiases, workspace, stream);
+  hipStream_t st = (hipStream_t)stream;
+  char* p = (char*)workspace;  // nrt_mlp_backward_multi_workspace_bytes(mlps, n, M)
+  std::vector<TrainWs> ws(n);
+  std::vector<SavedActs> sa(n);
+  std::vector<float*> A(n), dZ(n), Ac(n), Er(n), Ea(n);
+  std::vector<const float*> Sr(n), Sa(n);
+  for (int i = 0; i < n; ++i) {
+    ws[i] = carve(mlps[i], M, p);
+    p += region_bytes(d, M);
+    sa[i] = saved_split(d, Ms, saved[i]);
+    A[i] = sa[i].A;
+    dZ[i] = ws[i].dZ;
+    // compacted rows: the backward copies the saved rows it reads into the workspace (the
+    // weight gradients' operands, row-aligned with dZ)
+    Ac[i] = ws[i].A; Er[i] = ws[i].Eraw; Ea[i] = ws[i].Eact;
+    Sr[i] = sa[i].Eraw; Sa[i] = sa[i].Eact;
+    if (!rows) { Ac[i] = nullptr; Er[i] = nullptr; Ea[i] = nullptr; }
+  }
+  p += a256((size_t)n * sizeof(BwdJob));
+  void* table = p;
+  p += a256((size_t)n * kWgradTableBytes);
+  float* part = (float*)p;
+  int rc = NRT_OK;
+  {
+    ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M * n * 0.5);
+    if ((rc = ring_backward(mlps, n, x, M, dy, dx, A.data(), dZ.data(), Er.data(), Ea.data(), table, st,
+                            rows, Ms, Ac.data(), Sr.data(), Sa.data())))
+      return rc;
+  }
+  if (!dweights && !dbiases) return NRT_OK;
+  const size_t lay = (size_t)M * H;
+  WgradBatch batch;
+  const size_t cap = multi_part_floats(d, n, M, &batch.slices);
+  multi_jobs(d, n, M, batch, [&](int i, int l, int R, int kind, int C, int ldw, int c0) {
+    const float* dZl = l == L + 1 ? dy[i] : ws[i].dZ + (size_t)l * lay;
+    if (kind == 3) {
+      if (dbiases && dbiases[(size_t)i * NL + l]) batch.bias(dZl, R, M, dbiases[(size_t)i * NL + l]);
+      return;
+    }
+    if (!dweights || !dweights[(size_t)i * NL + l]) return;
+    // without compaction the saved activations themselves (Ms == M), else their compacted copy
+    const float* Ar = rows ? ws[i].A : sa[i].A;
+    const float* In = kind == 0 ? (rows ? ws[i].Eraw : sa[i].Eraw)
+                    : kind == 1 ? Ar + (size_t)(l - 1) * lay
+                                : (rows ? ws[i].Eact : sa[i].Eact);
+    batch.weight(dZl, R, In, C, M, dweights[(size_t)i * NL + l], ldw, c0);
+  });
+  return batch.run(table, part, cap, st);
+}
+
 static size_t gb_sizes(const MlpDev& d, int64_t M, size_t sz[9]) {
   const size_t lay = (size_t)(d.n_hidden + 1) * (size_t)M * d.hidden * 4;
   sz[0] = lay;          // Z

@@ -19,6 +19,7 @@ struct nrt_rprog {
   void* buf = nullptr;
   bool built = false;    // build attempted
   bool ok = false;       // false: some MLP has a shape without a compiled kernel
+  int fwd_chunks = 0;    // backward programs (build_rprog mode 1): chunks of the forward part
   ~nrt_rprog() { if (buf) (void)hipFree(buf); }
 };
 

@@ -286,7 +286,12 @@ struct MarchArgs {
   // shadow march (march_body mode 3): each ray's distance to the light; `count` (device) bounds
   // the compacted ray list
   const float* occ_max_t = nullptr;
+  // ring marches: one launch-wide job queue instead of per-wave lists (option "march_queue"):
+  // a zeroed device counter; waves take kQueueChunk jobs at a time from the launch's whole list
+  // ([march of every ray][scan segment s of every ray, s = 0 .. 7]); nullptr = per-wave lists
+  unsigned int* queue = nullptr;
 };
+constexpr int kQueueChunk = 16;
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
 __device__ __forceinline__ double scan_step_of(const MarchArgs& a, int64_t ray) {
@@ -584,11 +589,14 @@ __device__ __forceinline__ void march_body(
           ? (int64_t)__builtin_amdgcn_readfirstlane(*(const NRT_GLOBAL int32_t*)a.count)
           : P;
   const OwnedRays own(Pe, nw, w, WV, a.xcd_lines != 0);
-  const int64_t R = own.R;  // rays owned by this wave
+  // launch-wide queue (MarchArgs::queue): the list is every ray's, job k's ray is k, and every
+  // scan runs as segments; otherwise this wave's own rays
+  const bool dyn = a.queue != nullptr;
+  const int64_t R = dyn ? Pe : own.R;  // rays of this wave's list
   const bool scan = mode == 0 && a.primary;
   // scan jobs: the whole 129-point scan of each of the first R - T rays (one plain key store),
   // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail
-  const int64_t T = kScanSplit < 0 ? R : (R < kScanSplit ? R : (int64_t)kScanSplit);
+  const int64_t T = (dyn || kScanSplit < 0) ? R : (R < kScanSplit ? R : (int64_t)kScanSplit);
   // sdf(best) with a runner-up key: a second job per ray re-evaluates the runner-up where the
   // FP16 scan could not order the two (skipped elsewhere)
   const bool alt = MX && mode == 1 && a.keys2 != nullptr;
@@ -609,6 +617,8 @@ __device__ __forceinline__ void march_body(
   float mt = 0.f;                   // mode 3: the ray's distance to the light
   unsigned long long cps = ~0ull;   // NRT_MIXED: the zone checkpoint (MarchArgs::zone)
   int64_t cursor = 0;  // wave-uniform
+  int64_t cend = 0;    // queue: end of the wave's current chunk [cursor, cend)
+  bool dry = false;    // queue: drained
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
     for (;;) {
@@ -667,13 +677,25 @@ __device__ __forceinline__ void march_body(
       }
       const uint32_t want = (uint32_t)__ballot(kind == -1) & kRayMask;
       if (want == 0u) break;
-      if (cursor >= J) {
+      int64_t avail = J - cursor;  // list entries this pass can hand out from `cursor` on
+      if (dyn) {
+        if (cursor >= cend && !dry) {  // the next chunk of the launch's list
+          unsigned int b = 0u;
+          if (lane == 0) b = atomicAdd(a.queue, (unsigned int)kQueueChunk);
+          cursor = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+          cend = cursor + kQueueChunk < J ? cursor + kQueueChunk : J;
+          dry = cursor >= J;
+        }
+        avail = dry ? 0 : cend - cursor;
+      }
+      if (avail <= 0) {
         if (kind == -1) kind = -2;
         break;
       }
       if (kind == -1) {
         const int64_t q = cursor + __popc(want & lt);
-        if (q < J) {
+        // (a lane past a queue chunk's end stays -1 and takes from the next chunk)
+        if (q - cursor < avail) {
           int64_t k = q;
           int seg = -1;  // -1 march, kScanSegs whole scan, else a segment
           if (mode == 0 && q >= R) {
@@ -688,7 +710,7 @@ __device__ __forceinline__ void march_body(
           }
           const bool second_job = alt && q >= R;  // sdf(best)'s runner-up job
           if (second_job) k = q - R;
-          ray = own.ray(k);
+          ray = dyn ? k : own.ray(k);
           if (MX && a.list) ray = a.list[ray];
           if (mode == 2) {  // point evaluation: `rays` holds [P, 3] points, sdf(p) -> thr_out
             const float* pp = rays + ray * 3;
@@ -730,11 +752,11 @@ __device__ __forceinline__ void march_body(
             jend = whole ? 16 * kScanSegs : 16 * seg + 16;
             idx = -1;
           }
-        } else {
+        } else if (!dyn) {
           kind = -2;
         }
       }
-      cursor += __popc(want);
+      cursor += __popc(want) < avail ? (int64_t)__popc(want) : avail;
     }
     if (__syncthreads_or(kind >= 0 ? 1 : 0) == 0) break;
     float px = 0.f, py = 0.f, pz = 0.f;

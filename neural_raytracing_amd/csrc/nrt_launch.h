@@ -35,6 +35,8 @@ enum Option {
   OPT_MIXED_ZONE,      // "mixed_zone" (1e-7 units)
   OPT_BWD_COLSPLIT,    // "bwd_colsplit"
   OPT_BWD_RING,        // "bwd_ring"
+  OPT_MARCH_QUEUE,     // "march_queue"
+  OPT_TRAIN_SAVE,      // "train_save"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -226,7 +228,11 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
                      uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                      int32_t* cnt, unsigned long long* keys, char* mixed_ws, hipStream_t st);
 // workspace of ring_march: one 64-bit scan key per ray
-inline size_t ring_march_ws_bytes(int64_t P) { return ((size_t)P * 8 + 255) & ~(size_t)255; }
+// scan keys (P x u64) | the job-queue counter (MarchArgs::queue)
+inline size_t ring_march_ws_bytes(int64_t P) { return (((size_t)P * 8 + 255) & ~(size_t)255) + 256; }
+inline unsigned int* ring_march_queue(char* keys_base, int64_t P) {
+  return reinterpret_cast<unsigned int*>(keys_base + (((size_t)P * 8 + 255) & ~(size_t)255));
+}
 int ring_normals32(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
                    float* n, float* p_io, float eps, bool split, hipStream_t st);
 int ring_normals(const nrt_sdf* s, const int32_t* idx, const int32_t* cnt, int64_t M, float* grad,
@@ -249,6 +255,30 @@ int shade_program(const nrt_bsdf* b, const nrt_light* l, const float* p, const f
 // ---- FP32 / fp32-split shading on the row-program ring engines (nrt_shade_ring.hip) ----
 int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& out, int mode = 0);
 int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st);
+constexpr int kMaxSoloForward = 16;  // MLPs of one solo_forward_multi launch (rprog::kMaxSoloJobs)
+// save (nullable; else one buffer per MLP, saved_bytes each): the training forward, which also
+// stores the activations the ring backward reads (ring_backward with Ms >= 0)
+int solo_forward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                       float* const* y, hipStream_t st, void* const* save = nullptr);
+bool saved_forward_ok(const nrt_mlp* m);
+// one MLP's saved activations: A [L+1][M][H] | Eraw [M][dp] | Eact [M][dp], 256-byte aligned
+struct SavedActs {
+  float *A, *Eraw, *Eact;
+};
+inline size_t saved_part(size_t b) { return (b + 255) & ~(size_t)255; }
+inline size_t saved_bytes(const MlpDev& d, int64_t M) {
+  return saved_part((size_t)(d.n_hidden + 1) * M * d.hidden * 4) + 2 * saved_part((size_t)M * d.dp * 4);
+}
+inline SavedActs saved_split(const MlpDev& d, int64_t M, const void* base) {
+  char* p = (char*)base;
+  SavedActs s;
+  s.A = (float*)p;
+  p += saved_part((size_t)(d.n_hidden + 1) * M * d.hidden * 4);
+  s.Eraw = (float*)p;
+  p += saved_part((size_t)M * d.dp * 4);
+  s.Eact = (float*)p;
+  return s;
+}
 bool solo_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
                        void*& stream_dst, void*& bias_dst);
 int shade_ring(const nrt_bsdf* b, const nrt_light* l, const float* p, const float* n,
@@ -260,10 +290,16 @@ size_t ring_backward_table_bytes(int n);
 // true when every MLP has a ring-backward shape (and, refreshed, a refreshed backward program)
 bool ring_backward_ok(const nrt_mlp* const* mlps, int n);
 // per MLP k: dy[k] [M][out], dx[k] [M][3] or null, A[k] / dZ[k] [L+1][M][H], Eraw[k] / Eact[k]
-// [M][dp]; table: ring_backward_table_bytes(n) bytes of device memory
+// [M][dp]; table: ring_backward_table_bytes(n) bytes of device memory.  Ms >= 0: A[k] holds the
+// training forward's saved activations [L+1][Ms][H] and Sraw[k] / Sact[k] its encoding [Ms][dp]
+// (row i of this backward = saved row rows[i], or i when rows is null); only the backward chain
+// runs; with rows, the saved rows it reads are copied to Acopy[k] [L+1][M][H] and Eraw[k] /
+// Eact[k] [M][dp] (the weight gradients' operands, row-aligned with dZ).
 int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
                   const float* const* dy, float* const* dx, float* const* A, float* const* dZ,
-                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st);
+                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st,
+                  const int32_t* rows = nullptr, int64_t Ms = -1, float* const* Acopy = nullptr,
+                  const float* const* Sraw = nullptr, const float* const* Sact = nullptr);
 bool bwd_refresh_maps(const nrt_mlp* m, std::vector<int>& stream_map, std::vector<int>& bias_map,
                       void*& stream_dst, void*& bias_dst);
 

@@ -38,6 +38,7 @@ int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const Ma
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * kRingWaves)));
       // option "march_blocks": force the grid (tests check that results do not depend on the schedule)
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
+      if (a.queue) NRT_HIP(hipMemsetAsync(a.queue, 0, sizeof(unsigned int), st));
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
           s->host_dev, s->mlp->host_dev, rays, P, a, t, visible, nullptr, nullptr, nullptr, thr, keys);

@@ -33,6 +33,7 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
       const int64_t slots = (int64_t)std::max(per_cu, 1) * std::max(cus, 1);
       int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(slots, ceil_div64(P, 16 * WV)));
       if (const int64_t f = option(OPT_MARCH_BLOCKS)) blocks = (int)std::min<int64_t>(f, 1 << 20);
+      if (ma.queue) NRT_HIP(hipMemsetAsync(ma.queue, 0, sizeof(unsigned int), st));
       ProfScope prof(name, st);
       // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
       kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, nullptr,

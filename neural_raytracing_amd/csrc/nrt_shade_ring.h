@@ -104,8 +104,9 @@ struct Engine {
     issue(chunks[2 * ahead], chunks[2 * ahead + 1], s);
     ahead = ahead + 1 == nch ? 0 : ahead + 1;
   }
-  // block-wide; afterwards chunks 0 .. D - 2 are in flight
-  __device__ __forceinline__ void init(const RProgDev& p, char* lds) {
+  // block-wide; afterwards chunks 0 .. D - 2 are in flight.  chunk0: the program starts at that
+  // chunk of its table (the ring backward on saved activations skips the forward part)
+  __device__ __forceinline__ void init(const RProgDev& p, char* lds, int chunk0 = 0) {
     ring = reinterpret_cast<const float4*>(lds);
     ring_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds;
     float4* lq = reinterpret_cast<float4*>(lds + RING_BYTES);
@@ -120,8 +121,8 @@ struct Engine {
     changed = false;
     sbase = p.stream;
     sbytes = p.stream_bytes;
-    chunks = (const NRT_CONST int*)p.chunks;
-    nch = p.n_chunks;
+    chunks = (const NRT_CONST int*)p.chunks + 2 * chunk0;
+    nch = p.n_chunks - chunk0;
     lane = threadIdx.x & 63;
     wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     slot = 0;
@@ -235,6 +236,30 @@ __device__ __forceinline__ void enc_part32(En& E, const RProgMlp& m, const float
   }
 }
 
+// out layer (neural_blocks.py:86) on the last hidden activations dst (k-step order): one
+// sub-block, two chains over even / odd quads
+template <class S, class En>
+__device__ __forceinline__ f4v out32(En& E, const RProgMlp& m, const float (&dst)[S::H / 4]) {
+  constexpr int QH = S::QH;
+  const float4* A = E.begin();
+  f4v o0 = E.bias_at(m, m.L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
+  {
+    float4 w0 = A[0], w1 = A[64];
+#pragma unroll
+    for (int u = 0; u < QH; u += 2) {
+      float4 n0 = w0, n1 = w1;
+      if (u + 2 < QH) { n0 = A[(u + 2) * 64]; n1 = A[(u + 3) * 64]; }
+      o0 = ring32::mfma4(w0.x, dst[4 * u], o0); o1 = ring32::mfma4(w1.x, dst[4 * u + 4], o1);
+      o0 = ring32::mfma4(w0.y, dst[4 * u + 1], o0); o1 = ring32::mfma4(w1.y, dst[4 * u + 5], o1);
+      o0 = ring32::mfma4(w0.z, dst[4 * u + 2], o0); o1 = ring32::mfma4(w1.z, dst[4 * u + 6], o1);
+      o0 = ring32::mfma4(w0.w, dst[4 * u + 3], o0); o1 = ring32::mfma4(w1.w, dst[4 * u + 7], o1);
+      w0 = n0; w1 = n1;
+    }
+  }
+  E.end();
+  return o0 + o1;
+}
+
 // One SkipConnMLP evaluation for the wave's 16 rays; returns the out layer's 16x16 accumulator
 // (row 4 g + r of ray j in register r of lane 16 g + j).  Every wave of the block runs it.
 // Skip layers run their hidden part first (row-outer, raw accumulators kept), then the encoding
@@ -296,24 +321,7 @@ __device__ __forceinline__ f4v eval32(En& E, const RProgMlp& m, float x0, float 
       hidden(i, std::false_type{});
     }
   }
-  // out layer (neural_blocks.py:86): one sub-block, two chains over even / odd quads
-  const float4* A = E.begin();
-  f4v o0 = E.bias_at(m, L + 1, 0), o1 = f4v{0.f, 0.f, 0.f, 0.f};
-  {
-    float4 w0 = A[0], w1 = A[64];
-#pragma unroll
-    for (int u = 0; u < QH; u += 2) {
-      float4 n0 = w0, n1 = w1;
-      if (u + 2 < QH) { n0 = A[(u + 2) * 64]; n1 = A[(u + 3) * 64]; }
-      o0 = ring32::mfma4(w0.x, dst[4 * u], o0); o1 = ring32::mfma4(w1.x, dst[4 * u + 4], o1);
-      o0 = ring32::mfma4(w0.y, dst[4 * u + 1], o0); o1 = ring32::mfma4(w1.y, dst[4 * u + 5], o1);
-      o0 = ring32::mfma4(w0.z, dst[4 * u + 2], o0); o1 = ring32::mfma4(w1.z, dst[4 * u + 6], o1);
-      o0 = ring32::mfma4(w0.w, dst[4 * u + 3], o0); o1 = ring32::mfma4(w1.w, dst[4 * u + 7], o1);
-      w0 = n0; w1 = n1;
-    }
-  }
-  E.end();
-  return o0 + o1;
+  return out32<S>(E, m, dst);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -639,32 +647,26 @@ __global__ void __launch_bounds__(64 * WV, 1) k_bsdf_r(
   E.drain();
 }
 
-// nrt_mlp_forward of one MLP on its single-MLP row program: y [M, out] row-major
-template <int PREC, int D, int WV, class S>
-__global__ void __launch_bounds__(64 * WV, 1) k_mlp_ring(const RProgDev prog, const float* __restrict__ x,
-                                                        int64_t M, float* __restrict__ y, int out) {
-  extern __shared__ __attribute__((aligned(16))) char smem_c[];
-  const int64_t per_block = 16 * WV;
-  if ((int64_t)blockIdx.x * per_block >= M) return;
-  Engine<D, WV> E;
-  E.init(prog, smem_c);
-  const int lane = E.lane, j = lane & 15, g = lane >> 4;
-  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < M; b0 += (int64_t)gridDim.x * per_block) {
-    const int64_t i = b0 + 16 * E.wv + j;
-    const bool valid = i < M;
-    const int64_t ii = valid ? i : M - 1;
-    f4v o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], 0, x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
-    if constexpr (PREC == 2) {  // range guard (nrt_ring3.h)
-      while (E.retry(finite4(o)))
-        o = eval<PREC, S, ACT_LEAKY>(E, prog.mlp[0], 0, x[ii * 3], x[ii * 3 + 1], x[ii * 3 + 2]);
-    }
-    if (valid)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * g + r < out) y[i * out + 4 * g + r] = o[r];
-  }
-  E.drain();
-}
+// One MLP's single-MLP ("solo") row program and its output, a job of the forward kernel below.
+// The jobs travel as kernel arguments (no job-table copy): 16 x 88 B.
+struct SoloJob {
+  const void* stream;
+  const int* chunks;
+  const float* tables;
+  const float4* basis;
+  float* y;  // [M, out] row-major
+  // training forward (k_mlp_ring SAVE): the activations the ring backward reads (nrt_train_ring.h
+  // BwdRingJob): A [L+1][M][H], the encoding raw / activated [M][dp]
+  float *A, *Eraw, *Eact;
+  int stream_bytes, n_chunks, table_floats, basis_q, out;
+  RProgMlp mlp;
+};
+constexpr int kMaxSoloJobs = 16;
+struct SoloJobs {
+  SoloJob j[kMaxSoloJobs];
+};
+
+// (the forward kernel on SoloJobs, k_mlp_ring, is in nrt_train_ring.h beside its SAVE variant)
 
 }  // namespace rprog
 }  // namespace nrt

@@ -268,8 +268,10 @@ int build_rprog(const std::vector<const nrt_mlp*>& mlps, bool split, nrt_rprog& 
     const nrt_mlp_desc& md = m->desc;
     std::vector<float> lscale;
     if (int rc = walk_mlp(m, w, lscale, mode == 0)) return rc;
-    if (mode == 1)
+    if (mode == 1) {
+      out.fwd_chunks = (int)chunks.size() / 2;
       if (int rc = walk_mlp_bwd(m, w)) return rc;
+    }
     RProgMlp& pm = d.mlp[k];
     pm.L = md.num_layers; pm.skip = md.skip; pm.F = md.freqs; pm.out = md.out;
     pm.bstride = md.hidden;  // >= 16 rows of the out layer's sub-block
@@ -347,6 +349,31 @@ template <int PREC, int WV, class F>
 int with_depth(const RProgDev& d, F&& f) {
   if (rprog::Engine<3, WV>::lds_bytes(d) <= (size_t)kLdsBytes) return f(std::integral_constant<int, 3>{});
   if (rprog::Engine<2, WV>::lds_bytes(d) <= (size_t)kLdsBytes) return f(std::integral_constant<int, 2>{});
+  return NRT_EUNSUPPORTED;
+}
+
+int blocks_per_cu(const void* kern, int threads, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds) != hipSuccess) return 1;
+  return std::max(per_cu, 1);
+}
+
+// as with_depth, but 2 slots where that keeps more blocks resident on a CU (a kernel with few
+// registers: the 3-slot ring's LDS would hold the CU to one block); kern_of(depth) names the
+// kernel of each depth
+template <int WV, class KF, class F>
+int with_depth_occ(const RProgDev& d, KF&& kern_of, F&& f) {
+  using D3 = std::integral_constant<int, 3>;
+  using D2 = std::integral_constant<int, 2>;
+  const size_t l3 = rprog::Engine<3, WV>::lds_bytes(d), l2 = rprog::Engine<2, WV>::lds_bytes(d);
+  if (l3 <= (size_t)kLdsBytes) {
+    if (l2 <= (size_t)kLdsBytes &&
+        blocks_per_cu(reinterpret_cast<const void*>(kern_of(D2{})), 64 * WV, l2) >
+            blocks_per_cu(reinterpret_cast<const void*>(kern_of(D3{})), 64 * WV, l3))
+      return f(D2{});
+    return f(D3{});
+  }
+  if (l2 <= (size_t)kLdsBytes) return f(D2{});
   return NRT_EUNSUPPORTED;
 }
 }  // namespace
@@ -518,12 +545,18 @@ bool ring_backward_ok(const nrt_mlp* const* mlps, int n) {
 
 int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
                   const float* const* dy, float* const* dx, float* const* A, float* const* dZ,
-                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st) {
+                  float* const* Eraw, float* const* Eact, void* table, hipStream_t st,
+                  const int32_t* rows, int64_t Ms, float* const* Acopy, const float* const* Sraw,
+                  const float* const* Sact) {
   if (!ring_backward_ok(mlps, n)) return NRT_EUNSUPPORTED;
+  const bool saved = Ms >= 0;
   std::vector<rprog::BwdRingJob> jobs(n);
   for (int k = 0; k < n; ++k)
     jobs[k] = rprog::BwdRingJob{mlps[k]->bwd32.d, dy[k], dx ? dx[k] : nullptr, A[k], dZ[k],
-                                Eraw[k], Eact[k]};
+                                Eraw ? Eraw[k] : nullptr, Eact ? Eact[k] : nullptr, rows,
+                                saved ? Ms : M, mlps[k]->bwd32.fwd_chunks,
+                                Acopy ? Acopy[k] : nullptr, Sraw ? Sraw[k] : nullptr,
+                                Sact ? Sact[k] : nullptr};
   NRT_HIP(hipMemcpyAsync(table, jobs.data(), (size_t)n * sizeof(rprog::BwdRingJob),
                          hipMemcpyHostToDevice, st));
   const auto* tj = (const rprog::BwdRingJob*)table;
@@ -532,14 +565,19 @@ int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
   const RProgDev& d0 = mlps[0]->bwd32.d;  // the same shape: the same LDS plan for every MLP
   auto run = [&](auto sh) -> int {
     using S = decltype(sh);
-    return with_depth<0, WV>(d0, [&](auto dd) -> int {
-      constexpr int D = decltype(dd)::value;
-      auto kern = rprog::k_mlp_bwd_ring<D, WV, S>;
-      const size_t lds = rprog::Engine<D, WV>::lds_bytes(d0);
-      if (int r = set_lds(kern, lds)) return r;
-      kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want), n), dim3(64 * WV), lds, st>>>(tj, x, M);
-      return check_launch("k_mlp_bwd_ring");
-    });
+    auto go = [&](auto sv) -> int {
+      constexpr bool SV = decltype(sv)::value;
+      return with_depth_occ<WV>(d0, [](auto dd) { return rprog::k_mlp_bwd_ring<decltype(dd)::value, WV, S, SV>; },
+                                [&](auto dd) -> int {
+        constexpr int D = decltype(dd)::value;
+        auto kern = rprog::k_mlp_bwd_ring<D, WV, S, SV>;
+        const size_t lds = rprog::Engine<D, WV>::lds_bytes(d0);
+        if (int r = set_lds(kern, lds)) return r;
+        kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want), n), dim3(64 * WV), lds, st>>>(tj, x, M);
+        return check_launch("k_mlp_bwd_ring");
+      });
+    };
+    return saved ? go(std::true_type{}) : go(std::false_type{});
   };
   const int shape = solo_shape(mlps[0]);
   if (shape == 1) return run(rprog::LightShape{});
@@ -547,34 +585,64 @@ int ring_backward(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
   return run(rprog::BsdfShape{});
 }
 
-// NRT_EUNSUPPORTED when the MLP has no compiled ring shape (or a refreshed handle whose solo
-// program the refresh does not cover)
-int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st) {
-  const int shape = solo_shape(m);
+// NRT_EUNSUPPORTED when an MLP has no compiled ring shape, the MLPs' shapes differ, or a
+// refreshed handle's solo program is not covered by its refresh
+// the training forward can save activations for the ring backward (nrt_mlp_save_bytes > 0)
+bool saved_forward_ok(const nrt_mlp* m) {
+  if (option(OPT_SHADE_RING) == 0 || !solo_shape(m) || (m->refreshed && !m->solo_in_refresh)) return false;
+  return ring_backward_ok(&m, 1);
+}
+
+static_assert(kMaxSoloForward == rprog::kMaxSoloJobs, "solo job table size");
+int solo_forward_multi(const nrt_mlp* const* mlps, int n, const float* x, int64_t M,
+                       float* const* y, hipStream_t st, void* const* save) {
+  if (n < 1 || n > rprog::kMaxSoloJobs) return NRT_EUNSUPPORTED;
+  const int shape = solo_shape(mlps[0]);
   if (!shape) return NRT_EUNSUPPORTED;
-  nrt_rprog& sp = m->solo32;
-  if (m->refreshed && !m->solo_in_refresh) return NRT_EUNSUPPORTED;
-  if (!sp.built)
-    if (int rc = build_rprog({m}, false, sp)) return rc;
-  if (!sp.ok) return NRT_EUNSUPPORTED;
+  if (save && !ring_backward_ok(mlps, n)) return NRT_EUNSUPPORTED;
+  rprog::SoloJobs jobs{};
+  for (int k = 0; k < n; ++k) {
+    const nrt_mlp* m = mlps[k];
+    if (solo_shape(m) != shape || m->desc.out != mlps[0]->desc.out) return NRT_EUNSUPPORTED;
+    nrt_rprog& sp = m->solo32;
+    if (m->refreshed && !m->solo_in_refresh) return NRT_EUNSUPPORTED;
+    if (!sp.built)
+      if (int rc = build_rprog({m}, false, sp)) return rc;
+    if (!sp.ok) return NRT_EUNSUPPORTED;
+    const RProgDev& d = sp.d;
+    SavedActs sa{nullptr, nullptr, nullptr};
+    if (save) sa = saved_split(m->host_dev, M, save[k]);
+    jobs.j[k] = rprog::SoloJob{d.stream, d.chunks, d.tables, d.basis, y[k], sa.A, sa.Eraw, sa.Eact,
+                               d.stream_bytes, d.n_chunks, d.table_floats, d.basis_q, m->desc.out,
+                               d.mlp[0]};
+  }
   constexpr int WV = kRWaves;
   const int64_t want = ceil_div64(M, 16 * WV);
-  const int out = m->desc.out;
+  const RProgDev& d0 = mlps[0]->solo32.d;  // one shape: one LDS plan
   auto run = [&](auto sh) -> int {
     using S = decltype(sh);
-    return with_depth<0, WV>(sp.d, [&](auto dd) -> int {
-      constexpr int D = decltype(dd)::value;
-      auto kern = rprog::k_mlp_ring<0, D, WV, S>;
-      const size_t lds = rprog::Engine<D, WV>::lds_bytes(sp.d);
-      if (int r = set_lds(kern, lds)) return r;
-      ProfScope prof("k_mlp_ring32", st);
-      kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want)), dim3(64 * WV), lds, st>>>(sp.d, x, M, y, out);
-      return check_launch("k_mlp_ring32");
-    });
+    auto go = [&](auto sv) -> int {
+      constexpr bool SV = decltype(sv)::value;
+      return with_depth_occ<WV>(d0, [](auto dd) { return rprog::k_mlp_ring<decltype(dd)::value, WV, S, SV>; },
+                                [&](auto dd) -> int {
+        constexpr int D = decltype(dd)::value;
+        auto kern = rprog::k_mlp_ring<D, WV, S, SV>;
+        const size_t lds = rprog::Engine<D, WV>::lds_bytes(d0);
+        if (int r = set_lds(kern, lds)) return r;
+        ProfScope prof("k_mlp_ring32", st);
+        kern<<<dim3(persistent_grid(kern, 64 * WV, lds, want), n), dim3(64 * WV), lds, st>>>(jobs, x, M);
+        return check_launch("k_mlp_ring32");
+      });
+    };
+    return save ? go(std::true_type{}) : go(std::false_type{});
   };
   if (shape == 1) return run(rprog::LightShape{});
   if (shape == 2) return run(rprog::SpatialShape{});
   return run(rprog::BsdfShape{});
+}
+
+int solo_forward(const nrt_mlp* m, const float* x, int64_t M, float* y, hipStream_t st) {
+  return solo_forward_multi(&m, 1, x, M, &y, st);
 }
 
 }  // namespace nrt

@@ -32,16 +32,17 @@ namespace rprog {
 __device__ __forceinline__ float dleaky(float a) { return a > 0.f ? 1.f : 0.01f; }
 
 // The forward pass of one tile with its activations saved: eval32 (nrt_shade_ring.h) without the
-// out layer; save_a(layer, sb, f4v) receives every hidden layer's activations per sub-block,
-// save_e(slot, raw, act) every encoding slot this lane computes (once per tile).
+// out layer (dst: the last hidden layer's activations, out32's input); save_a(layer, sb, f4v)
+// receives every hidden layer's activations per sub-block, save_e(slot, raw, act) every encoding
+// slot this lane computes (once per tile).  Same arithmetic as eval32.
 template <class S, class En, class SaveA, class SaveE>
 __device__ __forceinline__ void fwd32_save(En& E, const RProgMlp& m, float x0, float x1, float x2,
-                                           SaveA&& save_a, SaveE&& save_e) {
+                                           float (&dst)[S::H / 4], SaveA&& save_a, SaveE&& save_e) {
   constexpr int NSB = S::NSB, NC = S::NC, QH = S::QH, KH = S::H / 4;
   const float4* basis = E.lbasis + m.basis_off;
   const int L = m.L, SK = m.skip;
   const int g = E.lane >> 4;
-  float src[KH], dst[KH];
+  float src[KH];
   f4v acc[NSB];
   // k-outer encoding part (enc_part32 with the encoding stored on the first pass)
   auto enc_part = [&](bool actv, bool store) {
@@ -277,10 +278,20 @@ struct BwdRingJob {
   RProgDev prog;
   const float* dY;   // [M][out]
   float* dX;         // [M][3] or null
-  float* A;          // [L+1][M][H] activations of the hidden layers
+  float* A;          // [L+1][M][H] activations of the hidden layers (SAVED: [L+1][Ms][H], read)
   float* dZ;         // [L+1][M][H] their gradients
   float* Eraw;       // [M][dp] the encoding, reference columns [x, sin, cos]
   float* Eact;       // [M][dp] leaky_relu of it (the skip layers' input)
+  // SAVED (the training forward stored A and the encoding, nrt_mlp_forward_multi with save
+  // buffers): row i of this backward is saved row rows[i] (nullptr: i) of Ms; the program starts
+  // after its forward part.  With rows, the saved rows read are copied compactly: A -> Acopy,
+  // Sraw / Sact (the saved encoding) -> Eraw / Eact (nothing written without rows).
+  const int32_t* rows;
+  int64_t Ms;
+  int fwd_chunks;
+  float* Acopy;
+  const float* Sraw;
+  const float* Sact;
 };
 
 // slot (the ring's encoding order: sin / cos pairs, then x) -> reference column (utils.py:37-40)
@@ -290,8 +301,73 @@ __device__ __forceinline__ int slot_column(int s, int F) {
   return -1;
 }
 
-// blockIdx.y = MLP (the mixture's NeuralBSDFs share x); a persistent grid over 16-row tiles
-template <int D, int WV, class S>
+// nrt_mlp_forward(_multi) at FP32: block (x, y) evaluates row tiles of MLP y on its solo program
+// (same-shape MLPs on one input -- the NeuralBSDF components of a spatial mixture, bsdfs.py:
+// 634-637 -- in one launch: n times the blocks, so a 38,400-row batch fills the CUs).  SAVE: the
+// training forward, which also stores what the ring backward reads (SoloJob A / Eraw / Eact), so
+// the backward does not evaluate the forward again.
+template <int D, int WV, class S, bool SAVE>
+__global__ void __launch_bounds__(64 * WV, 1) k_mlp_ring(const SoloJobs jobs, const float* __restrict__ x,
+                                                        int64_t M) {
+  extern __shared__ __attribute__((aligned(16))) char smem_c[];
+  const int64_t per_block = 16 * WV;
+  if ((int64_t)blockIdx.x * per_block >= M) return;
+  const SoloJob& jb = jobs.j[blockIdx.y];
+  RProgDev pd;
+  pd.stream = jb.stream;
+  pd.stream_bytes = jb.stream_bytes;
+  pd.chunks = jb.chunks;
+  pd.n_chunks = jb.n_chunks;
+  pd.tables = jb.tables;
+  pd.table_floats = jb.table_floats;
+  pd.basis = jb.basis;
+  pd.basis_q = jb.basis_q;
+  pd.n_mlp = 1;
+  Engine<D, WV> E;
+  E.init(pd, smem_c);
+  const RProgMlp m = jb.mlp;
+  const int out = jb.out, F = m.F, dp = 3 + 2 * F;
+  float* __restrict__ y = jb.y;
+  const int lane = E.lane, j = lane & 15, g = lane >> 4;
+  constexpr int H = S::H;
+  for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < M; b0 += (int64_t)gridDim.x * per_block) {
+    const int64_t i = b0 + 16 * E.wv + j;
+    const bool valid = i < M;
+    const int64_t ii = valid ? i : M - 1;
+    const float x0 = x[ii * 3], x1 = x[ii * 3 + 1], x2 = x[ii * 3 + 2];
+    f4v o;
+    if constexpr (SAVE) {
+      float last[H / 4];
+      const size_t lay = (size_t)M * H;
+      fwd32_save<S>(E, m, x0, x1, x2, last,
+                    [&](int layer, int sb, const f4v& a) {
+                      if (valid)
+                        *reinterpret_cast<float4*>(jb.A + (size_t)layer * lay + (size_t)ii * H + 16 * sb + 4 * g) =
+                            make_float4(a[0], a[1], a[2], a[3]);
+                    },
+                    [&](int slot, float raw, float act) {
+                      const int c = slot_column(slot, F);
+                      if (valid && c >= 0) {
+                        jb.Eraw[ii * dp + c] = raw;
+                        jb.Eact[ii * dp + c] = act;
+                      }
+                    });
+      o = out32<S>(E, m, last);
+    } else {
+      o = eval<0, S, ACT_LEAKY>(E, m, 0, x0, x1, x2);
+    }
+    if (valid)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < out) y[i * out + 4 * g + r] = o[r];
+  }
+  E.drain();
+}
+
+// blockIdx.y = MLP (the mixture's NeuralBSDFs share x); a persistent grid over 16-row tiles.
+// SAVED: the activations come from the training forward (BwdRingJob rows / Ms) and the tile runs
+// the backward chain only.
+template <int D, int WV, class S, bool SAVED>
 __global__ void __launch_bounds__(64 * WV, 1) k_mlp_bwd_ring(const BwdRingJob* __restrict__ jobs,
                                                             const float* __restrict__ x, int64_t M) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
@@ -299,40 +375,57 @@ __global__ void __launch_bounds__(64 * WV, 1) k_mlp_bwd_ring(const BwdRingJob* _
   const int64_t per_block = 16 * WV;
   if ((int64_t)blockIdx.x * per_block >= M) return;
   Engine<D, WV> E;
-  E.init(jb.prog, smem_c);
+  E.init(jb.prog, smem_c, SAVED ? jb.fwd_chunks : 0);
   const RProgMlp& m = jb.prog.mlp[0];
   const int lane = E.lane, j = lane & 15, g = lane >> 4;
   const int out = m.out, F = m.F, dp = 3 + 2 * F;
   constexpr int H = S::H;
   float* const Ag = jb.A;
   float* const dZg = jb.dZ;
+  const size_t lay = (size_t)M * H;
+  const size_t alay = SAVED ? (size_t)jb.Ms * H : lay;  // A's layer stride
   for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < M; b0 += (int64_t)gridDim.x * per_block) {
     const int64_t i = b0 + 16 * E.wv + j;
     const bool valid = i < M;
     const int64_t ii = valid ? i : M - 1;
     const float x0 = x[ii * 3], x1 = x[ii * 3 + 1], x2 = x[ii * 3 + 2];
-    const size_t lay = (size_t)M * H;
+    const int64_t ia = SAVED && jb.rows ? (int64_t)jb.rows[ii] : ii;  // A's row
+    const bool copy = SAVED && jb.rows != nullptr && valid;
+    if (copy) {  // the saved encoding row -> its compact row (4 lanes a row)
+      for (int c = g; c < dp; c += 4) {
+        jb.Eraw[ii * dp + c] = jb.Sraw[ia * dp + c];
+        jb.Eact[ii * dp + c] = jb.Sact[ia * dp + c];
+      }
+    }
     auto at = [&](float* base, int layer, int sb) -> float* {
       return base + (size_t)layer * lay + (size_t)ii * H + 16 * sb + 4 * g;
     };
-    fwd32_save<S>(E, m, x0, x1, x2,
-                  [&](int layer, int sb, const f4v& a) {
-                    if (valid) *reinterpret_cast<float4*>(at(Ag, layer, sb)) = make_float4(a[0], a[1], a[2], a[3]);
-                  },
-                  [&](int slot, float raw, float act) {
-                    const int c = slot_column(slot, F);
-                    if (valid && c >= 0) {
-                      jb.Eraw[ii * dp + c] = raw;
-                      jb.Eact[ii * dp + c] = act;
-                    }
-                  });
+    auto at_a = [&](int layer, int sb) -> float* {
+      return Ag + (size_t)layer * alay + (size_t)ia * H + 16 * sb + 4 * g;
+    };
+    if constexpr (!SAVED) {
+      float last[H / 4];
+      fwd32_save<S>(E, m, x0, x1, x2, last,
+                    [&](int layer, int sb, const f4v& a) {
+                      if (valid) *reinterpret_cast<float4*>(at_a(layer, sb)) = make_float4(a[0], a[1], a[2], a[3]);
+                    },
+                    [&](int slot, float raw, float act) {
+                      const int c = slot_column(slot, F);
+                      if (valid && c >= 0) {
+                        jb.Eraw[ii * dp + c] = raw;
+                        jb.Eact[ii * dp + c] = act;
+                      }
+                    });
+    }
     float dy[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) dy[s] = 4 * g + s < out ? jb.dY[ii * out + 4 * g + s] : 0.f;
     float dx[3];
     bwd32<S>(E, m, x0, x1, x2, dy,
              [&](int layer, int sb) -> f4v {
-               const float4 v = *reinterpret_cast<const float4*>(at(Ag, layer, sb));
+               const float4 v = *reinterpret_cast<const float4*>(at_a(layer, sb));
+               // every (layer, sub-block) of the tile is read exactly once: its compact copy
+               if (copy) *reinterpret_cast<float4*>(at(jb.Acopy, layer, sb)) = v;
                return f4v{v.x, v.y, v.z, v.w};
              },
              [&](int layer, int sb, const f4v& z) {

@@ -118,6 +118,28 @@ def _mlp_forward(mlp, x, lat, handle=None):
     return y
 
 
+def _forward_saving(handles, x, outs):
+    """ys[k] = mlp_k(x) for same-shape MLPs (no latent) in one nrt_mlp_forward_multi call.  Under
+    FP32 (and the mixed march's FP32 MLPs) with a ring-backward shape (nrt_mlp_save_bytes > 0) the
+    forward also saves the activations its backward reads -> (ys, save buffers) -- else
+    (ys, None) and the backward evaluates the forward again."""
+    import ctypes
+    lib = _lib.load(require_device=True)
+    n, M = len(handles), x.shape[0]
+    ys = [torch.empty(M, o, device=x.device) for o in outs]
+    P = ctypes.c_void_p
+    hs = (P * n)(*[h.value for h in handles])
+    save = None
+    if M > 0 and _lib.precision_code() != _lib.NRT_FP16:
+        nbytes = [lib.nrt_mlp_save_bytes(h.value, M) for h in handles]
+        if all(nbytes):
+            save = [torch.empty(b, dtype=torch.uint8, device=x.device) for b in nbytes]
+    _lib.call("nrt_mlp_forward_multi", hs, n, _lib.ptr(x), M, (P * n)(*[y.data_ptr() for y in ys]),
+              None if save is None else (P * n)(*[b.data_ptr() for b in save]),
+              _lib.precision_code(), _lib.stream())
+    return ys, save
+
+
 def _save_versions(ctx, params):
     """The backward kernels read the packed copy of the weights (the training handle, re-packed in
     place by nrt_mlp_refresh after an optimiser step), not saved tensors, so autograd's own
@@ -159,8 +181,13 @@ class _MlpFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mlp, x, lat, *params):
         handle = train_handle(mlp)  # device re-pack after an optimiser step
+        ctx.save = None
         with torch.no_grad():
-            y = _mlp_forward(mlp, x.detach(), None if lat is None else lat.detach(), handle)
+            if lat is None:
+                ys, ctx.save = _forward_saving([handle], x.detach(), [mlp.out.out_features])
+                y = ys[0]
+            else:
+                y = _mlp_forward(mlp, x.detach(), lat.detach(), handle)
         ctx.mlp = mlp
         ctx.handle = handle  # the packed weights this forward used
         _save_versions(ctx, params)
@@ -202,7 +229,16 @@ class _MlpFn(torch.autograd.Function):
         dbs = [mk(lin.bias) if lin.bias.requires_grad else None for lin in lins]
         wp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dws])
         bp = (ctypes.c_void_p * len(lins))(*[0 if t is None else t.data_ptr() for t in dbs])
-        if not zeros:
+        if not zeros and ctx.save is not None:  # the forward saved the activations
+            P = ctypes.c_void_p
+            ws = torch.empty(lib.nrt_mlp_backward_multi_workspace_bytes((P * 1)(ctx.handle.value), 1, M),
+                             dtype=torch.uint8, device=x.device)
+            rows = None if idx is None else idx.to(torch.int32)
+            _lib.call("nrt_mlp_backward_saved", (P * 1)(ctx.handle.value), 1, _lib.ptr(x), M,
+                      _lib.ptr(rows), (P * 1)(ctx.save[0].data_ptr()), full_x.shape[0] if idx is not None else M,
+                      (P * 1)(dy.data_ptr()), None if dx is None else (P * 1)(dx.data_ptr()),
+                      wp, bp, _lib.ptr(ws), _lib.stream())
+        elif not zeros:
             ws = torch.empty(lib.nrt_mlp_backward_workspace_bytes(ctx.handle.value, M),
                              dtype=torch.uint8, device=x.device)
             _lib.call("nrt_mlp_backward", ctx.handle.value, _lib.ptr(x), _lib.ptr(lat), M,
@@ -297,9 +333,10 @@ class _MultiMlpFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, mlps, x, *params):
+        import ctypes
         handles = [train_handle(m) for m in mlps]
         with torch.no_grad():
-            ys = [_mlp_forward(m, x.detach(), None, h) for m, h in zip(mlps, handles)]
+            ys, ctx.save = _forward_saving(handles, x.detach(), [m.out.out_features for m in mlps])
         ctx.mlps = mlps
         ctx.handles = handles
         _save_versions(ctx, params)
@@ -342,8 +379,15 @@ class _MultiMlpFn(torch.autograd.Function):
         if not zeros:
             ws = torch.empty(lib.nrt_mlp_backward_multi_workspace_bytes(hs, n, M),
                              dtype=torch.uint8, device=x.device)
-            _lib.call("nrt_mlp_backward_multi", hs, n, _lib.ptr(x), M, dyp, dxp, wp, bp,
-                      _lib.ptr(ws), _lib.stream())
+            if ctx.save is not None:  # the forward saved the activations
+                rows = None if idx is None else idx.to(torch.int32)
+                Ms = full_x.shape[0] if idx is not None else M
+                _lib.call("nrt_mlp_backward_saved", hs, n, _lib.ptr(x), M, _lib.ptr(rows),
+                          (P * n)(*[b.data_ptr() for b in ctx.save]), Ms, dyp, dxp, wp, bp,
+                          _lib.ptr(ws), _lib.stream())
+            else:
+                _lib.call("nrt_mlp_backward_multi", hs, n, _lib.ptr(x), M, dyp, dxp, wp, bp,
+                          _lib.ptr(ws), _lib.stream())
         dxs = None if dx is None else (dx.sum(0) if not zeros else torch.zeros_like(x))
         if idx is not None and dxs is not None:
             dxs = torch.zeros_like(full_x).index_copy_(0, idx, dxs)

@@ -518,9 +518,12 @@ def test_ring_march_schedule_invariant(monkeypatch):
     outs = []
     # (blocks, xcd_lines): the default grid with both ray deals, and grids of 1, 5, 13 blocks
     # (fewer XCD groups than XCDs, a group with one block more than another)
-    for blocks, xcd in ((0, 1), (0, 0), (1, 1), (5, 1), (13, 1), (5, 0)):
+    # and the launch-wide job queue (option march_queue) at the default grid and at 5 blocks
+    for blocks, xcd, q in ((0, 1, 0), (0, 0, 0), (1, 1, 0), (5, 1, 0), (13, 1, 0), (5, 0, 0),
+                           (0, 0, 1), (5, 0, 1)):
         _lib_opt("march_blocks", blocks)
         _lib_opt("xcd_lines", xcd)
+        _lib_opt("march_queue", q)
         random.seed(2)
         with torch.no_grad():
             it, hit = SDF(sdf=mine, max_steps=64).intersect(rays, primary=True)

@@ -167,9 +167,33 @@ def test_ring32_independent_of_grid_size():
     _, mine = _blob(128, 128, 32, "softplus", seed=9)
     rays = _rays(24, 11, eye=(0.0, 0.2, 1.1))
     base, bh, _ = _march(mine, rays)
-    for blocks, xcd in ((1, 1), (5, 1), (13, 1), (0, 0), (5, 0)):
+    # (blocks, xcd_lines, march_queue): the launch-wide queue too (every scan segmented, jobs
+    # taken 16 at a time in launch order, so lanes, waves and blocks differ from the lists')
+    for blocks, xcd, q in ((1, 1, 0), (5, 1, 0), (13, 1, 0), (0, 0, 0), (5, 0, 0), (0, 0, 1),
+                           (1, 0, 1), (13, 0, 1)):
         _lib_opt("march_blocks", blocks)
         _lib_opt("xcd_lines", xcd)
+        _lib_opt("march_queue", q)
+        it, h, _ = _march(mine, rays)
+        assert torch.equal(h, bh)
+        assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)
+        assert torch.equal(it.p, base.p) and torch.equal(it.n, base.n)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp32-split", "mixed"])
+def test_march_queue_matches_job_lists(prec):
+    """Option march_queue (one launch-wide job queue) on the FP16, split and NRT_MIXED marches
+    (k_march16, k_march3, the mixed flagging march + k_refine3 + k_best3): bit-identical t, hit,
+    p, n and throughput to the per-wave job lists, at the default grid and at 3 blocks."""
+    from neural_raytracing_amd import set_precision
+    _, mine = _blob(128, 128, 32, "softplus", seed=9)
+    rays = _rays(24, 11, eye=(0.0, 0.2, 1.1))
+    set_precision(prec)
+    base, bh, _ = _march(mine, rays)
+    assert bh.any() and not bh.all()
+    for blocks in (0, 3):
+        _lib_opt("march_blocks", blocks)
+        _lib_opt("march_queue", 1)
         it, h, _ = _march(mine, rays)
         assert torch.equal(h, bh)
         assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)

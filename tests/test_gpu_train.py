@@ -434,3 +434,116 @@ def test_ring_backward_multi_matches_single(M):
     for a, b in zip(grads(True), grads(False)):
         scale = b.abs().max().clamp_min(1e-6)
         assert float((a - b).abs().max() / scale) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,n,M", [("neural_bsdf_6x96_F64", 3, 1), ("neural_bsdf_6x96_F64", 8, 4100),
+                                      ("neural_bsdf_6x96_F64", 17, 300), ("light_field_10x256", 2, 129),
+                                      ("8x64_leaky", 3, 500)])
+def test_mlp_forward_multi_equals_single(name, n, M):
+    """nrt_mlp_forward_multi (one launch for same-shape MLPs on the ring engine, blockIdx.y = MLP;
+    more than 16 MLPs in launches of 16; other shapes as per-MLP calls) equals nrt_mlp_forward of
+    each MLP bit for bit, and the per-MLP forwards match the float64 oracle at the FP32 bar."""
+    import ctypes
+    from neural_raytracing_amd import _lib, set_precision
+    from neural_raytracing_amd.pathtracer._handles import mlp_handle
+    set_precision("fp32")
+    kw = SHAPES[name]
+    pairs = [_pair(kw, 200 + s) for s in range(n)]
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, kw["in_size"], generator=g) - 0.5)
+    xc = x.cuda().contiguous()
+    hs = [mlp_handle(m) for _, m in pairs]
+    single = []
+    for h, (_, m) in zip(hs, pairs):
+        y = torch.empty(M, kw["out"], device="cuda")
+        _lib.call("nrt_mlp_forward", h.value, _lib.ptr(xc), None, M, _lib.ptr(y),
+                  _lib.precision_code(), _lib.stream())
+        single.append(y)
+    multi = [torch.full((M, kw["out"]), float("nan"), device="cuda") for _ in range(n)]
+    P = ctypes.c_void_p
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    _lib.call("nrt_mlp_forward_multi", (P * n)(*[h.value for h in hs]), n, _lib.ptr(xc), M,
+              (P * n)(*[y.data_ptr() for y in multi]), None, _lib.precision_code(), _lib.stream())
+    torch.cuda.synchronize()
+    launches = _lib.profile_read("k_mlp_ring32")[1]
+    _lib.profile_enable(False)
+    if name != "8x64_leaky":
+        assert launches == (n + 15) // 16
+    for a, b in zip(multi, single):
+        assert torch.equal(a, b)
+    import copy
+    for (ref, _), y in zip(pairs[:2], single[:2]):
+        m64 = copy.deepcopy(ref).double()
+        m64.basis_p = ref.basis_p.double()
+        with torch.no_grad():
+            want = m64(x.double(), None)
+        assert (y.cpu().double() - want).abs().max().item() <= 1e-4 * max(1.0, want.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dead", [0.0, 0.5])
+@pytest.mark.parametrize("name", RING_SHAPES)
+def test_saved_activation_backward_equals_recompute(name, dead):
+    """The training forward saves the activations (nrt_mlp_forward_multi with save buffers,
+    nrt_mlp_save_bytes > 0) and nrt_mlp_backward_saved runs the backward chain on them: y and every
+    gradient bit-equal to the ring backward that evaluates the forward again (option train_save
+    0), with and without row compaction (dead: the fraction of rows whose dL/dy is 0, so the
+    saved backward reads saved rows through the live-row index)."""
+    from neural_raytracing_amd import _lib, set_precision
+    set_precision("fp32")
+    kw = SHAPES[name]
+    _, mine = _pair(kw, 31)
+    M = 3001
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(M, 3, generator=g) - 0.5).cuda()
+    dy = torch.randn(M, kw["out"], generator=g)
+    dy[torch.rand(M, generator=g) < dead] = 0.0
+    dy = dy.cuda()
+
+    def run(save):
+        with _lib.options(train_save=save):
+            mine.zero_grad(set_to_none=True)
+            xm = x.clone().requires_grad_(True)
+            y = mine(xm)
+            (y * dy).sum().backward()
+            return [y.detach().clone(), xm.grad.clone()] + [q.grad.clone() for q in mine.parameters()
+                                                            if q.grad is not None]
+    _lib.profile_enable(True)
+    _lib.profile_reset()
+    a = run(1)
+    saved_launches = _lib.profile_read("k_mlp_backward32")[1]
+    _lib.profile_enable(False)
+    b = run(0)
+    assert saved_launches == 1
+    assert len(a) == len(b) > 3
+    for u, v in zip(a, b):
+        assert torch.equal(u, v), (u - v).abs().max().item()
+
+
+@pytest.mark.gpu
+def test_saved_activation_multi_backward_equals_recompute():
+    """The mixture's NeuralBSDFs through mlp_multi: one saving forward launch for all of them,
+    one saved backward; every gradient bit-equal to the recomputing ring backward."""
+    from neural_raytracing_amd import _lib, set_precision
+    from neural_raytracing_amd.pathtracer.neural_blocks import mlp_multi
+    set_precision("fp32")
+    kw = SHAPES["neural_bsdf_6x96_F64"]
+    mlps = [_pair(kw, seed)[1] for seed in (4, 5, 6)]
+    M = 2500
+    g = torch.Generator().manual_seed(9)
+    x = (torch.rand(M, 3, generator=g) * 2 - 1).cuda()
+    dys = [torch.randn(M, 3, generator=g) for _ in mlps]
+    dead = torch.rand(M, generator=g) < 0.4
+    dys = [d.masked_fill(dead[:, None], 0.0).cuda() for d in dys]
+    params = [q for m in mlps for q in m.parameters()]
+
+    def grads(save):
+        with _lib.options(train_save=save):
+            xx = x.clone().requires_grad_(True)
+            ys = mlp_multi(mlps, xx)
+            loss = sum((y * dy).sum() for y, dy in zip(ys, dys))
+            return [y.detach() for y in ys] + list(torch.autograd.grad(loss, [xx] + params))
+    for u, v in zip(grads(1), grads(0)):
+        assert torch.equal(u, v), (u - v).abs().max().item()
