@@ -536,6 +536,13 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      the transposed weights streamed through a block-shared LDS ring, dZ kept in
  *                      registers between layers); 0: the bwd_colsplit kernels.  Same gradients to
  *                      FP32 rounding (different summation order), both held to float64 autograd
+ *   "wgrad_tile"     0  1: weight gradients (every backward) on k_wgrad_tile -- 128 x 128 output
+ *                      tiles of four waves, the batch rows staged through LDS (operands read twice
+ *                      per layer), each layer's bias summed from the staged dZ -- instead of
+ *                      k_wgrad_batch (64 x 64 tiles fed by direct loads); measured 10 % slower on
+ *                      the training step (1.06 vs 0.96 ms a launch: MFMA busy 0.36 vs 0.51, 32 % of
+ *                      wave time parked at the stage barriers).  Deterministic either way; the two
+ *                      differ by the split-K slice count (FP32 summation order)
  *   "train_save"     1  nrt_mlp_save_bytes > 0 for the ring backward's shapes (the training
  *                      forward saves its activations, nrt_mlp_backward_saved skips the forward
  *                      evaluation); 0: nrt_mlp_save_bytes returns 0 (the backward recomputes)

@@ -963,9 +963,6 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
 // dZ^T) and In[m + h][c0 + 32b + i] (B), 128-byte row segments per half-wave -- then the waves'
 // accumulators are summed in wave order through LDS and the slice partials in slice order
 // (deterministic).  S is chosen from the shapes alone (same inputs, same bits).
-#ifndef NRT_WGRAD_TILE
-#define NRT_WGRAD_V1 1
-#endif
 constexpr int kSplitMax = 64;
 constexpr int64_t kSliceRows = 256;  // batch rows per slice at least
 constexpr int kWgradWaves = 4;        // waves per block
@@ -984,6 +981,9 @@ struct WgradJob {
   int64_t M, slice_rows, part_off, out0;
   int R, C, ldi, ldw, c0, tiles_c, n_tiles, block0;
   int bias;  // 1: db = the column sums of dZ (In unused)
+  // k_wgrad_tile: this weight job's c0 = 0 tiles also sum dZ's rows below bias_M into the partials
+  // at bias_off (a bias job's, which then has no blocks of its own); -1: none
+  int64_t bias_off, bias_M;
 };
 
 template <int = 0>
@@ -1083,30 +1083,32 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
     }
 }
 
-// ---- LDS-staged weight gradients (NRT_WGRAD_TILE builds it in place of k_wgrad_batch) --------
-// Measured slower than k_wgrad_batch on the training step's batches (7.0 vs 3.3 ms a step): one
-// 8-wave block per CU leaves ~1 wave per SIMD once the slices are dealt (29 weight tiles x 6
-// slices for the spatial MLP's 47 jobs), the 96-row NeuralBSDF tiles fill 37 % of a 256 x 256
-// tile, and the bias jobs' column sums are latency chains.  Kept for the next attempt (smaller
-// tiles, more blocks).
-// k_wgrad_batch fed each MFMA from 4-byte global loads in the MFMA's lane order (round-4 PMC:
-// 65-75 % of wave time waiting at ~0.5 MFMA busy) and, with 64 x 64 tiles, read a 256 x 256
-// layer's dZ and In slices four times each.  Here one block of 8 waves computes a whole 256 x 256
-// output tile over its slice of the batch -- a layer's operands are read once per slice (64 FLOP
-// per byte) -- and the rows stream through three LDS stages of 16 rows ([16][256 + 1] floats of
-// dZ and of In: coalesced 1 KiB row segments, loaded two stages ahead into registers so ~8k cycles
-// of MFMA cover each load).  Wave (wr, wc) takes rows 128 wr .., columns 64 wc .. of the tile as
-// 4 x 2 v_mfma_f32_32x32x2_f32 accumulators with operands read from LDS.  Exact f32, each output's
-// products in row order within the slice (deterministic).  A bias job (the product against a
-// column of ones) is a column sum of dZ on the VALU.
-constexpr int kWgT = 256;   // tile side
+// ---- LDS-staged weight gradients (option "wgrad_tile"; measured 10 % slower than k_wgrad_batch
+// on the training step: MFMA busy 0.36 vs 0.51, 32 % of wave time parked at the stage barriers,
+// 1.85 waves per SIMD; profiles/r05/probe/pmc_wgrad_stall.txt) ----------------------------------
+// k_wgrad_batch feeds each MFMA from 4-byte global loads in the MFMA's lane order and, with 64 x 64
+// tiles, reads a 256-wide layer's dZ and In slices four times each (16 FLOP per byte fetched;
+// round-4 PMC: 65-75 % of wave time waiting at ~0.5 MFMA busy).  Here a block of four waves
+// computes a 128 x 128 output tile over its slice of the batch -- operands read twice per layer,
+// 32 FLOP per byte -- with the rows streaming through three LDS stages of 16 rows ([16][128 + 1]
+// floats of dZ and of In: coalesced 512-byte row segments, loaded two stages ahead into registers
+// so ~4k cycles of MFMA cover each load).  Wave (wr, wc) takes rows 64 wr .., columns 64 wc .. of
+// the tile as 2 x 2 v_mfma_f32_32x32x2_f32 accumulators with operands read from LDS.  Exact f32,
+// each output's products in row order within the slice (deterministic).  The bias gradient of a
+// layer (dZ's column sums) rides on the layer's first weight tiles (c0 = 0): the staged dZ rows are
+// summed from LDS (bias_off / bias_M); a bias job with no such weight job (the double backward's
+// biases over the primal half of the stacked rows) is a column sum of its own (wave-parallel).
+// A round-5 256 x 256 / 8-wave version of this kernel ran at one wave per SIMD on these batches and
+// with the biases as per-thread load chains: 2x slower than k_wgrad_batch.
+constexpr int kWgT = 128;   // tile side
 constexpr int kWgKS = 16;   // rows per LDS stage
 constexpr int kWgNS = 3;    // stages
 constexpr int kWgLd = kWgT + 1;
+constexpr int kWgThreads = 256;  // four waves, 2 x 2 of 64 x 64
 
 template <int = 0>
-__global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restrict__ jobs, int n_jobs,
-                                                       int S, float* __restrict__ part) {
+__global__ void __launch_bounds__(kWgThreads, 3) k_wgrad_tile(const WgradJob* __restrict__ jobs, int n_jobs,
+                                                              int S, float* __restrict__ part) {
   typedef float f16v_ __attribute__((ext_vector_type(16)));
   extern __shared__ float wsm[];  // [kWgNS][2][kWgKS][kWgLd]
   int j = 0;
@@ -1120,30 +1122,43 @@ __global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restric
   const int64_t m0 = (int64_t)slice * jb.slice_rows;
   const int64_t m1 = std::min<int64_t>(jb.M, m0 + jb.slice_rows);
   const int t = threadIdx.x;
+  const int w = t >> 6, lane = t & 63, i = lane & 31, h = lane >> 5;
   float* out = part + jb.part_off + (size_t)slice * R * C;
-  if (jb.bias) {  // bias: column sums over the slice, in row order
-    for (int r = t; r < R; r += 512) {
-      float acc = 0.f;
-      int64_t m = m0;
-      for (; m + 8 <= m1; m += 8) {  // eight loads in flight, added in row order
-        float v[8];
+  if (jb.bias) {  // a bias job of its own: column sums over the slice, wave w takes rows w, w + 4 ..
+    constexpr int NW = kWgThreads / 64;
+    __shared__ float red[NW - 1][256];
+    for (int cb = 0; cb < R; cb += 256) {  // columns cb + lane + 64 q
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int64_t m = m0 + w; m < m1; m += NW) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = dZ[(m + k) * R + r];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) acc += v[k];
+        for (int q = 0; q < 4; ++q)
+          if (cb + lane + 64 * q < R) acc[q] += dZ[m * R + cb + lane + 64 * q];
       }
-      for (; m < m1; ++m) acc += dZ[m * R + r];
-      out[r] = acc;
+      if (w > 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w - 1][lane + 64 * q] = acc[q];
+      __syncthreads();
+      if (w == 0)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float v = acc[q];
+#pragma unroll
+          for (int k = 0; k < NW - 1; ++k) v += red[k][lane + 64 * q];
+          if (cb + lane + 64 * q < R) out[cb + lane + 64 * q] = v;
+        }
+      __syncthreads();
     }
     return;
   }
   const int r0 = (tile / jb.tiles_c) * kWgT, c0 = (tile % jb.tiles_c) * kWgT;
-  const int w = t >> 6, lane = t & 63, i = lane & 31, h = lane >> 5;
-  const int wr = w >> 2, wc = w & 3;
-  // this wave's row blocks / column blocks that hold any output (the rest of its tile is padding)
-  const bool live = r0 + 128 * wr < R && c0 + 64 * wc < C;
-  // staging: thread t loads column (t & 255) of rows (t >> 8) + 2 k, k < 8, of both operands
-  const int lc = t & 255, lr = t >> 8;
+  const int wr = w >> 1, wc = w & 1;
+  // this wave's rows / columns hold any output (the rest of its tile is padding)
+  const bool live = r0 + 64 * wr < R && c0 + 64 * wc < C;
+  // the layer's bias rides on its c0 = 0 tiles: threads t < kWgT sum column r0 + t of the staged dZ
+  const bool bias_here = jb.bias_off >= 0 && c0 == 0;
+  float bsum = 0.f;
+  // staging: thread t loads column (t & 127) of rows (t >> 7) + 2 k, k < 8, of both operands
+  const int lc = t & (kWgT - 1), lr = t >> 7;
   const bool rok = r0 + lc < R, cok = c0 + lc < C;
   // through global-address-space pointers: flat loads would also count in lgkmcnt, so every LDS
   // read's wait would drain the staging loads in flight
@@ -1171,7 +1186,7 @@ __global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restric
       sB(st, lr + 2 * k, lc) = ok && cok ? ia[q][k] : 0.f;
     }
   };
-  f16v_ acc[4][2] = {};
+  f16v_ acc[2][2] = {};
   const int64_t nst = (m1 - m0 + kWgKS - 1) / kWgKS;  // stages of the slice
   // prologue: stage 0 into LDS, stage 1 into registers
   if (nst > 0) { load(0, m0); stash(0, 0, m0); }
@@ -1182,26 +1197,30 @@ __global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restric
   auto body = [&](int64_t s, auto qc) {
     constexpr int Q = decltype(qc)::value;
     const int st = (int)(s % kWgNS);
-    // stage s + 1 waits in set Q ^ 1; stage s + 2 goes into set Q (its stage s is in LDS since
-    // the last barrier)
-    // unconditional (rows past the slice load as zeros): a load under a branch makes the
-    // compiler's wait-count analysis drain every load at the stash below
+    // stage s + 2 into set Q (unconditional: rows past the slice load clamped and stash as zeros;
+    // a load under a branch makes the compiler's wait-count analysis drain every load early)
     load(Q, m0 + (s + 2) * kWgKS);
     if (live) {
 #pragma unroll
       for (int ks = 0; ks < kWgKS / 2; ++ks) {
         const int row = 2 * ks + h;
-        float a[4], bv[2];
+        float a[2], bv[2];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) a[x] = sA(st, row, 128 * wr + 32 * x + i);
+        for (int x = 0; x < 2; ++x) a[x] = sA(st, row, 64 * wr + 32 * x + i);
 #pragma unroll
         for (int y = 0; y < 2; ++y) bv[y] = sB(st, row, 64 * wc + 32 * y + i);
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
           for (int y = 0; y < 2; ++y)
             acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], bv[y], acc[x][y], 0, 0, 0);
       }
+    }
+    if (bias_here && t < kWgT) {  // the stage's dZ rows below bias_M, in row order
+      const int64_t ms = m0 + s * kWgKS;
+#pragma unroll
+      for (int row = 0; row < kWgKS; ++row)
+        if (ms + row < jb.bias_M) bsum += sA(st, row, t);
     }
     // stage s + 1 (registers) into its slot: the slot of stage s - 2, read two barriers ago
     stash(Q ^ 1, (int)((s + 1) % kWgNS), m0 + (s + 1) * kWgKS);
@@ -1211,18 +1230,19 @@ __global__ void __launch_bounds__(512, 2) k_wgrad_tile(const WgradJob* __restric
     body(s, std::integral_constant<int, 0>{});
     if (s + 1 < nst) body(s + 1, std::integral_constant<int, 1>{});
   }
+  if (bias_here && t < kWgT && r0 + t < R) part[jb.bias_off + (size_t)slice * R + r0 + t] = bsum;
   if (!live) return;
-  // accumulator (x, y) register q: row 128 wr + 32 x + (q & 3) + 8 (q >> 2) + 4 h, column
+  // accumulator (x, y) register q: row 64 wr + 32 x + (q & 3) + 8 (q >> 2) + 4 h, column
   // 64 wc + 32 y + i of the tile
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) {
       const int cc = c0 + 64 * wc + 32 * y + i;
       if (cc >= C) continue;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int rr = r0 + 128 * wr + 32 * x + (q & 3) + 8 * (q >> 2) + 4 * h;
+        const int rr = r0 + 64 * wr + 32 * x + (q & 3) + 8 * (q >> 2) + 4 * h;
         if (rr < R) out[(size_t)rr * C + cc] = acc[x][y][q];
       }
     }
@@ -1254,11 +1274,7 @@ static_assert(kMaxWgradJobs * sizeof(WgradJob) <= kWgradTableBytes, "job table")
 // the slice count of a batch: about 3 blocks (12 waves, the kernel's occupancy) per CU over all
 // the batch's tiles, at least kSliceRows rows per slice
 int batch_slices(int64_t total_tiles, int64_t M) {
-#ifdef NRT_WGRAD_V1
   int64_t S = std::max<int64_t>(1, (256 * 3 + total_tiles - 1) / total_tiles);
-#else
-  int64_t S = std::max<int64_t>(1, (256 + total_tiles - 1) / total_tiles);  // a block per CU
-#endif
   S = std::min<int64_t>(S, kSplitMax);
   S = std::max<int64_t>(1, std::min<int64_t>(S, (M + kSliceRows - 1) / kSliceRows));
   return (int)S;
@@ -1282,18 +1298,34 @@ struct WgradBatch {
     j.bias = 1;
     jobs.push_back(j);
   }
+  // which kernel: k_wgrad_tile (option "wgrad_tile", default) or k_wgrad_batch
+  bool tile = option(OPT_WGRAD_TILE) != 0;
   // lay out tiles, slices and partial offsets; returns the partial floats needed
   size_t plan(int& S) {
     int64_t tiles = 0, Mmax = 1;
-    for (auto& j : jobs) {
-#ifdef NRT_WGRAD_V1
-      j.tiles_c = (j.C + 63) / 64;
-      j.n_tiles = ((j.R + 63) / 64) * j.tiles_c;
-#else
-      // k_wgrad_tile: 128 x 128 tiles; a bias job is one block per slice
-      j.tiles_c = j.bias ? 1 : (j.C + kWgT - 1) / kWgT;
-      j.n_tiles = j.bias ? 1 : ((j.R + kWgT - 1) / kWgT) * j.tiles_c;
-#endif
+    std::vector<int> link(jobs.size(), -1);  // bias job -> the weight job that sums it
+    for (size_t b = 0; tile && b < jobs.size(); ++b) {
+      if (!jobs[b].bias) continue;
+      for (size_t w = 0; w < jobs.size(); ++w) {
+        const WgradJob& q = jobs[w];
+        if (!q.bias && q.dZ == jobs[b].dZ && q.R == jobs[b].R && q.M >= jobs[b].M) { link[b] = (int)w; break; }
+      }
+    }
+    for (size_t k = 0; k < jobs.size(); ++k) {
+      WgradJob& j = jobs[k];
+      j.bias_off = -1;
+      j.bias_M = 0;
+      if (!tile) {
+        j.tiles_c = (j.C + 63) / 64;
+        j.n_tiles = ((j.R + 63) / 64) * j.tiles_c;
+      } else if (j.bias) {
+        // summed by its weight job's tiles, or one column-sum block per slice
+        j.tiles_c = 1;
+        j.n_tiles = link[k] >= 0 ? 0 : 1;
+      } else {
+        j.tiles_c = (j.C + kWgT - 1) / kWgT;
+        j.n_tiles = ((j.R + kWgT - 1) / kWgT) * j.tiles_c;
+      }
       tiles += j.n_tiles;
       Mmax = std::max(Mmax, j.M);
     }
@@ -1309,6 +1341,13 @@ struct WgradBatch {
       j.out0 = out;
       out += (int64_t)j.R * j.C;
     }
+    for (size_t b = 0; b < jobs.size(); ++b)
+      if (link[b] >= 0) {
+        // the weight job's slices (its slice_rows) carry the sums; rows past the bias job's M
+        // (the stacked tangent half of the double backward) are not summed
+        jobs[link[b]].bias_off = jobs[b].part_off;
+        jobs[link[b]].bias_M = jobs[b].M;
+      }
     return off;
   }
   // table: kMaxWgradJobs * sizeof(WgradJob) bytes of device memory; part: the plan's floats
@@ -1326,14 +1365,14 @@ struct WgradBatch {
     for (auto& j : jobs) flop += 2.0 * j.R * j.C * (double)j.M;
     {
       ProfScope prof("k_wgrad", st, flop);
-#ifdef NRT_WGRAD_V1
-      k_wgrad_batch<><<<dim3((unsigned)blocks), dim3(64 * kWgradWaves), 0, st>>>(tj, (int)jobs.size(), S, part);
-      if (int rc = check_launch("k_wgrad_batch")) return rc;
-#else
-      if (int rc = set_lds(k_wgrad_tile<>, kWgLdsBytes)) return rc;
-      k_wgrad_tile<><<<dim3((unsigned)blocks), dim3(512), kWgLdsBytes, st>>>(tj, (int)jobs.size(), S, part);
-      if (int rc = check_launch("k_wgrad_tile")) return rc;
-#endif
+      if (!tile) {
+        k_wgrad_batch<><<<dim3((unsigned)blocks), dim3(64 * kWgradWaves), 0, st>>>(tj, (int)jobs.size(), S, part);
+        if (int rc = check_launch("k_wgrad_batch")) return rc;
+      } else if (blocks > 0) {
+        if (int rc = set_lds(k_wgrad_tile<>, kWgLdsBytes)) return rc;
+        k_wgrad_tile<><<<dim3((unsigned)blocks), dim3(kWgThreads), kWgLdsBytes, st>>>(tj, (int)jobs.size(), S, part);
+        if (int rc = check_launch("k_wgrad_tile")) return rc;
+      }
     }
     k_split_reduce_batch<><<<dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st>>>(
         tj, (int)jobs.size(), S, total, part);
@@ -1669,10 +1708,6 @@ int nrt_mlp_backward_saved(const nrt_mlp* const* mlps, int n, const float* x, in
   }
   const MlpDev& d = mlps[0]->host_dev;
   if (M > INT32_MAX || Ms > INT32_MAX) { set_error("nrt_mlp_backward_saved: at most 2^31-1 rows per call"); return NRT_EINVAL; }
-#ifdef NRT_WGRAD_TILE
-  set_error("nrt_mlp_backward_saved: not with the NRT_WGRAD_TILE weight-gradient kernel");
-  return NRT_EUNSUPPORTED;
-#endif
   if (!ring_backward_ok(mlps, n)) {
     set_error("nrt_mlp_backward_saved: no ring backward for these MLPs (nrt_mlp_save_bytes is 0)");
     return NRT_EUNSUPPORTED;

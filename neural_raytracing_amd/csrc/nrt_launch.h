@@ -37,6 +37,7 @@ enum Option {
   OPT_BWD_RING,        // "bwd_ring"
   OPT_MARCH_QUEUE,     // "march_queue"
   OPT_TRAIN_SAVE,      // "train_save"
+  OPT_WGRAD_TILE,      // "wgrad_tile"
   OPT_COUNT
 };
 int64_t option(Option o);

@@ -92,6 +92,41 @@ def test_mlp_backward_matches_autograd(name, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_weight_gradients_batch_kernel_matches_autograd(name):
+    """The weight gradients on k_wgrad_batch (option wgrad_tile 0: 64 x 64 tiles fed by direct
+    loads, separate bias column sums) as well as on the default k_wgrad_tile (128 x 128 tiles
+    staged through LDS, biases summed on the first weight tiles): both at the float64 bar, and
+    within FP32 summation-order noise of each other."""
+    from neural_raytracing_amd import _lib, set_precision
+    kw = SHAPES[name]
+    M = 2000
+    ref, mine = _pair(kw, 140)
+    set_precision("fp32")
+    g = torch.Generator().manual_seed(M)
+    x = (torch.rand(M, kw["in_size"], generator=g) - 0.5)
+    lat = torch.randn(M, kw["latent_size"], generator=g) if kw.get("latent_size") else None
+    dy = torch.randn(M, kw["out"], generator=g)
+    want = _grads(ref, x, lat, dy, torch.float64)
+    ref32 = _grads(ref, x, lat, dy, torch.float32)
+
+    def run(tile):
+        with _lib.options(wgrad_tile=tile):
+            mine.zero_grad(set_to_none=True)
+            xm = x.cuda().requires_grad_(True)
+            lm = lat.cuda() if lat is not None else None
+            (mine(xm, lm) * dy.cuda()).sum().backward()
+            return {**{f"dW[{i}]": a.weight.grad.clone() for i, a in enumerate(mine._linears())},
+                    **{f"db[{i}]": a.bias.grad.clone() for i, a in enumerate(mine._linears())}}
+    a, b = run(0), run(1)
+    for k in a:
+        _close(a[k], want[k], ref32[k], "batch " + k)
+        _close(b[k], want[k], ref32[k], "tile " + k)
+        scale = a[k].abs().max().clamp_min(1e-6)
+        assert float((a[k] - b[k]).abs().max() / scale) < 1e-4, k
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dead", [0.6, 1.0])
 @pytest.mark.parametrize("name", ["sp_var_16x256_F128", "latent_4x32", "neural_bsdf_6x96_F64"])
 def test_mlp_backward_compacts_zero_gradient_rows(name, dead):
