@@ -1043,7 +1043,7 @@ def train_torch_profile(step, path):
             f.write(f"{n:6d}  {site}\n")
 
 
-def cpu_train_baseline(sdf, bsdf, lights, size, focal, samples, crop=112):
+def cpu_train_baseline(sdf, bsdf, lights, size, focal, samples, crop=176):
     """The oracle (torch-CPU restatement, 'port') running the same training step -- forward,
     create_graph normals, loss = MSE + eikonal, backward -- on one view's crop x crop window, on
     this host's threads; rate in training ray-samples/s like the GPU line."""

@@ -595,8 +595,12 @@ __device__ __forceinline__ void march_body(
   const int64_t R = dyn ? Pe : own.R;  // rays of this wave's list
   const bool scan = mode == 0 && a.primary;
   // scan jobs: the whole 129-point scan of each of the first R - T rays (one plain key store),
-  // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail
-  const int64_t T = (dyn || kScanSplit < 0) ? R : (R < kScanSplit ? R : (int64_t)kScanSplit);
+  // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail; the
+  // launch-wide queue segments the last 16 rays per wave of the grid (every ray segmented took
+  // HBM traffic per 800^2 launch from 178 to 325 MB: 8 key atomics per ray)
+  const int64_t tq = 16 * nw;
+  const int64_t T = dyn ? (R < tq ? R : tq)
+                        : (kScanSplit < 0 ? R : (R < kScanSplit ? R : (int64_t)kScanSplit));
   // sdf(best) with a runner-up key: a second job per ray re-evaluates the runner-up where the
   // FP16 scan could not order the two (skipped elsewhere)
   const bool alt = MX && mode == 1 && a.keys2 != nullptr;

@@ -8,8 +8,8 @@ import pathlib
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 # the round's final line (bench.py with the CPU baseline) and the rocprofv3 --kernel-trace --stats
 # summary of the same frame (bench.py --no-cpu-baseline --no-extra-legs)
-BENCH = ROOT / "profiles" / "r04" / "final" / "bench.json"
-STATS = ROOT / "profiles" / "r04" / "final" / "kernel_stats.csv"
+BENCH = ROOT / "profiles" / "r05" / "final" / "bench.json"
+STATS = ROOT / "profiles" / "r05" / "final" / "kernel_stats.csv"
 PEAK = {"fp32": 157.3, "fp16": 2500.0, "fp32-split": 2500.0, "mixed": 2500.0}
 
 REQUIRED = ["metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
