@@ -392,6 +392,16 @@ int nrt_raygen(const nrt_camera* host_cams, int32_t N, int32_t x0, int32_t y0, i
 int nrt_sphere_intersect(const float* center, double radius, const float* rays, int64_t P,
                          float* t, uint8_t* hit, float* p, float* n, float* upper,
                          int32_t* hit_idx, int32_t* hit_count, void* stream);
+/* SphereCloud (shapes/shapes.py:99-206): the nearest hit over N spheres per ray.  spheres:
+ * device [N][4] floats (centre x, y, z, radius).  split_n, t_max: intersect's arguments (the
+ * chunk of spheres per pass; a root counts when in [1e-8, t_max), the best distance starts at
+ * t_max).  Outputs as nrt_sphere_intersect's (NULL = skip; hit is intersect_test's answer).  The
+ * reference's own broadcasting is well-formed for one sphere, where the results are its bit for
+ * bit; more spheres follow the same per-ray statements (the nearest sphere's index within its
+ * chunk of split_n names the normal's centre, as the reference keeps it). */
+int nrt_sphere_cloud_intersect(const float* spheres, int64_t N, int64_t split_n, double t_max,
+                               const float* rays, int64_t P, float* t, uint8_t* hit, float* p,
+                               float* n, int32_t* hit_idx, int32_t* hit_count, void* stream);
 int nrt_frames(const float* rays, const float* n, int64_t P, float* frame, float* wi,
                void* stream);
 

@@ -92,6 +92,8 @@ _SIGNATURES = {
     "nrt_light_create_renderer_point": (_I32, [_P, _P, _F, ctypes.POINTER(_P)]),
     "nrt_light_destroy": (_I32, [_P]),
     "nrt_sphere_intersect": (_I32, [_P, ctypes.c_double, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "nrt_sphere_cloud_intersect": (_I32, [_P, _I64, _I64, ctypes.c_double, _P, _I64, _P, _P, _P, _P,
+                                          _P, _P, _P]),
     "nrt_bsdf_create": (_I32, [_I32, _P, _P, ctypes.POINTER(_P)]),
     "nrt_bsdf_destroy": (_I32, [_P]),
     "nrt_shade_direct": (_I32, [_P, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _I32, _P]),

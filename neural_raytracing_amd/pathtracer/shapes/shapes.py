@@ -98,19 +98,63 @@ class Sphere(Shape):
 
 
 class SphereCloud(Shape):
-    """shapes.py:99-200 (unused by the drivers, off the hot path): import-resolvable only."""
+    """SphereCloud (shapes.py:99-206): the nearest of N analytic spheres per ray on the HIP kernel
+    ``nrt_sphere_cloud_intersect`` (one thread per ray over the sphere table; quad_solve per
+    sphere in the reference's float32 op order, split_n spheres per pass as the reference's
+    chunks).  The reference's tensor broadcasting is well-formed for one sphere only; there the
+    results are its own bit for bit, and more spheres follow the same per-ray statements."""
 
     def __init__(self, centers=[[0, 0, 0]], radii=1, device="cuda"):
         self.device = torch.device(device)
-        self.centers = torch.tensor(centers, dtype=torch.float, device=self.device).reshape(-1, 3)
-        self.radii = torch.full([self.centers.shape[0]], radii, dtype=torch.float,
-                                device=self.device)
+        N = len(centers)
+        self.centers = torch.zeros([N, 3], dtype=torch.float, device=self.device)
+        for i in range(N):
+            self.centers[i] = torch.tensor(centers[i], device=device)
+        self.radii = torch.full([N], radii, dtype=torch.float, device=self.device)
 
     def __len__(self):
         return 1
 
+    def _table(self, dev):
+        return torch.cat([self.centers.detach().float(), self.radii.detach().float()[:, None]],
+                         dim=-1).to(dev).contiguous()
+
+    def _run(self, rays, t_max, split_n, want_p=True, want_list=True):
+        if rays.device.type != "cuda":
+            raise _lib.NrtError("SphereCloud runs on the HIP path: rays must be on the GPU")
+        lead = rays.shape[:-1]
+        flat = rays.reshape(-1, 6).float().contiguous()
+        P = flat.shape[0]
+        dev = flat.device
+        table = self._table(dev)
+        t = torch.empty(P, device=dev)
+        hit = torch.empty(P, dtype=torch.uint8, device=dev)
+        p = torch.empty(P, 3, device=dev) if want_p else None
+        n = torch.empty(P, 3, device=dev) if want_p else None
+        hit_idx = torch.empty(max(P, 1), dtype=torch.int32, device=dev) if want_list else None
+        hit_count = torch.zeros(1, dtype=torch.int32, device=dev) if want_list else None
+        _lib.load(require_device=True)
+        _lib.call("nrt_sphere_cloud_intersect", _lib.ptr(table), table.shape[0], int(split_n),
+                  float(t_max), _lib.ptr(flat), P, _lib.ptr(t), _lib.ptr(hit), _lib.ptr(p),
+                  _lib.ptr(n), _lib.ptr(hit_idx), _lib.ptr(hit_count), _lib.stream())
+        return lead, flat, P, t, hit.bool().reshape(lead), p, n, hit_idx, hit_count
+
     def intersect(self, rays, active=True, t_max=math.inf, split_n=256):
-        raise _lib.NrtError("SphereCloud has no HIP implementation (no driver uses it)")
+        """shapes.py:111-179: SurfaceInteraction(p, t, n, frame, wi = to_local(-d)), hit mask."""
+        lead, flat, P, t, hit, p, n, hit_idx, hit_count = self._run(rays, t_max, split_n)
+        si = HipInteraction(p=p.reshape(lead + (3,)), t=t.reshape(lead), obj=self)
+        si.n = n.reshape(lead + (3,))
+        frame = torch.empty(P, 9, device=flat.device)
+        wi = torch.empty(P, 3, device=flat.device)
+        if P:
+            _lib.call("nrt_frames", _lib.ptr(flat), _lib.ptr(n), P, _lib.ptr(frame), _lib.ptr(wi),
+                      _lib.stream())
+        si.frame = frame.reshape(lead + (3, 3))
+        si.wi = wi.reshape(lead + (3,))
+        si._nrt_hits = (hit_idx, hit_count, flat)
+        si._nrt_hit_mask = hit
+        return si, hit
 
     def intersect_test(self, rays, active=True, t_max=math.inf, split_n=256):
-        raise _lib.NrtError("SphereCloud has no HIP implementation (no driver uses it)")
+        """shapes.py:180-206: the hit mask alone."""
+        return self._run(rays, t_max, split_n, want_p=False, want_list=False)[4]

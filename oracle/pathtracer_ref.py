@@ -304,6 +304,82 @@ class SphereRef:
         return ts.min(dim=-1)[0], ts.max(dim=-1)[0], mask
 
 
+class SphereCloudRef:
+    """SphereCloud, shapes.py:99-206, statement by statement -- including its broadcasting, which
+    is well-formed for one sphere only: intersect's `sphere_exp ... .transpose(0, 1)` (:131-132)
+    pairs every sphere with every row of rays unless N = 1 and the rays' first dim is 1, and
+    intersect_test's `(radii * radii)[..., None]` (:196) aligns [N, 1] with the rays' last two
+    dims.  The parity tests run it where it is well-formed; the HIP kernel states the per-ray
+    nearest-hit semantics those cases pin (test_gpu_sphere.py)."""
+
+    def __init__(self, centers=((0.0, 0.0, 0.0),), radii=1.0):
+        N = len(centers)
+        self.centers = torch.zeros([N, 3], dtype=torch.float)
+        for i in range(N):
+            self.centers[i] = torch.tensor(list(centers[i]), dtype=torch.float)
+        self.radii = torch.full([N], radii, dtype=torch.float)
+
+    def __len__(self):
+        return 1
+
+    def intersect(self, rays, active=True, t_max=math.inf, split_n=256):
+        """shapes.py:111-179."""
+        r_o, r_d = torch.split(rays, 3, dim=-1)
+        out_active = torch.zeros(r_o.shape[:-1], dtype=torch.bool)
+        best_dists = torch.full_like(out_active, t_max, dtype=torch.float)
+        best_faces = torch.full_like(out_active, -1, dtype=torch.long)
+        r_o_r = r_o.expand(split_n, *r_o.shape)
+        r_d_r = r_d.expand_as(r_o_r)
+        for spheres, radii in zip(self.centers.split(split_n, dim=0), self.radii.split(split_n, dim=0)):
+            batch_size = spheres.shape[0]
+            r_o_r, r_d_r = r_o_r[:batch_size], r_d_r[:batch_size]
+            sphere_exp = spheres[:, None, None, None].repeat(1, *r_d_r.shape[1:-1], 1).transpose(0, 1)
+            radii_exp = radii[:, None, None, None].repeat(1, *r_d_r.shape[1:-1]).transpose(0, 1)
+            fs = r_o_r - sphere_exp
+            a = torch.sum(r_d_r * r_d_r, dim=-1)
+            b = 2 * torch.sum(r_d_r * fs, dim=-1)
+            c = torch.sum(fs * fs, dim=-1) - (radii_exp * radii_exp)
+            intersections, mask = quad_solve(a, b, c)
+            mask = mask & ((intersections >= SPHERE_EPS) & (intersections < t_max)).any(-1)
+            intersections[intersections < SPHERE_EPS] = math.inf
+            valid_mins = mask.any(0)
+            out_active = out_active | valid_mins
+            t, _ = intersections.min(dim=-1)
+            t[~mask] = math.inf
+            min_t, sph_idx = t.min(dim=0)
+            lesser = best_dists > min_t
+            replace_cond = valid_mins & lesser
+            best_dists[replace_cond] = min_t[replace_cond]
+            best_faces[replace_cond] = sph_idx[replace_cond]
+        p = r_o + best_dists[..., None] * r_d
+        n = torch.zeros_like(p, dtype=torch.float)
+        n[out_active] = F.normalize(p[out_active] - self.centers[best_faces[out_active]], dim=-1)
+        p += n * 1e-5
+        it = Interaction(p=p, t=best_dists)
+        it.set_normals(n)
+        it.wi = it.to_local(-r_d)
+        return it, out_active
+
+    def intersect_test(self, rays, active=True, t_max=math.inf, split_n=256):
+        """shapes.py:180-206."""
+        r_o, r_d = torch.split(rays, 3, dim=-1)
+        out_active = torch.zeros(r_o.shape[:-1], dtype=torch.bool)
+        r_o_r = r_o.expand(split_n, *r_o.shape)
+        r_d_r = r_d.expand_as(r_o_r)
+        for spheres, radii in zip(self.centers.split(split_n, dim=0), self.radii.split(split_n, dim=0)):
+            batch_size = spheres.shape[0]
+            r_o_r, r_d_r = r_o_r[:batch_size], r_d_r[:batch_size]
+            sphere_exp = spheres[:, None, None, None].repeat(1, *r_d_r.shape[1:-1], 1)
+            fs = r_o_r - sphere_exp
+            a = torch.sum(r_d_r * r_d_r, dim=-1)
+            b = 2 * torch.sum(r_d_r * fs, dim=-1)
+            c = torch.sum(fs * fs, dim=-1) - (radii * radii)[..., None]
+            intersections, mask = quad_solve(a, b, c)
+            mask = mask & ((intersections >= SPHERE_EPS) & (intersections < t_max)).any(-1)
+            out_active = out_active | mask.any(0)
+        return out_active
+
+
 # ---------------------------------------------------------------------------------------------
 # Interaction frames  (interaction.py:9-119)
 # ---------------------------------------------------------------------------------------------

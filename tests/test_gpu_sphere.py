@@ -71,6 +71,115 @@ def test_sphere_empty_batch():
     assert mask.numel() == 0 and it.p.shape == (0, 3)
 
 
+def _cloud_rays(n, seed, lead=1):
+    g = torch.Generator().manual_seed(seed)
+    o = torch.tensor([0.0, 0.1, 2.5]) + 0.3 * torch.randn(lead, n, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(lead, n, 1, 2, generator=g) * 1.2 - 0.6,
+                               -torch.ones(lead, n, 1, 1)], -1), dim=-1)
+    return torch.cat([o, d], -1)
+
+
+@pytest.mark.parametrize("t_max", [math.inf, 2.3])
+@pytest.mark.parametrize("n", [1, 300, 4000])
+def test_sphere_cloud_one_sphere_matches_oracle(n, t_max):
+    """SphereCloud (shapes.py:99-206) where the reference's broadcasting is well-formed: one
+    sphere, rays [1, n, 1, 6] for intersect and [3, n, 1, 6] for intersect_test; t, p, n, wi of
+    the hits at the Sphere test's bar, the hit masks and the misses' t (t_max) equal."""
+    from neural_raytracing_amd.pathtracer.shapes import SphereCloud
+    centers, radius = [[0.05, 0.1, 0.2]], 0.6
+    ref = R.SphereCloudRef(centers=centers, radii=radius)
+    mine = SphereCloud(centers=centers, radii=radius, device="cuda")
+    rays = _cloud_rays(n, n)
+    want, wmask = ref.intersect(rays, t_max=t_max)
+    got, mask = mine.intersect(rays.cuda(), t_max=t_max)
+    assert torch.equal(mask.cpu(), wmask)
+    if n > 10:
+        assert 0.1 < wmask.float().mean() < 0.9
+    h = wmask
+    for name, a, b in (("t", got.t.cpu(), want.t), ("p", got.p.cpu(), want.p),
+                       ("n", got.n.cpu(), want.n), ("wi", got.wi.cpu(), want.wi)):
+        err = (a[h] - b[h]).abs().max().item() if h.any() else 0.0
+        report(f"sphere_cloud[{n},{t_max}].{name}", rays=n, hits=int(h.sum()), maxabs=err)
+        assert err <= 1e-6, (name, err)
+    assert torch.equal(got.t.cpu()[~h], want.t[~h])
+    assert torch.equal(got.n.cpu()[~h], want.n[~h])
+    rays3 = _cloud_rays(n, n + 1, lead=3)
+    assert torch.equal(mine.intersect_test(rays3.cuda(), t_max=t_max).cpu(),
+                       ref.intersect_test(rays3, t_max=t_max))
+    idx, cnt, _ = got._nrt_hits
+    listed = torch.zeros(n, dtype=torch.bool)
+    listed[idx[: int(cnt.item())].long().cpu()] = True
+    assert torch.equal(listed, wmask.reshape(-1))
+
+
+def _cloud_restated(centers, radii, rays, t_max, split_n):
+    """SphereCloud.intersect's per-ray statements (shapes.py:111-179) for N spheres, sphere by
+    sphere on the CPU in float32 (the reference's own broadcasting is well-formed for N = 1 only):
+    per chunk the first minimum's index within the chunk names the normal's centre."""
+    r_o, r_d = torch.split(rays, 3, dim=-1)
+    lead = r_o.shape[:-1]
+    out_active = torch.zeros(lead, dtype=torch.bool)
+    best = torch.full(lead, t_max, dtype=torch.float)
+    face = torch.full(lead, -1, dtype=torch.long)
+    for j0 in range(0, centers.shape[0], split_n):
+        ts = []
+        for j in range(j0, min(j0 + split_n, centers.shape[0])):
+            fs = r_o - centers[j]
+            a = torch.sum(r_d * r_d, dim=-1)
+            b = 2 * torch.sum(r_d * fs, dim=-1)
+            c = torch.sum(fs * fs, dim=-1) - radii[j] * radii[j]
+            inter, mask = R.quad_solve(a, b, c)
+            mask = mask & ((inter >= R.SPHERE_EPS) & (inter < t_max)).any(-1)
+            inter[inter < R.SPHERE_EPS] = math.inf
+            t, _ = inter.min(dim=-1)
+            t[~mask] = math.inf
+            ts.append((t, mask))
+        t = torch.stack([q[0] for q in ts])
+        valid = torch.stack([q[1] for q in ts]).any(0)
+        out_active |= valid
+        min_t, idx = t.min(dim=0)
+        rep = valid & (best > min_t)
+        best[rep] = min_t[rep]
+        face[rep] = idx[rep]
+    p = r_o + best[..., None] * r_d
+    n = torch.zeros_like(p)
+    n[out_active] = F.normalize(p[out_active] - centers[face[out_active]], dim=-1)
+    return best, p + n * 1e-5, n, out_active
+
+
+@pytest.mark.parametrize("split_n", [256, 7])
+def test_sphere_cloud_many_spheres_matches_restatement(split_n):
+    """37 spheres (the reference's broadcasting breaks past one sphere, so the per-ray statements
+    are restated sphere by sphere): nearest hit, chunks of split_n (7: six chunks, the normal's
+    centre named by the index within the chunk, as the reference keeps it), t_max = 3.1."""
+    from neural_raytracing_amd.pathtracer.shapes import SphereCloud
+    g = torch.Generator().manual_seed(11)
+    centers = (torch.rand(37, 3, generator=g) * 2 - 1) * torch.tensor([1.0, 1.0, 0.5])
+    mine = SphereCloud(centers=centers.tolist(), radii=0.18, device="cuda")
+    rays = _cloud_rays(3000, 4)
+    radii = torch.full([37], 0.18)
+    t_max = 3.1
+    wt, wp, wn, wmask = _cloud_restated(centers, radii, rays, t_max, split_n)
+    got, mask = mine.intersect(rays.cuda(), t_max=t_max, split_n=split_n)
+    assert torch.equal(mask.cpu(), wmask)
+    assert 0.05 < wmask.float().mean() < 0.95
+    h = wmask
+    # n = normalize(p - c) scales p's last-bit differences by 1 / r = 5.6 (radius 0.18): 4e-6
+    for name, a, b, tol in (("t", got.t.cpu(), wt, 1e-6), ("p", got.p.cpu(), wp, 1e-6),
+                            ("n", got.n.cpu(), wn, 4e-6)):
+        err = (a[h] - b[h]).abs().max().item()
+        report(f"sphere_cloud_many[{split_n}].{name}", rays=3000, hits=int(h.sum()), maxabs=err)
+        assert err <= tol, (name, err)
+    assert torch.equal(got.t.cpu()[~h], wt[~h])
+    assert torch.equal(mine.intersect_test(rays.cuda(), t_max=t_max, split_n=split_n).cpu(), wmask)
+
+
+def test_sphere_cloud_empty_batch():
+    from neural_raytracing_amd.pathtracer.shapes import SphereCloud
+    it, mask = SphereCloud().intersect(torch.zeros(0, 6, device="cuda"))
+    assert mask.numel() == 0 and it.p.shape == (0, 3)
+
+
 def _bases(seed=5):
     """A NeuralBSDF, a Diffuse and a Conductor basis, oracle and product with equal numbers."""
     from neural_raytracing_amd.pathtracer.bsdf import (ComposeSpatialVarying, Conductor, Diffuse,

@@ -255,3 +255,24 @@ def test_renderer_point_light_ref_known_answer():
     assert torch.allclose(ds.d, torch.tensor([[0.0, 1.0, 3.0]]) / (1e-7 + dist))
     assert torch.allclose(le, torch.full((1, 3), 100 * 0.5 / (1e-7 + dist) ** 2))
     assert torch.allclose(ds.dist, torch.tensor([[dist]]))
+
+
+def test_sphere_cloud_ref_one_sphere_is_the_sphere():
+    """SphereCloudRef (shapes.py:99-206 statement by statement) with one sphere and t_max = inf
+    equals SphereRef (shapes.py:31-97) on the hits -- the pin of the HIP SphereCloud's one-sphere
+    case -- and misses keep t = inf."""
+    import math
+    g = torch.Generator().manual_seed(3)
+    o = torch.tensor([0.0, 0.0, 2.0]) + 0.2 * torch.randn(1, 64, 1, 3, generator=g)
+    d = torch.nn.functional.normalize(torch.cat([torch.rand(1, 64, 1, 2, generator=g) - 0.5,
+                                                 -torch.ones(1, 64, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+    cloud = R.SphereCloudRef(centers=[(0.1, 0.0, 0.0)], radii=0.5)
+    sph = R.SphereRef((0.1, 0.0, 0.0), 0.5)
+    ic, mc = cloud.intersect(rays)
+    is_, ms = sph.intersect(rays)
+    assert torch.equal(mc, ms) and 0 < int(mc.sum()) < 64
+    assert torch.equal(ic.t[mc], is_.t[ms]) and torch.equal(ic.p[mc], is_.p[ms])
+    assert torch.isinf(ic.t[~mc]).all()
+    assert torch.equal(cloud.intersect_test(rays), sph.intersect_test(rays))
+    assert math.isinf(float(ic.t[~mc][0])) if (~mc).any() else True
