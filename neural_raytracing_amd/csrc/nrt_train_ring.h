@@ -22,6 +22,12 @@
 // backward stores dZ_l [L+1][M][H].  The encoding rows of the T-enc layers fold straight into
 // dL/dx (three running sums per lane): d sin(p_q)/dx_i = cos(p_q) B_iq, d cos(p_q)/dx_i =
 // -sin(p_q) B_iq, d x_i / dx_i = 1, times leaky'(enc) on skip layers (their input is act(enc)).
+//
+// Saved activations (round 5): the training forward k_mlp_ring<..., SAVE> (below; nrt_mlp_forward_
+// multi with save buffers) runs fwd32_save + out32 on the solo program and stores A_l and the
+// encoding, and k_mlp_bwd_ring<..., SAVED> starts the backward program after its forward chunks
+// (BwdRingJob::fwd_chunks) and reads A through the caller's live-row index, copying the rows it
+// reads compactly for the weight gradients.  Same bits as the recomputing variant.
 #pragma once
 #include "nrt_shade_ring.h"
 
