@@ -310,7 +310,7 @@ def main():
             extra["api_paths"] = api_path_legs(scene, args)
             # the training step (training_utils.py:246-285) at the reference's
             # arithmetic and with the mixed march, each with its backward roofline
-            extra["train"] = {p: train_leg(p, 10, 2, cpu=(p == "fp32" and not args.no_cpu_baseline))
+            extra["train"] = {p: train_leg(p, 20, 3, cpu=(p == "fp32" and not args.no_cpu_baseline))
                               for p in ("fp32", "mixed")}
         if not args.no_cpu_baseline:
             extra.update(cpu_baseline(scene, size, args))

@@ -39,8 +39,9 @@ def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, w
 def _composite(out, values, mask, background, xs, ys, chunk, trim=0):
     valid = mask.any(dim=-1)
     v = torch.mean(values, dim=-2)
-    # v[~valid] = background, without the boolean scatter's host sync
-    v = torch.where(valid.unsqueeze(-1), v, v.new_tensor(float(background)))
+    # v[~valid] = background, without the boolean scatter's host sync (and the scalar as a
+    # wrapped number: a new_tensor would be a pageable host-to-device copy, a sync of its own)
+    v = torch.where(valid.unsqueeze(-1), v, float(background))
     if trim:
         # the tile was rendered with a `trim`-pixel border; keep its interior.  The reference
         # writes this as v[trim:-trim, trim:-trim] (main.py:52), which slices v's camera and row
