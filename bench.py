@@ -61,6 +61,9 @@ def parse():
                          "BASELINE.json configs[2..4] as one-GPU workloads")
     ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
     ap.add_argument("--crop", type=int, default=80, help="--scene train: crop side")
+    ap.add_argument("--envmap", action="store_true",
+                    help="--scene nerfle: NeRF+LE (NeRFLE(envmap=True), the light's envmap as the "
+                         "colour MLP's input, nerf.py:183-191) instead of NeRF+PT")
     ap.add_argument("--nrt-option", action="append", default=[], metavar="NAME=VALUE",
                     help="nrt_set_option before the run (include/nrt.h runtime options), e.g. "
                          "xcd_lines=0 for an A/B of a schedule switch; repeatable")
@@ -684,9 +687,12 @@ def api_path_legs(scene, args, reps=3):
 
 FLOP_SHIFT_8x128 = 331_200      # SphereSDF shift MLP per evaluation
 FLOP_NERFLE_SAMPLE = 327_840    # NeRFLE first (5x128, out 65) + second (8x64, in 70)
+# NeRF+LE: the colour MLP reads 64 latent + 3 + 4^2 x 3 envmap values (in 115): per sample
+# 2 x (dp H + L H^2 + skips dp H + H out + in F) = 2 x 72,432 for it (dp = 115 + 2 x 16)
+FLOP_NERFLE_ENVMAP_SAMPLE = 207_456 + 144_864
 
 
-def build_other_scene(name, device, samples):
+def build_other_scene(name, device, samples, envmap=False):
     """BASELINE.json configs[2..4] as single-GPU workloads (synthetic, seeded random init):
     colocate (cfg3: FoV camera, SphereSDF(n=64) + 8x128 shift, 4-component BSDF, point light),
     dtu (cfg4: DTU pinhole, 8x256 MLP SDF, 10 NeuralBSDF + 6 Diffuse, LightField),
@@ -748,14 +754,22 @@ def build_other_scene(name, device, samples):
                              "sensor), 8x256 F16 MLP SDF, ComposeSpatialVarying([NeuralBSDF x10, "
                              "Diffuse(sigmoid) x6]), LightField, NeRFIntegrator(Direct())")
     if name == "nerfle":
-        nerf = NeRFLE(device="cpu", steps=samples).to(device)
+        nerf = NeRFLE(device="cpu", steps=samples, envmap=envmap).to(device)
         focal = float(0.5 * 800 / math.tan(0.5 * 0.6911))
+        if envmap:
+            workload = (f"NeRFLE (NeRF+LE, envmap=True, nerf.py:153-214, 183-191): 5x128 "
+                        f"density/latent MLP + 8x64 colour MLP on 115 inputs (latent, view, the "
+                        f"point light's 4x4 envmap) at {samples} depths per ray, NeRFReproduce "
+                        f"(the per-MLP path: [S P, 115] inputs through HBM)")
+        else:
+            workload = (f"NeRFLE (NeRF+PT, nerf.py:153-214): 5x128 density/latent MLP + "
+                        f"8x64 colour MLP at {samples} depths per ray, point light, "
+                        "NeRFReproduce")
         return dict(kind="nerfle", nerf=nerf, integrator=NeRFReproduce(),
                     lights=PointLights(location=[0.0, 1.0, 0.0], device=device),
-                    c2w=view_c2w(0, 1), flop_sample=FLOP_NERFLE_SAMPLE,
-                    workload=f"NeRFLE (NeRF+PT, nerf.py:153-214): 5x128 density/latent MLP + "
-                             f"8x64 colour MLP at {samples} depths per ray, point light, "
-                             "NeRFReproduce")
+                    c2w=view_c2w(0, 1),
+                    flop_sample=FLOP_NERFLE_ENVMAP_SAMPLE if envmap else FLOP_NERFLE_SAMPLE,
+                    workload=workload)
     raise ValueError(name)
 
 
@@ -774,7 +788,7 @@ def bench_other(args):
         args.precision = "fp16"  # BASELINE cfg5 names the fp16 MFMA path
     nra.set_precision(args.precision)
     size = args.size
-    sc = build_other_scene(args.scene, device, args.samples)
+    sc = build_other_scene(args.scene, device, args.samples, envmap=args.envmap)
     if sc["kind"] == "march":
         rr = RowRenderer(sc["shape"], sc["lights"], sc["cameras"], sc["integrator"], sc["bsdf"],
                          size, range(size), background=0.0, with_noise=1e-3, device=device)
