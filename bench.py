@@ -692,11 +692,12 @@ FLOP_NERFLE_SAMPLE = 327_840    # NeRFLE first (5x128, out 65) + second (8x64, i
 FLOP_NERFLE_ENVMAP_SAMPLE = 207_456 + 144_864
 
 
-def build_other_scene(name, device, samples, envmap=False):
-    """BASELINE.json configs[2..4] as single-GPU workloads (synthetic, seeded random init):
-    colocate (cfg3: FoV camera, SphereSDF(n=64) + 8x128 shift, 4-component BSDF, point light),
-    dtu (cfg4: DTU pinhole, 8x256 MLP SDF, 10 NeuralBSDF + 6 Diffuse, LightField),
-    nerfle (cfg5: NeRFLE, NeRF+PT, `samples` depths per ray)."""
+def build_other_scene(name, device, samples, envmap=False, views=1):
+    """BASELINE.json configs[2..4] (synthetic, seeded random init): colocate (cfg3: FoV camera,
+    SphereSDF(n=64) + 8x128 shift, 4-component BSDF, point light), dtu (cfg4: DTU pinhole, 8x256
+    MLP SDF, 10 NeuralBSDF + 6 Diffuse, LightField), nerfle (cfg5: NeRFLE, NeRF+PT, `samples`
+    depths per ray).  views: camera views of the batch (bench_other renders one view per rank,
+    each rank its rows of every view, as the headline; view 0 is the one-GPU scene's)."""
     import neural_raytracing_amd.pathtracer as pt
     from neural_raytracing_amd.pathtracer.bsdf import (ComposeSpatialVarying, Conductor, Diffuse,
                                                         NeuralBSDF)
@@ -720,7 +721,8 @@ def build_other_scene(name, device, samples, envmap=False):
         for c in comps[:2]:
             c.mlp.to(device)
         bsdf.sp_var_fn.to(device)
-        R, T = pt.cameras.look_at_view_transform(dist=1.0, elev=30.0, azim=45.0)
+        R, T = pt.cameras.look_at_view_transform(
+            dist=1.0, elev=30.0, azim=[45.0 + 360.0 * i / views for i in range(views)])
         cam = pt.cameras.OpenGLPerspectiveCameras(R=R, T=T, device=device)
         lights = PointLights(location=(cam.get_camera_center()[0] * 1.05).tolist(), scale=5.0,
                              device=device)
@@ -742,10 +744,15 @@ def build_other_scene(name, device, samples, envmap=False):
         bsdf.sp_var_fn.to(device)
         K = torch.eye(4)
         K[0, 0], K[1, 1], K[0, 2], K[1, 2] = 2890.0, 2890.0, 800.0, 600.0
-        pose = torch.eye(4)
-        pose[:3, :4] = look_at((0.0, 0.5, 0.866))
-        pose[:3, 1:3] *= -1  # DTU/IDR cameras look down +z
-        cam = pt.cameras.DTUCamera(pose=pose[None].to(device), intrinsic=K[None].to(device),
+        poses = []
+        for i in range(views):
+            a = 2 * math.pi * i / views
+            pose = torch.eye(4)
+            pose[:3, :4] = look_at((0.866 * math.sin(a), 0.5, 0.866 * math.cos(a)))
+            pose[:3, 1:3] *= -1  # DTU/IDR cameras look down +z
+            poses.append(pose)
+        cam = pt.cameras.DTUCamera(pose=torch.stack(poses).to(device),
+                                   intrinsic=K[None].expand(views, 4, 4).contiguous().to(device),
                                    device=device)
         return dict(kind="march", shape=SDF(sdf=sdf.to(device), max_steps=samples), bsdf=bsdf,
                     lights=LightField(device="cpu").to(device), integrator=NeRFIntegrator(Direct()),
@@ -767,80 +774,172 @@ def build_other_scene(name, device, samples, envmap=False):
                         "NeRFReproduce")
         return dict(kind="nerfle", nerf=nerf, integrator=NeRFReproduce(),
                     lights=PointLights(location=[0.0, 1.0, 0.0], device=device),
-                    c2w=view_c2w(0, 1),
+                    c2w=torch.stack([view_c2w(i, views) for i in range(views)]),
                     flop_sample=FLOP_NERFLE_ENVMAP_SAMPLE if envmap else FLOP_NERFLE_SAMPLE,
                     workload=workload)
     raise ValueError(name)
 
 
+def _dist_env():
+    """(world, rank, local rank, process-group path on?) from torchrun's environment; a
+    torch.distributed.run launch takes the process-group path even at one rank."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return world, rank, local, world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+
+
+class NerfRowRenderer:
+    """bench_other's NeRFLE rows: this rank's rows of every view -- NeRFCamera raygen on the rows'
+    pixel positions, then NeRFReproduce's nerf(rays, lights) (integrators.py:260-267) -- into
+    [views, rows, size, 3]."""
+
+    def __init__(self, nerf, lights, cameras, size, rows, device):
+        self.nerf, self.lights, self.cameras, self.size = nerf, lights, cameras, size
+        R = len(rows)
+        v = torch.tensor(list(rows), dtype=torch.float32, device=device)[:, None].expand(R, size)
+        u = torch.arange(size, dtype=torch.float32, device=device)[None, :].expand(R, size)
+        self.positions = torch.stack([u, v], dim=-1).contiguous()
+        self.R = R
+
+    def render(self):
+        rays = self.cameras.rays_tile(0, 0, self.R, self.size, self.size, False,
+                                      positions=self.positions)
+        return self.nerf(rays, self.lights).reshape(len(self.cameras), self.R, self.size, 3)
+
+
 def bench_other(args):
-    """Single-GPU bench line for a non-default scene (--scene colocate|dtu|nerfle)."""
+    """Bench line of a non-default scene (--scene colocate|dtu|nerfle): one view per rank (weak
+    scaling, as the headline), each rank renders its rows of every view (row_shard, --tile-rows)
+    and one RCCL all-gather per step assembles the frames (make_step) -- BASELINE cfg4 / cfg5 are
+    8-GPU configurations.  Under torch.distributed.run the process-group path runs even at N = 1."""
     from neural_raytracing_amd import _lib
     import neural_raytracing_amd as nra
     import neural_raytracing_amd.pathtracer as pt
-    from neural_raytracing_amd.pathtracer.render import RowRenderer
-    if int(os.environ.get("WORLD_SIZE", "1")) != 1:
-        raise SystemExit("--scene other than nerf_synthetic runs on one GPU")
-    device = torch.device("cuda", 0)
+    from neural_raytracing_amd.pathtracer.render import RowRenderer, broadcast_module, row_shard
+    world, rank, local, dist_on = _dist_env()
+    if dist_on:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     _lib.load(require_device=True)
     if args.scene == "nerfle" and not args.precision_set:
         args.precision = "fp16"  # BASELINE cfg5 names the fp16 MFMA path
     nra.set_precision(args.precision)
     size = args.size
-    sc = build_other_scene(args.scene, device, args.samples, envmap=args.envmap)
+    sc = build_other_scene(args.scene, device, args.samples, envmap=args.envmap, views=world)
+    if dist_on:
+        for key in ("shape", "bsdf", "lights", "nerf"):
+            if sc.get(key) is not None:
+                broadcast_module(sc[key])
+    rows = row_shard(size, rank, world, args.tile_rows)
     if sc["kind"] == "march":
         rr = RowRenderer(sc["shape"], sc["lights"], sc["cameras"], sc["integrator"], sc["bsdf"],
-                         size, range(size), background=0.0, with_noise=1e-3, device=device)
-        step = rr.render
+                         size, rows, background=0.0, with_noise=1e-3, device=device)
+        render = rr.render
         kernel = MARCH_KERNEL[args.precision]
+        channels = sc["integrator"].dims()
     else:
         focal = float(0.5 * size / math.tan(0.5 * 0.6911))
-        cam = pt.cameras.NeRFCamera(cam_to_world=sc["c2w"][None].to(device), focal=focal,
-                                    device=device)
-        rays = cam.rays_tile(0, 0, size, size, size)
-
-        def step():
-            return sc["nerf"](rays, sc["lights"])
+        cam = pt.cameras.NeRFCamera(cam_to_world=sc["c2w"].to(device), focal=focal, device=device)
+        rr = NerfRowRenderer(sc["nerf"], sc["lights"], cam, size, rows, device)
+        render = rr.render
         kernel = "k_nerfle"
+        channels = 3
+    step = make_step(render, rows, size, rank, world, args.tile_rows, device, channels=channels,
+                     gather=dist_on)
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        if dist_on:
+            torch.distributed.barrier()
         _lib.profile_reset()
         _lib.profile_enable(True)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
+        if dist_on:
+            torch.distributed.barrier()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
         k_ms, k_n = _lib.profile_read(kernel)
-    rays_total = size * size * args.steps
+        evals = count_evals(render) if sc["kind"] == "march" else None
+        elapsed = max_over_ranks(elapsed, world, device, force=dist_on)
+    rays_rank = len(rows) * size * world  # this rank's rows of every view, per step
+    rays_total = world * size * size * args.steps
     if sc["kind"] == "march":
-        flop = rays_total * (args.samples + MARCH_KERNEL_SCAN_EVALS) * sc["flop_eval"]
-        if args.precision == "fp32-split":
-            flop *= 3  # f16 MFMA products per f32 product
+        products = 3 if args.precision == "fp32-split" else 1  # f16 MFMA products per f32 one
+        flop = rays_rank * args.steps * (args.samples + MARCH_KERNEL_SCAN_EVALS) * \
+            sc["flop_eval"] * products
     else:
-        flop = rays_total * args.samples * sc["flop_sample"]
+        flop = rays_rank * args.steps * args.samples * sc["flop_sample"]
     achieved = flop / (k_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.precision]
+    roof = {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
+            "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+            "flop_per_step": flop / args.steps, "kernel_ms_per_step": k_ms / args.steps,
+            "launches": k_n}
+    if evals is not None:
+        # the evaluations the job lists ran (device counter, one untimed frame), less the
+        # sdf(best) pass's: the kernel's utilisation (the algorithmic count prices every ray at
+        # every march step and can pass 1 when rays stop early, as on DTU)
+        exe = (evals - rays_rank) * sc["flop_eval"] * products * args.steps
+        roof["executed_flop_per_step"] = exe / args.steps
+        roof["executed_achieved"] = exe / (k_ms * 1e-3) / 1e12
+        roof["executed_frac"] = roof["executed_achieved"] / peak
+        roof["executed_evals_per_ray"] = evals / rays_rank
+        if args.precision == "mixed":
+            # the split refinement's time too (its evaluations are in the count, priced at one
+            # product though a split evaluation issues three: a lower bound)
+            ex_ms = k_ms
+            for k in ("k_refine3", "k_best3"):
+                ex_ms += _lib.profile_read(k)[0]
+            roof["executed_achieved"] = exe / (ex_ms * 1e-3) / 1e12
+            roof["executed_frac"] = roof["executed_achieved"] / peak
+    pmc = _committed_pmc(kernel, args.scene, size, args.precision)
+    if pmc is not None:
+        roof["traffic"], roof["traffic_source"] = pmc
     line = {
         "metric": f"ray-samples/sec/GPU ({args.scene} {size}x{size}x{args.samples})",
-        "value": rays_total * args.samples / elapsed, "unit": "ray-samples/s", "n_gpus": 1,
+        "value": rays_total * args.samples / elapsed, "unit": "ray-samples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000 * elapsed / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": args.precision, "data": "synthetic (seeded random-init weights)",
         "config": {"workload": sc["workload"], "image": [size, size],
-                   "samples_per_ray": args.samples},
-        "roofline": {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                     "flop_per_step": flop / args.steps,
-                     "kernel_ms_per_step": k_ms / args.steps, "launches": k_n},
+                   "samples_per_ray": args.samples, "views_per_step": world,
+                   "parallelism": f"row-tile shard x{world} ({args.tile_rows}-row tiles) + RCCL "
+                                  "all-gather"},
+        "roofline": roof,
     }
     if sc["kind"] == "march" and args.scene == "colocate":
         line["valu_roofline"] = colocate_valu_roofline(size, args, k_ms / max(k_n, 1))
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def _committed_pmc(kernel, scene, size, precision):
+    """(HBM bytes per launch, source) from a committed PMC pass of this scene's kernel
+    (profiles/pmc_<scene>_<kernel>.json: FETCH_SIZE + WRITE_SIZE per launch, tools/pmc.sh), or
+    None; the pass must be of the same frame size and precision."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{scene}_{kernel}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    if pm.get("size") != size or pm.get("precision") != precision:
+        return None
+    return pm.get("hbm_bytes_per_launch"), (f"committed PMC pass, profiles/pmc_{scene}_{kernel}"
+                                            f".json ({size}^2 {precision}); not measured in "
+                                            "this run")
 
 
 # VALU operations per SDF evaluation of the colocate scene's SphereSDF(n=64) (sdfs.py:37-43,

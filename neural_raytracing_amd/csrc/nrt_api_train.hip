@@ -925,7 +925,7 @@ double grad_bwd_row_flop(const MlpDev& d) {
 constexpr size_t kWgradTableBytes = 16384;  // device copy of a WgradBatch's job table
 
 struct TrainWs {
-  float *Z, *A, *dZ, *Eraw, *Eact, *Et, *Gt, *part, *kpart;
+  float *Z, *A, *dZ, *Eraw, *Eact, *Et, *Gt, *table, *part;
 };
 
 // per-wave encoding / encoding-gradient tiles of k_mlp_backward32: [waves][ke][32] floats
@@ -946,8 +946,8 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
   w.Eact = (float*)p; p += a256(enc);
   w.Et = (float*)p; p += a256(enc_tile_bytes(d, M));
   w.Gt = (float*)p; p += a256(enc_tile_bytes(d, M));
-  w.part = (float*)p; p += a256(kWgradTableBytes);  // weight-gradient job table
-  w.kpart = (float*)p;  // batched partial products
+  w.table = (float*)p; p += a256(kWgradTableBytes);  // weight-gradient job table
+  w.part = (float*)p;  // batched partial products
   return w;
 }
 
@@ -1298,7 +1298,7 @@ struct WgradBatch {
     j.bias = 1;
     jobs.push_back(j);
   }
-  // which kernel: k_wgrad_tile (option "wgrad_tile", default) or k_wgrad_batch
+  // which kernel: k_wgrad_batch (the default) or k_wgrad_tile (option "wgrad_tile" nonzero)
   bool tile = option(OPT_WGRAD_TILE) != 0;
   // lay out tiles, slices and partial offsets; returns the partial floats needed
   size_t plan(int& S) {
@@ -1537,7 +1537,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
   // workspace's weight-gradient table region (the weight gradients copy theirs after it ran)
   if (!latent && ring_backward_ok(&m, 1) && ring_backward_table_bytes(1) <= kWgradTableBytes) {
     ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M);
-    if ((rc = ring_backward(&m, 1, x, M, &dy, &dx, &w.A, &w.dZ, &w.Eraw, &w.Eact, w.part, st)))
+    if ((rc = ring_backward(&m, 1, x, M, &dy, &dx, &w.A, &w.dZ, &w.Eraw, &w.Eact, w.table, st)))
       return rc;
   } else {
     ProfScope prof("k_mlp_backward32", st, bwd_row_flop(d) * (double)M);
@@ -1583,7 +1583,7 @@ int nrt_mlp_backward(const nrt_mlp* m, const float* x, const float* latent, int6
     const float* In = kind == 0 ? w.Eraw : kind == 1 ? w.A + (size_t)(l - 1) * lay : w.Eact;
     batch.weight(dZ, R, In, C, M, dweights[l], ldw, c0);
   });
-  return batch.run(w.part, w.kpart, cap, st);
+  return batch.run(w.table, w.part, cap, st);
 }
 
 size_t nrt_mlp_backward_multi_workspace_bytes(const nrt_mlp* const* mlps, int n, int64_t M) {

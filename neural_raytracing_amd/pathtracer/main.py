@@ -36,7 +36,10 @@ def _tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, batch_dims, w
                                     with_noise=with_noise)
 
 
-def _composite(out, values, mask, background, xs, ys, chunk, trim=0):
+def _composite(out, values, mask, background, xs, ys, chunk, trim=0, H=None):
+    """values [N, W, H, B, C] of a W x H tile (W = chunk rows, H = chunk columns unless given)
+    into out[:, xs:xs + W, ys:ys + H] (main.py:85-90)."""
+    H = chunk if H is None else H
     valid = mask.any(dim=-1)
     v = torch.mean(values, dim=-2)
     # v[~valid] = background, without the boolean scatter's host sync (and the scalar as a
@@ -48,7 +51,7 @@ def _composite(out, values, mask, background, xs, ys, chunk, trim=0):
         # axes ([N, W, H, C]) -- a shape error at the assignment for every trim > 0 -- so the
         # intended crop of the two pixel axes is what runs here.
         v = v[:, trim:-trim, trim:-trim]
-    out[:, xs:xs + chunk, ys:ys + chunk, :] = v
+    out[:, xs:xs + chunk, ys:ys + H, :] = v
 
 
 def _fused(integrator, cameras, w_isect, addition):
@@ -63,6 +66,19 @@ def _fused(integrator, cameras, w_isect, addition):
     return tuple(fused) + (w_isect,)
 
 
+def _row_separable(integrator, shapes, addition, trim, bsdf, lights, w_isect):
+    """Tiles whose rows can be rendered on different ranks with the single-process result: the
+    integrator's draws per call must not depend on the number of rays -- NeRFReproduce over a
+    NeRFLE (one random.random() per call for its depths, nerf.py:178) -- with no addition hook
+    (it would see one rank's interaction), no trim border and no gradients (the all-gather is not
+    differentiable).  The fused Direct tiles are the other sharded case (render_tiles)."""
+    from .integrators import NeRFReproduce
+    from .shapes.nerf import NeRFLE
+    if addition is not nothing or trim or needs_grad(shapes, bsdf, lights, w_isect):
+        return False
+    return type(integrator) is NeRFReproduce and isinstance(shapes, NeRFLE)
+
+
 def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=None, height=None,
               chunk_size=32, bundle_size=4, background=1, addition=nothing, sampler=Sampler(),
               silent=False, trim=0, device="cuda", squeeze_first=True, w_isect=False,
@@ -71,10 +87,13 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     (main.py:67-68) and keeps the tile's interior (see _composite).
 
     Multi-GPU (the parallelism TODO of main.py:60): under an initialised torch.distributed
-    process group of several ranks that all ask for the same frame, the fused tile path renders
-    only this rank's bands of tile rows (band j of chunk_size rows when j % world == rank) and
-    one all-gather assembles the frame on every rank; the frame is the single-process frame (every
-    tile's camera and scan jitter is drawn in the reference's order on every rank).  shard: None =
+    process group of several ranks that all ask for the same frame, every rank generates every
+    tile's rays (the camera jitter and scan jitter drawn in the reference's order), marches and
+    shades only its row slices of each tile -- the tile's rows dealt round-robin, one row at a
+    time (render.tile_slice_rows), so one chunk_size == size tile (test_nerf's call) spreads over
+    all ranks -- and one all-gather assembles the frame on every rank; the frame and the RNG
+    states afterwards are the single-process render's.  Sharded: Direct / NeRFIntegrator(Direct)
+    on the fused tile path, and NeRFReproduce over a NeRFLE (_row_separable).  shard: None =
     automatic, False = render the whole frame on every rank, True = require sharding (render.
     shard_of); group: the process group.  The scene's weights must be equal on the ranks
     (render.broadcast_module replicates them)."""
@@ -93,7 +112,8 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
     ys = list(range(0, height, chunk_size))
     it = None
     fused = _fused(integrator, cameras, w_isect, addition) if trim == 0 else None
-    if needs_grad(shapes, bsdf, lights, w_isect):
+    grads = needs_grad(shapes, bsdf, lights, w_isect)
+    if grads:
         # training (a learned occlusion MLP included, as Direct.sample checks it):
         # integrator.sample carries the gradients
         fused = None
@@ -103,32 +123,43 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
         fused = None
     if getattr(lights, "per_camera", lambda: None)() is not None:
         fused = None  # one light per camera: Direct.sample shades camera by camera
+    tiles = []
+    for ij in range(len(xs) * len(ys)):  # the reference's tile order (main.py:63-65)
+        i, j = divmod(ij, len(ys))
+        tiles.append((xs[j], ys[i]))
+    sh = None
+    if fused is not None or _row_separable(integrator, shapes, addition, trim, bsdf, lights,
+                                           w_isect):
+        sh = _render.shard_of(cameras, size, width, chunk_size, background, group, shard)
+    elif shard:
+        raise _lib.NrtError("pathtrace(shard=True) shards Direct / NeRFIntegrator(Direct) tiles "
+                            "and NeRFReproduce over NeRFLE (no addition hook, trim 0, no "
+                            "gradients)")
+    dst, rows = out, None
+    if sh is not None:
+        # this rank's row slices of every tile (render.tile_slice_rows) into a slab, then one
+        # all-gather assembles the frame on every rank
+        rows = _render.tile_slice_rows(chunk_size, *sh)
+        dst = torch.full([batch_dims, (width // chunk_size) * len(rows), height,
+                          integrator.dims()], background, device=device, dtype=torch.float)
     if fused is not None:
         # every tile in the reference's order, batched into few launch chains (render.py)
-        tiles = []
-        for ij in range(len(xs) * len(ys)):
-            i, j = divmod(ij, len(ys))
-            tiles.append((xs[j], ys[i]))
-        sh = _render.shard_of(cameras, size, width, chunk_size, background, group, shard)
-        keep = None
-        if sh is not None:
-            rank, world = sh
-            keep = lambda k: (k % len(ys)) % world == rank  # noqa: E731  (band j = k % len(ys))
-        _render.render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk_size, size,
-                             with_noise, background, keep=keep)
-        if sh is not None:
-            _render.gather_tile_rows(out, chunk_size, sh[0], sh[1], group)
-    elif shard:
-        raise _lib.NrtError("pathtrace(shard=True) renders on the fused tile path only "
-                            "(Direct / NeRFIntegrator(Direct), no addition hook, a packed SDF)")
-    for ij in range(len(xs) * len(ys) if fused is None else 0):
-        i, j = divmod(ij, len(ys))
-        x0, y0 = xs[j], ys[i]
-        rays = _tile_rays(cameras, x0 - trim, y0 - trim, chunk_size + 2 * trim, size, sampler,
-                          bundle_size, batch_dims, with_noise, device, positions=bool(trim))
-        values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
-                                             sampler=sampler, w_isect=w_isect)
-        _composite(out, values, mask, background, x0, y0, chunk_size, trim)
+        _render.render_tiles(fused, shapes, lights, cameras, bsdf, dst, tiles, chunk_size, size,
+                             with_noise, background, rows=rows)
+    else:
+        sel = None if rows is None else torch.tensor(rows, dtype=torch.long, device=device)
+        R = chunk_size if rows is None else len(rows)
+        for x0, y0 in tiles:
+            rays = _tile_rays(cameras, x0 - trim, y0 - trim, chunk_size + 2 * trim, size, sampler,
+                              bundle_size, batch_dims, with_noise, device, positions=bool(trim))
+            if sel is not None:
+                rays = rays.index_select(1, sel)  # this rank's rows of the tile (all its draws made)
+            values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
+                                                 sampler=sampler, w_isect=w_isect)
+            X0 = x0 if rows is None else (x0 // chunk_size) * R
+            _composite(dst, values, mask, background, X0, y0, R, trim, H=chunk_size)
+    if sh is not None:
+        _render.gather_tile_shard(dst, out, chunk_size, sh[0], sh[1], group)
     if squeeze_first and batch_dims == 1:
         out = out.squeeze(0)
     return out, addition(it)

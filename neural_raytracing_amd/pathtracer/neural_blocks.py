@@ -118,11 +118,13 @@ def _mlp_forward(mlp, x, lat, handle=None):
     return y
 
 
-def _forward_saving(handles, x, outs):
+def _forward_saving(handles, x, outs, keep=True):
     """ys[k] = mlp_k(x) for same-shape MLPs (no latent) in one nrt_mlp_forward_multi call.  Under
     FP32 (and the mixed march's FP32 MLPs) with a ring-backward shape (nrt_mlp_save_bytes > 0) the
     forward also saves the activations its backward reads -> (ys, save buffers) -- else
-    (ys, None) and the backward evaluates the forward again."""
+    (ys, None) and the backward evaluates the forward again.  The save costs (L + 1) M H + 2 M dp
+    floats per MLP (about 11 KB a row for LightField 10x256): keep=False (a module in eval mode,
+    where a backward is not expected) skips it, and a backward that does come recomputes."""
     import ctypes
     lib = _lib.load(require_device=True)
     n, M = len(handles), x.shape[0]
@@ -130,7 +132,7 @@ def _forward_saving(handles, x, outs):
     P = ctypes.c_void_p
     hs = (P * n)(*[h.value for h in handles])
     save = None
-    if M > 0 and _lib.precision_code() != _lib.NRT_FP16:
+    if keep and M > 0 and _lib.precision_code() != _lib.NRT_FP16:
         nbytes = [lib.nrt_mlp_save_bytes(h.value, M) for h in handles]
         if all(nbytes):
             save = [torch.empty(b, dtype=torch.uint8, device=x.device) for b in nbytes]
@@ -184,7 +186,8 @@ class _MlpFn(torch.autograd.Function):
         ctx.save = None
         with torch.no_grad():
             if lat is None:
-                ys, ctx.save = _forward_saving([handle], x.detach(), [mlp.out.out_features])
+                ys, ctx.save = _forward_saving([handle], x.detach(), [mlp.out.out_features],
+                                               keep=mlp.training)
                 y = ys[0]
             else:
                 y = _mlp_forward(mlp, x.detach(), lat.detach(), handle)
@@ -271,8 +274,8 @@ class _MlpFn(torch.autograd.Function):
                                 "path for one-output MLPs (an SDF) only")
         if _parameters_upstream(x):
             raise _lib.NrtError("second derivatives with respect to the MLP's inputs are not on "
-                                "the HIP path: the SDF callable's points depend on a trainable "
-                                "parameter")
+                                "the HIP path: the SDF callable's points depend on a tensor that "
+                                "takes gradients")
         with torch.no_grad():
             _, dlat, grads = _MlpFn._first_order(ctx, dy)
         dx = None
@@ -282,19 +285,36 @@ class _MlpFn(torch.autograd.Function):
         return (None, dx, dlat, *grads)
 
 
+def diff_points(p):
+    """A leaf copy of the points p that autograd differentiates an SDF at (SDF.autograd_diff,
+    sdfs.py:184-197): tagged so the create_graph backward knows the leaf is the point set the
+    normal is taken at, not a trainable input (_parameters_upstream)."""
+    q = p.detach().requires_grad_(True)
+    q._nrt_diff_points = True
+    return q
+
+
+def _trainable_leaf(v):
+    return v is not None and v.requires_grad and not getattr(v, "_nrt_diff_points", False)
+
+
 def _parameters_upstream(t, limit=20000):
-    """True when the autograd graph of `t` reaches an nn.Parameter (a leaf that trains)."""
+    """True when the autograd graph of `t` reaches a leaf that takes gradients -- an
+    nn.Parameter or any other requires_grad leaf (a learned pose or offset held as a bare tensor)
+    -- other than the point leaf of diff_points.  A graph larger than `limit` nodes counts as
+    reaching one (the caller then refuses rather than dropping a term silently)."""
     fn = t.grad_fn
     if fn is None:
-        return isinstance(t, nn.Parameter)
+        return _trainable_leaf(t)
     seen, stack = set(), [fn]
-    while stack and len(seen) < limit:
+    while stack:
+        if len(seen) >= limit:
+            return True
         f = stack.pop()
         if f is None or f in seen:
             continue
         seen.add(f)
-        var = getattr(f, "variable", None)
-        if isinstance(var, nn.Parameter):
+        if _trainable_leaf(getattr(f, "variable", None)):  # AccumulateGrad of a leaf
             return True
         stack.extend(n for n, _ in getattr(f, "next_functions", ()))
     return False
@@ -336,7 +356,8 @@ class _MultiMlpFn(torch.autograd.Function):
         import ctypes
         handles = [train_handle(m) for m in mlps]
         with torch.no_grad():
-            ys, ctx.save = _forward_saving(handles, x.detach(), [m.out.out_features for m in mlps])
+            ys, ctx.save = _forward_saving(handles, x.detach(), [m.out.out_features for m in mlps],
+                                           keep=all(m.training for m in mlps))
         ctx.mlps = mlps
         ctx.handles = handles
         _save_versions(ctx, params)

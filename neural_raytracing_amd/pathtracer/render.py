@@ -138,78 +138,83 @@ MAX_BATCH_RAYS = 1 << 22
 
 
 def render_tiles(fused, shapes, lights, cameras, bsdf, out, tiles, chunk, size, with_noise,
-                 background, ox=0, oy=0, keep=None):
+                 background, ox=0, oy=0, rows=None):
     """pathtrace's fused tile loop (main.py:63-90) as few launch chains as possible: the rays of
     consecutive tiles are generated tile by tile (same camera-jitter draws, same order), marched,
     scanned and shaded in one nrt_sdf_intersect + nrt_shade_direct over all of them -- each tile
     keeps its own scan jitter (nrt_march_params.scan_max_t_groups) -- and composited tile by
     tile.  Equal to rendering the tiles one at a time; the GPU sees up to MAX_BATCH_RAYS rays per
     launch instead of chunk_size^2.
-    keep: predicate on the tile index -- only those tiles are rendered (a rank's row-tile shard,
-    pathtrace under torch.distributed); every tile's camera jitter and scan jitter are still
-    drawn, in the reference's tile order, so each rendered tile sees the numbers it would see in
-    a single-process render."""
+    rows: tile-local rows (a rank's row slices under torch.distributed, tile_slice_rows) -- every
+    tile's rays are generated whole (its camera jitter drawn as in a single-process render), then
+    only those rows of it are marched and shaded, and tile (x0, y0) lands in `out` -- the rank's
+    slab [N, bands x len(rows), height, C] -- at rows (x0 // chunk) * len(rows) ... ; every tile's
+    scan jitter is drawn in tile order, so each rendered ray sees the numbers it would see in a
+    single-process render."""
     direct, with_alpha = fused[:2]
     w_isect = fused[2] if len(fused) > 2 else False  # pathtrace's w_isect (main.py _fused)
     N = len(cameras)
-    per_tile = N * chunk * chunk
+    R = chunk if rows is None else len(rows)
+    per_tile = N * R * chunk
     dev = out.device
-    step = max(1, MAX_BATCH_RAYS // per_tile)
+    sel = None if rows is None else torch.tensor(list(rows), dtype=torch.long, device=dev)
+    step = max(1, MAX_BATCH_RAYS // max(per_tile, 1))
     primary = bool(direct.training)
-    mine = [k for k in range(len(tiles)) if keep is None or keep(k)]
     # the scan jitter of every tile (sdfs.py:236) in tile order: python's RNG, independent of the
     # camera's torch draws, so drawing them up front leaves both sequences as the per-tile loop
     scan = [random.random() for _ in tiles] if primary else None
-    pos = 0  # next tile whose camera jitter is to be drawn
-    for t0 in range(0, len(mine), step):
-        batch = mine[t0:t0 + step]
+    for t0 in range(0, len(tiles), step):
+        batch = range(t0, min(t0 + step, len(tiles)))
         rays = torch.empty(len(batch), per_tile, 6, device=dev)
         for k, ti in enumerate(batch):
-            while pos < ti:  # tiles of other ranks: draw their jitter, render nothing
-                _draw_tile_noise(cameras, tiles[pos], chunk, size, with_noise)
-                pos += 1
             x0, y0 = tiles[ti]
-            rays[k] = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise).reshape(-1, 6)
-            pos = ti + 1
+            r = cameras.rays_tile(x0, y0, chunk, chunk, size, with_noise)
+            if sel is not None:
+                r = r.index_select(1, sel)  # [N, chunk rows, chunk cols, ...] -> this rank's rows
+            rays[k] = r.reshape(-1, 6)
+        if per_tile == 0:
+            continue  # (no rows of these tiles here: their draws are taken, nothing to render)
         b = direct_kernels(direct, shapes, rays.reshape(-1, 6), bsdf, lights,
                            scan_groups=len(batch) if len(batch) > 1 else None, w_isect=w_isect,
                            scan_draws=[scan[ti] for ti in batch] if primary else None)
         for k, ti in enumerate(batch):
             x0, y0 = tiles[ti]
-            composite_slice(b, slice(k * per_tile, (k + 1) * per_tile), N, chunk, with_alpha,
-                            background, out, x0 - ox, y0 - oy)
-    while pos < len(tiles):  # the jitter of the trailing tiles of other ranks
-        _draw_tile_noise(cameras, tiles[pos], chunk, size, with_noise)
-        pos += 1
+            X0 = x0 - ox if rows is None else ((x0 - ox) // chunk) * R
+            composite_slice(b, slice(k * per_tile, (k + 1) * per_tile), N, R, chunk, with_alpha,
+                            background, out, X0, y0 - oy)
 
 
-def composite_slice(b, sl, N, chunk, with_alpha, background, out, X0, Y0):
-    """composite() of the rays sl of a batched buffer set (one chunk x chunk tile)."""
+def composite_slice(b, sl, N, W, H, with_alpha, background, out, X0, Y0):
+    """composite() of the rays sl of a batched buffer set (one W x H tile, [N, W, H] order)."""
     _lib.call("nrt_composite", _lib.ptr(b.rgb[sl]), _lib.ptr(b.thr[sl]), _lib.ptr(b.hit[sl]),
-              N, chunk, chunk, int(with_alpha), int(not with_alpha), float(background),
+              N, W, H, int(with_alpha), int(not with_alpha), float(background),
               _lib.ptr(out), out.shape[1], out.shape[2], out.shape[3], int(X0), int(Y0),
               _lib.stream())
 
 
-def _draw_tile_noise(cameras, tile, chunk, size, with_noise):
-    """Consume the camera-jitter draw of a tile this rank does not render (cameras.rays_tile's
-    torch.rand, cameras.py:45-48 in the reference): the same RNG state afterwards as a render of
-    that tile."""
-    if with_noise:
-        draw = getattr(cameras, "tile_noise", None)
-        if draw is not None:
-            draw(chunk, chunk)
-        else:
-            cameras.rays_tile(tile[0], tile[1], chunk, chunk, size, with_noise)
+def tile_slice_rows(chunk, rank, world):
+    """Tile-local rows of `rank` under pathtrace's row sharding: the rows of every chunk-row tile
+    are dealt round-robin, one row at a time, so a single chunk_size == size tile (test_nerf's
+    call, training_utils.py:325) spreads over every rank and the ranks' row counts differ by at
+    most one per tile (a centred object's cost spreads evenly too)."""
+    return list(range(rank, chunk, world))
+
+
+def tile_shard_rows(width, chunk, rank, world):
+    """Image rows of `rank` (tile_slice_rows of every band of chunk rows), in slab order."""
+    local = tile_slice_rows(chunk, rank, world)
+    return [x0 + r for x0 in range(0, width, chunk) for r in local]
 
 
 def shard_of(cameras, size, width, chunk, background, group=None, shard=None):
-    """(rank, world) when pathtrace should render a row-tile shard (images shard by
-    pixel-row tiles, one all-gather at frame end), else None.  shard: None = automatic (a
-    process group of more than one rank, and every rank asks for the same frame -- checked with
-    one small all-gather of the cameras' corner rays and the frame parameters, so ranks that
-    render different views each keep rendering their own full frame), False = never, True =
-    always (an error if the ranks' frames differ)."""
+    """(rank, world) when pathtrace should render a row shard (images shard by pixel
+    rows, one all-gather at frame end), else None.  shard: None = automatic (a process group of
+    more than one rank, and every rank asks for the same frame -- checked with one small
+    all-gather of the cameras' corner rays and the frame parameters, so ranks that render
+    different views each keep rendering their own full frame), False = never, True = always (an
+    error if the ranks' frames differ or the frame cannot be sharded).  Once a group of several
+    ranks exists, every rank takes part in the fingerprint all-gather whatever its own
+    parameters, so ranks that disagree about the frame fall back together instead of hanging."""
     if shard is False:
         return None
     try:
@@ -222,19 +227,24 @@ def shard_of(cameras, size, width, chunk, background, group=None, shard=None):
                                 "process group")
         return None
     world = dist.get_world_size(group)
-    if (world <= 1 and not shard) or width % chunk:
+    if world <= 1 and not shard:
         return None  # (shard=True at one rank runs the sharded path: the RCCL test's case)
     rank = dist.get_rank(group)
+    shardable = width % chunk == 0 and chunk >= world
+    if shard and not shardable:
+        raise _lib.NrtError(f"pathtrace(shard=True): width {width} must be a multiple of "
+                            f"chunk_size {chunk} and chunk_size >= the {world} ranks")
     dev = torch.device("cuda", torch.cuda.current_device()) \
         if dist.get_backend(group) == "nccl" else torch.device("cpu")
     # a fixed-length fingerprint (the collective needs equal shapes on every rank): the frame
-    # parameters and three moments of the cameras' corner rays
+    # parameters, whether this rank can shard it, and three moments of the cameras' corner rays
     corners = torch.cat([cameras.rays_tile(x, y, 1, 1, size, False).reshape(-1).double().cpu()
                          for x, y in ((0, 0), (width - 1, size - 1))])
     w = torch.arange(1, corners.numel() + 1, dtype=torch.float64)
     key = torch.tensor([float(len(cameras)), float(size), float(width), float(chunk),
-                        float(background), float(corners.sum()), float((corners * w).sum()),
-                        float((corners * corners).sum())], dtype=torch.float64).to(dev)
+                        float(background), float(shardable), float(corners.sum()),
+                        float((corners * w).sum()), float((corners * corners).sum())],
+                       dtype=torch.float64).to(dev)
     keys = [torch.empty_like(key) for _ in range(world)]
     dist.all_gather(keys, key, group=group)
     same = all(torch.equal(k, keys[0]) for k in keys)
@@ -242,17 +252,18 @@ def shard_of(cameras, size, width, chunk, background, group=None, shard=None):
         if shard:
             raise _lib.NrtError("pathtrace(shard=True): the ranks asked for different frames")
         return None
+    if not shardable:
+        return None
     return rank, world
 
 
-def gather_tile_rows(out, chunk, rank, world, group=None):
-    """After each rank rendered its row-tile shard into `out` [N, width, height, C] (the rows of
-    tile band j when j % world == rank), every rank's rows into every rank's `out` by one
-    all-gather (RowGather)."""
-    rows = row_shard(out.shape[1], rank, world, chunk)
-    idx = torch.tensor(rows, dtype=torch.long, device=out.device)
-    local = out.index_select(1, idx)
-    return gather_rows(local, out.shape[1], rank, world, chunk, out=out, group=group)
+def gather_tile_shard(slab, out, chunk, rank, world, group=None):
+    """After each rank rendered its row slices (tile_shard_rows) into its slab
+    [N, bands x rows, height, C], every rank's rows into every rank's `out` [N, width, height, C]
+    by one all-gather (RowGather over the ranks' tile_shard_rows)."""
+    width = out.shape[1]
+    shards = tuple(tuple(tile_shard_rows(width, chunk, r, world)) for r in range(world))
+    return gather_rows(slab, width, rank, world, chunk, out=out, group=group, shards=shards)
 
 
 def row_shard(size, rank, world, tile_rows=16):
@@ -307,10 +318,12 @@ class RowGather:
     tensors are built once per frame shape, not per step."""
 
     def __init__(self, size, rank, world, tile_rows, shape, device, dtype=torch.float32,
-                 group=None):
+                 group=None, shards=None):
         N, W, C = shape
         self.size, self.rank, self.world, self.group = size, rank, world, group
-        self.shards = [row_shard(size, r, world, tile_rows) for r in range(world)]
+        # shards: every rank's image rows in its slab's order (default: row_shard's tiles)
+        self.shards = [list(s) for s in shards] if shards is not None else \
+            [row_shard(size, r, world, tile_rows) for r in range(world)]
         self.max_rows = max(len(s) for s in self.shards)
         self.slab = torch.zeros(N, self.max_rows, W, C, device=device, dtype=dtype)
         self.buf = torch.empty(world * N, self.max_rows, W, C, device=device, dtype=dtype)
@@ -339,15 +352,17 @@ def clear_gathers():
     _GATHERS.clear()
 
 
-def gather_rows(local, size, rank, world, tile_rows, out=None, group=None):
+def gather_rows(local, size, rank, world, tile_rows, out=None, group=None, shards=None):
     """All-gather every rank's row slab ([N, R_rank, W, C]) and assemble [N, size, W, C]
     (a RowGather per frame shape / device / group from a small LRU; a caller that renders many
-    shapes should own its RowGather, as bench.make_step does)."""
+    shapes should own its RowGather, as bench.make_step does).  shards: the ranks' row lists
+    (tuple of tuples), default row_shard's tiles of tile_rows."""
     N, _, W, C = local.shape
-    key = (size, rank, world, tile_rows, N, W, C, local.device, local.dtype, group)
+    key = (size, rank, world, tile_rows, N, W, C, local.device, local.dtype, group, shards)
     g = _GATHERS.pop(key, None)
     if g is None:
-        g = RowGather(size, rank, world, tile_rows, (N, W, C), local.device, local.dtype, group)
+        g = RowGather(size, rank, world, tile_rows, (N, W, C), local.device, local.dtype, group,
+                      shards=shards)
     _GATHERS[key] = g  # most recent last
     while len(_GATHERS) > _GATHERS_MAX:
         _GATHERS.pop(next(iter(_GATHERS)))

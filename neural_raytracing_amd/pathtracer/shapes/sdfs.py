@@ -446,8 +446,9 @@ class SDF:
         """SDF.autograd_diff (sdfs.py:184-197) through the callable: create_graph, so the normal
         carries gradients for whatever parameters the callable closes over (a render under
         no_grad takes the same values without the graph)."""
+        from ..neural_blocks import diff_points
         with torch.enable_grad():
-            q = p.detach().requires_grad_(True)
+            q = diff_points(p)  # the point leaf (not a trainable input of the callable)
             out = self.sdf(q)
             (g,) = torch.autograd.grad(out, q, torch.ones_like(out), create_graph=create_graph)
         return g if create_graph else g.detach()

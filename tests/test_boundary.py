@@ -331,8 +331,8 @@ def _stub_fused_path(monkeypatch, rendered):
         rendered.extend(sorted(set(rays_flat[:, 1].long().tolist())))
         return types.SimpleNamespace(rgb=rgb)
 
-    def composite_slice(b, sl, N, chunk, with_alpha, background, out, X0, Y0):
-        out[:, X0:X0 + chunk, Y0:Y0 + chunk, :3] = b.rgb[sl].view(N, chunk, chunk, 3)
+    def composite_slice(b, sl, N, W, H, with_alpha, background, out, X0, Y0):
+        out[:, X0:X0 + W, Y0:Y0 + H, :3] = b.rgb[sl].view(N, W, H, 3)
 
     monkeypatch.setattr(render, "direct_kernels", direct_kernels)
     monkeypatch.setattr(render, "composite_slice", composite_slice)
@@ -343,12 +343,12 @@ def _stub_fused_path(monkeypatch, rendered):
     return main, shapes, direct
 
 
-def _pathtrace_frame(main, shapes, direct, seed, views=2, **kw):
+def _pathtrace_frame(main, shapes, direct, seed, views=2, size=48, chunk=8, **kw):
     import random
     torch.manual_seed(seed)
     random.seed(seed)
-    out, _ = main.pathtrace(shapes, None, _StubCameras(views), direct, bsdf=None, size=48,
-                            chunk_size=8, bundle_size=1, background=0.25, silent=True,
+    out, _ = main.pathtrace(shapes, None, _StubCameras(views), direct, bsdf=None, size=size,
+                            chunk_size=chunk, bundle_size=1, background=0.25, silent=True,
                             device="cpu", with_noise=1e-3, **kw)
     return out, random.random(), torch.rand(1)  # the RNG states after the frame
 
@@ -356,38 +356,46 @@ def _pathtrace_frame(main, shapes, direct, seed, views=2, **kw):
 def _pathtrace_shard_worker(rank, world, port, q):
     import torch.distributed as dist
     from _pytest.monkeypatch import MonkeyPatch
+    from neural_raytracing_amd.pathtracer.render import tile_shard_rows
     mpatch = MonkeyPatch()
     rendered = []
     main, shapes, direct = _stub_fused_path(mpatch, rendered)
-    want = _pathtrace_frame(main, shapes, direct, 5, shard=False)  # before any process group
-    n_single = len(rendered)
+    cases = [(48, 8), (64, 64)]  # tiles of 8 rows; one 64-row tile (test_nerf: chunk == size)
+    want = [_pathtrace_frame(main, shapes, direct, 5, size=s, chunk=c, shard=False)
+            for s, c in cases]  # before any process group
+    n_single = len(set(rendered))
     rendered.clear()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    got = _pathtrace_frame(main, shapes, direct, 5)  # automatic: sharded
-    from neural_raytracing_amd.pathtracer.render import row_shard
-    mine = sorted(set(rendered))
+    res = []
+    for (s, c), w in zip(cases, want):
+        rendered.clear()
+        got = _pathtrace_frame(main, shapes, direct, 5, size=s, chunk=c)  # automatic: sharded
+        mine = sorted(set(rendered))
+        res.append((bool(torch.equal(got[0], w[0])), got[1] == w[1], bool(torch.equal(got[2], w[2])),
+                    mine == sorted(tile_shard_rows(s, c, rank, world)), len(mine)))
     # ranks asking for different frames (here: different camera counts) each render their own
     rendered.clear()
     own = _pathtrace_frame(main, shapes, direct, 6, views=2 + rank)
     n_own = len(set(rendered))
-    q.put((rank, (bool(torch.equal(got[0], want[0])), got[1] == want[1],
-                  bool(torch.equal(got[2], want[2])), mine == row_shard(48, rank, world, 8),
-                  n_single, n_own, tuple(own[0].shape))))
+    q.put((rank, (res, n_single, n_own, tuple(own[0].shape))))
     dist.destroy_process_group()
     mpatch.undo()
 
 
 def test_pathtrace_row_tile_shard_gloo_world2():
-    """pathtrace under a 2-rank process group (gloo): each rank renders the rows of its tile
-    bands only (render.row_shard with chunk_size rows), the all-gather assembles the frame, and
-    the frame and both RNG states afterwards equal the single-process render's (main.py:54-90,
-    the parallelism TODO at :60)."""
+    """pathtrace under a 2-rank process group (gloo): each rank renders its row slices of every
+    tile only (render.tile_slice_rows), the all-gather assembles the frame, and the frame and
+    both RNG states afterwards equal the single-process render's (main.py:54-90, the parallelism
+    TODO at :60) -- for 8-row tiles and for the one-tile frame test_nerf asks for
+    (chunk_size == size, training_utils.py:325), where each rank renders half the rows."""
     res = _spawn(_pathtrace_shard_worker, 2)
     for rank in (0, 1):
-        frame_eq, py_rng_eq, torch_rng_eq, rows_ok, n_single, n_own, shape = res[rank]
-        assert frame_eq and py_rng_eq and torch_rng_eq and rows_ok, res
-        assert n_single == 48  # unsharded: every row
+        cases, n_single, n_own, shape = res[rank]
+        for frame_eq, py_rng_eq, torch_rng_eq, rows_ok, n_rows in cases:
+            assert frame_eq and py_rng_eq and torch_rng_eq and rows_ok, res
+        assert cases[0][4] == 24 and cases[1][4] == 32  # half the rows of each frame
+        assert n_single == 64  # unsharded: every row
         assert n_own == 48 and shape == (2 + rank, 48, 48, 3)  # different frames: not sharded
 
 
@@ -400,3 +408,62 @@ def test_pathtrace_shard_off_without_process_group(monkeypatch):
     assert sorted(set(rendered)) == list(range(48)) and out.shape == (2, 48, 48, 3)
     with pytest.raises(NrtError):
         _pathtrace_frame(main, shapes, direct, 3, shard=True)
+
+
+def _stub_nerfle():
+    """A NeRFLE whose forward is a torch stand-in with the reference's draw (one random.random()
+    per call for the depths, nerf.py:178): what pathtrace's NeRFReproduce shard must preserve."""
+    from neural_raytracing_amd.pathtracer.shapes import NeRFLE
+
+    class StubNeRF(NeRFLE):
+        def forward(self, rays, lights):
+            u = random.random()
+            return rays[..., :3] + u * rays[..., 3:6]
+
+    import random
+    return StubNeRF(device="cpu")
+
+
+def _nerf_frame(nerf, seed, **kw):
+    import random
+    from neural_raytracing_amd.pathtracer import main
+    from neural_raytracing_amd.pathtracer.integrators import NeRFReproduce
+    torch.manual_seed(seed)
+    random.seed(seed)
+    with torch.no_grad():  # as the scripts render (training_utils.py:319)
+        out, _ = main.pathtrace(nerf, None, _StubCameras(2), NeRFReproduce(), size=32,
+                                chunk_size=32, bundle_size=1, background=0, device="cpu",
+                                with_noise=1e-3, **kw)
+    return out, random.random(), torch.rand(1)
+
+
+def _nerf_shard_worker(rank, world, port, q):
+    import torch.distributed as dist
+    torch.manual_seed(0)
+    nerf = _stub_nerfle()
+    seen = []
+    fwd = nerf.forward
+
+    def spy(rays, lights):
+        seen.append(rays.shape)
+        return fwd(rays, lights)
+    nerf.forward = spy
+    want = _nerf_frame(nerf, 7, shard=False)
+    seen.clear()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    got = _nerf_frame(nerf, 7)
+    q.put((rank, (bool(torch.equal(got[0], want[0])), got[1] == want[1],
+                  bool(torch.equal(got[2], want[2])), [tuple(s) for s in seen])))
+    dist.destroy_process_group()
+
+
+def test_pathtrace_nerf_reproduce_shard_gloo_world2():
+    """NeRFReproduce over a NeRFLE (cfg5's path, nerf.py:175-214) shards like the fused tiles:
+    each of 2 ranks runs the NeRF on half the rows of the one 32-row tile, with the same depth
+    draw, and the gathered frame and RNG states equal the single-process render's."""
+    res = _spawn(_nerf_shard_worker, 2)
+    for rank in (0, 1):
+        frame_eq, py_eq, torch_eq, seen = res[rank]
+        assert frame_eq and py_eq and torch_eq, res
+        assert seen == [(2, 16, 32, 1, 6)], seen

@@ -1,0 +1,39 @@
+"""Host-side guards of the training path (CPU): the create_graph backward of _MlpFn drops the
+d2y/dx2 term, so it must refuse whenever the MLP's inputs depend on anything that takes
+gradients other than the point leaf the normal is taken at (SDF.autograd_diff, sdfs.py:184-197)."""
+import torch
+
+from neural_raytracing_amd.pathtracer.neural_blocks import _parameters_upstream, diff_points
+
+
+def test_point_leaf_is_not_upstream():
+    q = diff_points(torch.randn(5, 3))
+    assert not _parameters_upstream(q)
+    assert not _parameters_upstream(q * 2.0 + 1.0)
+    assert not _parameters_upstream(torch.randn(5, 3))  # no graph at all
+
+
+def test_parameter_upstream():
+    w = torch.nn.Parameter(torch.randn(3))
+    q = diff_points(torch.randn(5, 3))
+    assert _parameters_upstream(q + w)
+    assert _parameters_upstream(w)
+
+
+def test_bare_requires_grad_leaf_upstream():
+    """a learned offset held as a plain requires_grad tensor (not nn.Parameter)."""
+    offset = torch.zeros(3, requires_grad=True)
+    q = diff_points(torch.randn(5, 3))
+    assert _parameters_upstream(q + offset)
+    assert _parameters_upstream(offset.expand(5, 3) * 1.0)
+    plain = torch.randn(5, 3, requires_grad=True)  # an untagged leaf as the MLP's input itself
+    assert _parameters_upstream(plain)
+
+
+def test_node_limit_counts_as_upstream():
+    q = diff_points(torch.randn(4, 3))
+    x = q
+    for _ in range(50):
+        x = x * 1.0
+    assert not _parameters_upstream(x)  # within the default limit: a clean chain
+    assert _parameters_upstream(x, limit=10)  # the walk gave up: refuse
