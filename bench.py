@@ -766,8 +766,9 @@ def build_other_scene(name, device, samples, envmap=False, views=1):
         if envmap:
             workload = (f"NeRFLE (NeRF+LE, envmap=True, nerf.py:153-214, 183-191): 5x128 "
                         f"density/latent MLP + 8x64 colour MLP on 115 inputs (latent, view, the "
-                        f"point light's 4x4 envmap) at {samples} depths per ray, NeRFReproduce "
-                        f"(the per-MLP path: [S P, 115] inputs through HBM)")
+                        f"point light's 4x4 envmap) at {samples} depths per ray, NeRFReproduce; "
+                        f"fp16: the fused k_nerfle16 with the frame-constant envmap folded into "
+                        f"one input column (FLOP priced at the 115-input count)")
         else:
             workload = (f"NeRFLE (NeRF+PT, nerf.py:153-214): 5x128 density/latent MLP + "
                         f"8x64 colour MLP at {samples} depths per ray, point light, "

@@ -439,7 +439,11 @@ int nrt_render_tile(const nrt_camera* host_cams, int32_t N, int32_t x0, int32_t 
  * light[light_dim] (device) is the point light's location (envmap=False, light_dim 3) or
  * its envmap encoding from nrt_light_envmap (envmap=True, light_dim 3 bins^2).
  * first: 3 -> 65, second: (67 + light_dim) -> 3.  ts[S] device; rgb [P,3].  FP16 with the
- * default shapes (light_dim 3) runs the fused k_nerfle16 kernel.
+ * default shapes runs the fused k_nerfle16 kernel -- for the envmap too: the envmap is one
+ * constant per call, so its share of the colour MLP's input (W[:, env] env in the init and skip
+ * layers, env B[env, :] in the Fourier projection) is folded into one constant input column of
+ * the kernel's 70-input program, rebuilt when the envmap changes (one 4 light_dim-byte read-back
+ * and a stream synchronisation per call).
  * workspace: nrt_nerfle_workspace_bytes(P, S, light_dim) bytes of device memory.
  * ------------------------------------------------------------------------------------- */
 size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim);

@@ -473,20 +473,29 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
   E.drain();
 }
 
-// first: 3 -> 65, hidden 128, F 16; second: 70 -> 3, hidden 64, F 16; both leaky_relu, no latent
+// first: 3 -> 65, hidden 128, F 16; second: 67 + LK -> 3, hidden 64, F 16 (LK = 3: the point
+// light's location; LK = 3 bins^2: NeRF+LE's envmap, folded into one constant input column by
+// build_nerf_program); both leaky_relu, no latent
 static bool nerf_fusable(const nrt_mlp* f, const nrt_mlp* s) {
   const MlpDev& a = f->host_dev;
   const MlpDev& b = s->host_dev;
   if (f->refreshed || s->refreshed) return false;  // stale program streams: unfused path
   return a.in_size == 3 && a.nb == 4 && a.freqs == 16 && a.out == 65 && a.latent == 0 &&
-         a.act == ACT_LEAKY && b.in_size == 70 && b.nb == 2 && b.freqs == 16 && b.out == 3 &&
+         a.act == ACT_LEAKY && b.in_size >= 70 && b.nb == 2 && b.freqs == 16 && b.out == 3 &&
          b.latent == 0 && b.act == ACT_LEAKY && a.n_hidden == kNerfL1 && b.n_hidden == kNerfL2 &&
          a.skip == kNerfSkip && b.skip == kNerfSkip && (int)f->host_w.size() == a.n_hidden + 2 &&
          (int)s->host_w.size() == b.n_hidden + 2 && a.ke == 48;
 }
 
-// the program stream of k_nerfle16 (chunk order in the kernel's header comment)
-static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out) {
+// the program stream of k_nerfle16 (chunk order in the kernel's header comment).
+// env (NeRF+LE, nerf.py:183-199): the light's envmap, LK = s->in_size - 67 values.  It is one
+// constant per frame, so its share of the colour MLP's input is folded into the kernel's 70-input
+// layout: input column 67 is a constant 1 (the kernel's light input is (1, 0, 0)), its weight in
+// the init and skip layers is W[:, env] . env and its row of the Fourier basis is env . B[env, :]
+// (both summed in double, rounded once to f32); columns 68-69 are zero.  x'.B' = x.B and
+// W' x' = W x up to the order of the sums: the FP16 kernel's products are unchanged in kind.
+static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out,
+                              const float* env = nullptr) {
   out.ok = false;
   const MlpDev& a = f->host_dev;
   const MlpDev& b = s->host_dev;
@@ -514,8 +523,14 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
       return NRT_EUNSUPPORTED;
     }
   }
-  // element (h, j) of second-MLP encoding k-step e -> reference input column (-1: none)
+  // element (h, j) of second-MLP encoding k-step e -> kernel input column (-1: none)
   const int IN = 70, F = 16;
+  const int INo = s->host_dev.in_size;  // the MLP's own input width (70, or 67 + 3 bins^2)
+  const int LK = INo - 67;
+  if (env == nullptr && INo != IN) {
+    set_error("build_nerf_program: a NeRF+LE colour MLP needs its envmap");
+    return NRT_EINVAL;
+  }
   auto enc_col = [&](int e, int hf, int j) -> int {
     if (e < 2) {
       const int q = 8 * e + 4 * hf + (j >> 1);
@@ -528,6 +543,29 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
     }
     return (hf == 0 && j < 6) ? 64 + j : -1;
   };
+  // the second MLP's basis at kernel input column col (< IN), with the envmap fold
+  auto basis_at = [&](int col, int q) -> float {
+    if (env == nullptr || col < 67) return s->host_basis[(size_t)col * F + q];
+    if (col > 67) return 0.f;
+    double acc = 0.0;
+    for (int k = 0; k < LK; ++k) acc += (double)env[k] * s->host_basis[(size_t)(67 + k) * F + q];
+    return (float)acc;
+  };
+  // weight of layer l at (row, kernel column col) of its [hidden? H | x (IN) | sin F | cos F]
+  // layout; Co is the layer's own width ([hidden? H | x (INo) | sin F | cos F])
+  auto weight_at = [&](const std::vector<float>& W, int row, int col, int base, int Co) -> float {
+    if (col < base) return W[(size_t)row * Co + col];
+    const int ic = col - base;
+    if (ic < 67 || env == nullptr) {
+      const int oc = ic < IN ? ic : INo + (ic - IN);
+      return W[(size_t)row * Co + base + oc];
+    }
+    if (ic >= IN) return W[(size_t)row * Co + base + INo + (ic - IN)];
+    if (ic > 67) return 0.f;
+    double acc = 0.0;
+    for (int k = 0; k < LK; ++k) acc += (double)W[(size_t)row * Co + base + 67 + k] * env[k];
+    return (float)acc;
+  };
   // projection chunk: A[q][k] = basis[x index of k][q] split into hi and lo halves
   coff.push_back((int)frags.size());
   for (int part = 0; part < 2; ++part)
@@ -537,7 +575,7 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
         const int q = lane & 31, hf = lane >> 5;
         for (int j = 0; j < 8; ++j) {
           const int col = enc_col(2 + tt, hf, j);
-          const float v = (q < F && col >= 0) ? s->host_basis[(size_t)col * F + q] : 0.f;
+          const float v = (q < F && col >= 0) ? basis_at(col, q) : 0.f;
           const _Float16 hi = (_Float16)v;
           fr[lane * 8 + j] = part == 0 ? hi : (_Float16)(v - (float)hi);
         }
@@ -553,6 +591,7 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
     const bool hid = !init;
     const bool enc = init || skip;
     const int R = outl ? 3 : H, C = (hid ? H : 0) + (enc ? IN + 2 * F : 0);
+    const int Co = (hid ? H : 0) + (enc ? INo + 2 * F : 0);
     const std::vector<float>& W = s->host_w[l];
     const int nrb = outl ? 1 : NB;
     const int ks = (hid ? 2 * NB : 0) + (enc ? 9 : 0);
@@ -570,7 +609,8 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
               const int c = enc_col(st - (hid ? 2 * NB : 0), hf, j);
               col = c < 0 ? -1 : (hid ? H : 0) + c;
             }
-            const float v = (row < R && col >= 0 && col < C) ? W[(size_t)row * C + col] : 0.f;
+            const float v = (row < R && col >= 0 && col < C)
+                                ? weight_at(W, row, col, hid ? H : 0, Co) : 0.f;
             fr[lane * 8 + j] = (_Float16)v;
           }
         }
@@ -606,10 +646,14 @@ static int build_nerf_program(const nrt_mlp* f, const nrt_mlp* s, nrt_prog& out)
   const size_t o_coff = a256(stream_bytes);
   const size_t o_bias = a256(o_coff + coff.size() * 4);
   const size_t o_basis = a256(o_bias + bias.size() * 4);
-  const size_t total = a256(o_basis + basis.size() * 16);
+  const size_t o_light = a256(o_basis + basis.size() * 16);
+  const size_t total = a256(o_light + 16);
   char* buf = nullptr;
   NRT_HIP(hipMalloc((void**)&buf, total));
   out.buf = buf;
+  const float unit[4] = {1.f, 0.f, 0.f, 0.f};
+  NRT_HIP(hipMemcpy(buf + o_light, unit, sizeof(unit), hipMemcpyHostToDevice));
+  out.unit_light = env != nullptr ? reinterpret_cast<const float*>(buf + o_light) : nullptr;
   NRT_HIP(hipMemcpy(buf, frags.data(), stream_bytes, hipMemcpyHostToDevice));
   NRT_HIP(hipMemcpy(buf + o_coff, coff.data(), coff.size() * 4, hipMemcpyHostToDevice));
   NRT_HIP(hipMemcpy(buf + o_bias, bias.data(), bias.size() * 4, hipMemcpyHostToDevice));
@@ -636,8 +680,8 @@ size_t nrt_nerfle_workspace_bytes(int64_t P, int32_t S, int32_t light_dim) {
 
 size_t nrt_nerfle_workspace_bytes_for(const nrt_mlp* first, const nrt_mlp* second, int64_t P,
                                        int32_t S, int32_t light_dim, int32_t precision) {
-  if (first && second && precision == NRT_FP16 && option(OPT_NERF_FUSED) != 0 && light_dim == 3 &&
-      nerf_fusable(first, second)) {
+  if (first && second && precision == NRT_FP16 && option(OPT_NERF_FUSED) != 0 && light_dim >= 3 &&
+      second->host_dev.in_size == 67 + light_dim && nerf_fusable(first, second)) {
     // fused k_nerfle16: alpha_raw [P S] + rgb_raw [P S, 3]
     const size_t n = (size_t)std::max<int64_t>(P, 1) * (size_t)std::max(S, 1);
     return a256(n * 4) + a256(n * 12);
@@ -673,13 +717,25 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
   char* ws = (char*)workspace;
   if (precision == NRT_FP16 && option(OPT_NERF_FUSED) != 0 &&
       nerf_fusable(first, second)) {
-    if (!second->nerf_prog || second->nerf_first_serial != first->serial) {
+    // NeRF+LE: the envmap (one constant per frame) is folded into the program; the host copy of
+    // it decides whether the cached program still holds (one small read-back per call)
+    std::vector<float> env;
+    if (light_dim != 3) {
+      env.resize((size_t)light_dim);
+      NRT_HIP(hipMemcpyAsync(env.data(), light, env.size() * 4, hipMemcpyDeviceToHost, st));
+      NRT_HIP(hipStreamSynchronize(st));
+    }
+    if (!second->nerf_prog || second->nerf_first_serial != first->serial ||
+        second->nerf_env != env) {
       std::unique_ptr<nrt_prog> pr(new nrt_prog());
-      if (int rc = build_nerf_program(first, second, *pr)) return rc;
+      if (int rc = build_nerf_program(first, second, *pr, env.empty() ? nullptr : env.data()))
+        return rc;
       second->nerf_prog = std::move(pr);
       second->nerf_first_serial = first->serial;
+      second->nerf_env = env;
     }
     const ProgDev& pd = second->nerf_prog->d;
+    if (!env.empty()) light = second->nerf_prog->unit_light;
     float* alpha = (float*)ws;
     float* rgb_raw = (float*)(ws + a256(n * 4));
     auto kern = k_nerfle16<kNerfWaves>;

@@ -37,6 +37,8 @@ struct nrt_mlp {
   // fused NeRFLE program built for (nerf_first, this) on first use (nrt_api_nerf.hip)
   mutable std::unique_ptr<nrt_prog> nerf_prog;
   mutable uint64_t nerf_first_serial = 0;
+  // NeRF+LE: the envmap the program's folded light column was built for (empty: point light)
+  mutable std::vector<float> nerf_env;
   uint64_t serial = 0;  // unique per created MLP (cache key; addresses can be reused)
   // nrt_mlp_refresh (nrt_refresh.hip): gather maps of the per-kernel fragment arrays, built on
   // the first refresh; after a refresh the FP16 ring / program streams and the host copies
@@ -65,6 +67,7 @@ struct nrt_mlp {
 struct nrt_prog {
   nrt::ProgDev d{};
   void* buf = nullptr;
+  const float* unit_light = nullptr;  // NeRF+LE fold: (1, 0, 0) in buf, the kernel's light input
   bool ok = false;       // false: some MLP has a shape without a compiled program kernel
   ~nrt_prog() { if (buf) (void)hipFree(buf); }
 };

@@ -292,6 +292,10 @@ class Path(Integrator):
     bounce) replaces the draws, for parity tests.
     """
 
+    # secondary intersections march only the rays whose path is still active (compacted on the
+    # device; the same per-ray results as marching every spawned ray)
+    compact = True
+
     def __init__(self, training=False, **kwargs):
         super().__init__(**kwargs)
         self.training = training
@@ -343,13 +347,34 @@ class Path(Integrator):
                       _lib.ptr(curr.wi.reshape(P, 3).contiguous()), P, _lib.ptr(act),
                       _lib.ptr(thr), _lib.ptr(res), _lib.ptr(u_comp), _lib.ptr(u_sel),
                       _lib.ptr(rays_out), _lib.ptr(ws), _lib.precision_code(), _lib.stream())
-            if depth + 1 == self.max_depth or not bool(act.any()):
+            if depth + 1 == self.max_depth:
                 break  # the reference's last spawn is never shaded (:309, :342)
-            curr, hits = shapes.intersect(rays_out.reshape(*lead, 6), primary=False)
-            act &= hits.reshape(-1).to(torch.uint8)
+            # the spawned rays of the still-active paths only (one host synchronisation, as the
+            # reference's act.any()): marching the dead ones would change nothing but the time
+            live = torch.nonzero(act).reshape(-1)
+            if live.numel() == 0:
+                break
+            if self.compact and live.numel() < P:
+                sub, hits = shapes.intersect(rays_out.index_select(0, live), primary=False)
+                curr = _Scattered(sub, live, P, dev)
+                act.zero_().index_copy_(0, live, hits.reshape(-1).to(torch.uint8))
+            else:
+                curr, hits = shapes.intersect(rays_out.reshape(*lead, 6), primary=False)
+                act &= hits.reshape(-1).to(torch.uint8)
             if not bool(act.any()):
                 break
         return result, original_active, it
+
+
+class _Scattered:
+    """The p / n / wi of a compacted secondary intersection (rays `live` of P) in the full ray
+    order nrt_path_bounce reads; rays off the list keep zeros (they are inactive)."""
+
+    def __init__(self, sub, live, P, dev):
+        for name in ("p", "n", "wi"):
+            full = torch.zeros(P, 3, device=dev)
+            full.index_copy_(0, live, getattr(sub, name).reshape(-1, 3))
+            setattr(self, name, full)
 
 
 class NeRFReproduce(Integrator):

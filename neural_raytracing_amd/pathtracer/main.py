@@ -79,6 +79,51 @@ def _row_separable(integrator, shapes, addition, trim, bsdf, lights, w_isect):
     return type(integrator) is NeRFReproduce and isinstance(shapes, NeRFLE)
 
 
+# pathtrace(Path) marches all tiles of a frame in one batch (_path_tiles); False: tile by tile
+BATCH_PATH = True
+
+
+def _path_batchable(integrator, shapes, lights, cameras, addition, trim, bsdf, w_isect):
+    """Path (integrators.py:275-354) without the coarse scan over a packed SDF, one light for
+    every camera, no addition hook / trim / gradients: its tiles can run as one batch."""
+    from .integrators import Path
+    if not BATCH_PATH or type(integrator) is not Path or integrator.training:
+        return False
+    if addition is not nothing or trim or not hasattr(cameras, "rays_tile"):
+        return False
+    if not hasattr(shapes, "sdf") or not is_hip_sdf(shapes.sdf):
+        return False
+    if getattr(lights, "per_camera", lambda: None)() is not None:
+        return False
+    return not needs_grad(shapes, bsdf, lights, w_isect)
+
+
+def _path_tiles(integrator, shapes, lights, cameras, bsdf, out, tiles, chunk, size, bundle_size,
+                sampler, with_noise, background, w_isect, device):
+    """pathtrace's tile loop for Path as few Path.sample calls as possible (SURVEY §8f rank 3,
+    path_nerv.py:86-104: 200^2 in 100^2 tiles, 32 passes a frame): the rays of consecutive tiles
+    (each tile's camera jitter drawn in tile order) are concatenated along the camera axis, so one
+    primary march, one nrt_path_bounce and one compacted secondary march per bounce serve them
+    all, and each tile is composited from its slice.  Per ray the same arithmetic as the tile
+    loop; the sampler's draws are taken per batch instead of per tile (every draw is still one
+    independent uniform per ray and component: the same distribution, a different stream --
+    like the reference's torch.multinomial, which this path already replaces by an inverse CDF)."""
+    N = len(cameras)
+    per_tile = N * chunk * chunk
+    step = max(1, _render.MAX_BATCH_RAYS // per_tile)
+    it = None
+    for t0 in range(0, len(tiles), step):
+        batch = tiles[t0:t0 + step]
+        rays = torch.cat([_tile_rays(cameras, x0, y0, chunk, size, sampler, bundle_size, N,
+                                     with_noise, device) for x0, y0 in batch], dim=0)
+        values, mask, it = integrator.sample(shapes, rays, bsdf=bsdf, lights=lights,
+                                             sampler=sampler, w_isect=w_isect)
+        for k, (x0, y0) in enumerate(batch):
+            _composite(out, values[k * N:(k + 1) * N], mask[k * N:(k + 1) * N], background, x0,
+                       y0, chunk)
+    return it
+
+
 def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=None, height=None,
               chunk_size=32, bundle_size=4, background=1, addition=nothing, sampler=Sampler(),
               silent=False, trim=0, device="cuda", squeeze_first=True, w_isect=False,
@@ -146,6 +191,10 @@ def pathtrace(shapes, lights, cameras, integrator, bsdf=None, size=512, width=No
         # every tile in the reference's order, batched into few launch chains (render.py)
         _render.render_tiles(fused, shapes, lights, cameras, bsdf, dst, tiles, chunk_size, size,
                              with_noise, background, rows=rows)
+    elif sh is None and _path_batchable(integrator, shapes, lights, cameras, addition, trim, bsdf,
+                                        w_isect):
+        it = _path_tiles(integrator, shapes, lights, cameras, bsdf, out, tiles, chunk_size, size,
+                         bundle_size, sampler, with_noise, background, w_isect, device)
     else:
         sel = None if rows is None else torch.tensor(rows, dtype=torch.long, device=device)
         R = chunk_size if rows is None else len(rows)

@@ -858,11 +858,18 @@ def test_nerfle_depth_counts(prec, steps, monkeypatch):
     assert (got - want).abs().max().item() <= tol, (got - want).abs().max()
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp16-unfused"])
 def test_nerfle_envmap_matches_oracle(prec):
     """NeRFLE(envmap=True) (NeRF+LE, nerf.py:183-191): the colour MLP's light input is the point
-    light's envmap at 16 directions (nrt_light_envmap) -> second MLP 115 -> 3."""
+    light's envmap at 16 directions (nrt_light_envmap) -> second MLP 115 -> 3.  "fp16" runs the
+    fused k_nerfle16 with the envmap folded into one constant input column (build_nerf_program),
+    "fp16-unfused" the per-MLP kernels on the 115 inputs."""
     from neural_raytracing_amd import set_precision
+    if prec == "fp16-unfused":
+        _lib_opt("nerf_fused", 0)
+        prec = "fp16"
+    else:
+        _lib_opt("nerf_fused", 1)
     from neural_raytracing_amd.pathtracer.lights import PointLights
     ref, mine = _nerfle_pair(29, envmap=True)
     g = torch.Generator().manual_seed(5)
@@ -881,9 +888,54 @@ def test_nerfle_envmap_matches_oracle(prec):
     random.seed(6)
     with torch.no_grad():
         want = ref(rays, None, jitter=random.random(), light=lref)
+    _lib_opt("nerf_fused", 1)
     assert got.shape == want.shape == (1, 9, 7, 1, 3)
     tol = 1e-4 if prec == "fp32" else 2e-2
     assert (got - want).abs().max().item() <= tol, (got - want).abs().max()
+
+
+def test_nerfle_envmap_fused_psnr_and_refold():
+    """NeRF+LE on the fused FP16 kernel over 2,048 rays x 64 depths: PSNR against the oracle
+    (FP32 arithmetic) at least the unfused FP16 path's less 3 dB and above 60 dB; a changed light
+    (another envmap) rebuilds the folded program, a repeated one reuses it (same bits)."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    ref, mine = _nerfle_pair(31, envmap=True)
+    g = torch.Generator().manual_seed(9)
+    o = torch.tensor([0.0, 0.2, 1.2]) + 0.1 * torch.randn(1, 32, 64, 1, 3, generator=g)
+    d = F.normalize(torch.cat([torch.rand(1, 32, 64, 1, 2, generator=g) - 0.5,
+                               -torch.ones(1, 32, 64, 1, 1)], -1), dim=-1)
+    rays = torch.cat([o, d], -1)
+
+    def psnr(a, b):
+        mse = float(((a - b) ** 2).mean())
+        return 10 * math.log10(float(b.abs().max()) ** 2 / mse) if mse > 0 else float("inf")
+    res = {}
+    for kw in (dict(intensity=(0.9, 0.5, 0.3), location=(0.3, 1.0, 0.2), scale=3.0),
+               dict(intensity=(0.2, 0.8, 0.6), location=(-0.5, 0.7, 0.4), scale=2.0)):
+        lref = R.PointLightRef(**kw)
+        lights = PointLights(intensity=list(kw["intensity"]), location=list(kw["location"]),
+                             scale=kw["scale"], device="cuda")
+        random.seed(2)
+        with torch.no_grad():
+            want = ref(rays, None, jitter=random.random(), light=lref)
+        set_precision("fp16")
+        outs = {}
+        for fused in (1, 0, 1):
+            _lib_opt("nerf_fused", fused)
+            random.seed(2)
+            with torch.no_grad():
+                outs.setdefault(fused, []).append(mine(rays.cuda(), lights).cpu())
+        _lib_opt("nerf_fused", 1)
+        set_precision("fp32")
+        fused_a, fused_b = outs[1]
+        assert torch.equal(fused_a, fused_b)
+        res[kw["scale"]] = (psnr(fused_a, want), psnr(outs[0][0], want), fused_a)
+        report("nerfle_envmap_fused_psnr", scale=kw["scale"], fused_db=res[kw["scale"]][0],
+               unfused_db=res[kw["scale"]][1])
+    for fused_db, unfused_db, _ in res.values():
+        assert fused_db >= min(unfused_db - 3.0, 80.0) and fused_db > 60.0, res
+    assert not torch.equal(res[3.0][2], res[2.0][2])  # the second light was not served stale
 
 
 def test_nerfle_pathtrace_nerf_reproduce():
@@ -987,3 +1039,80 @@ def test_path_integrator_matches_oracle(prec, w_isect):
     else:  # measured 1.7e-4 max, 46 of 2304 pixels > 1e-4
         assert err.max().item() <= 1e-3, err.max()
         assert int((err > 1e-4).sum()) <= 0.05 * err.numel()
+
+
+@pytest.mark.parametrize("prec,w_isect", [("fp32", True), ("fp32", False), ("mixed", True)])
+def test_path_batched_tiles_and_compaction_bit_equal(prec, w_isect):
+    """Path on pathtrace's batched tiles (main._path_tiles): four 24^2 tiles concatenated into
+    one Path.sample -- one primary march, one bounce kernel and one compacted secondary march per
+    bounce -- equal the four tiles sampled one at a time, and the compacted secondary march
+    (Path.compact, the live spawned rays only) equals marching every spawned ray, bit for bit,
+    with the same injected uniforms (integrators.py:309-350)."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    _, mine = _path_pair()
+    c2w = recipes.look_at_c2w((0.1, 0.5, 0.9)).unsqueeze(0)
+    ocam = R.NeRFCameraRef(c2w, recipes.nerf_focal(48))
+    tiles = [ocam.sample_positions(R._tile_positions(x0, y0, 24), 48)
+             for x0 in (0, 24) for y0 in (0, 24)]
+    g = torch.Generator().manual_seed(17)
+    lead = tiles[0].shape[:-1]
+    unif = [[(torch.rand(*lead, 3, 2, generator=g), torch.rand(*lead, generator=g))
+             for _ in range(2)] for _ in tiles]
+    set_precision(prec)
+    try:
+        with torch.no_grad():
+            per_tile = [Path().sample(mine["shape"], t.cuda(), mine["bsdf"], lights=mine["lights"],
+                                      w_isect=w_isect, uniforms=u) for t, u in zip(tiles, unif)]
+            cat_u = [tuple(torch.cat([u[d][i] for u in unif], 0) for i in range(2))
+                     for d in range(2)]
+            batched, bmask, _ = Path().sample(mine["shape"], torch.cat(tiles, 0).cuda(),
+                                              mine["bsdf"], lights=mine["lights"],
+                                              w_isect=w_isect, uniforms=cat_u)
+            full = Path()
+            full.compact = False
+            uncompacted, umask, _ = full.sample(mine["shape"], torch.cat(tiles, 0).cuda(),
+                                                mine["bsdf"], lights=mine["lights"],
+                                                w_isect=w_isect, uniforms=cat_u)
+    finally:
+        set_precision("fp32")
+    assert torch.equal(torch.cat([v for v, _, _ in per_tile], 0), batched)
+    assert torch.equal(torch.cat([m for _, m, _ in per_tile], 0), bmask)
+    assert torch.equal(batched, uncompacted) and torch.equal(bmask, umask)
+    assert float(bmask.float().mean()) > 0.2 and float(batched.abs().max()) > 0
+
+
+def test_pathtrace_path_batches_its_tiles(monkeypatch):
+    """pathtrace(integrator=Path(), w_isect=True) (path_nerv.py:86-99) calls Path.sample once for
+    all its tiles and composites each tile from its slice; with BATCH_PATH off it calls it per
+    tile.  Both frames have the same hit mask (the primary march) and background."""
+    from neural_raytracing_amd import set_precision
+    from neural_raytracing_amd.pathtracer import main
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    import neural_raytracing_amd.pathtracer as pt
+    _, mine = _path_pair()
+    set_precision("fp32")
+    calls = []
+    orig = Path.sample
+
+    def spy(self, shapes, rays, bsdf, **kw):
+        calls.append(tuple(rays.shape))
+        return orig(self, shapes, rays, bsdf, **kw)
+    monkeypatch.setattr(Path, "sample", spy)
+    cam = pt.cameras.NeRFCamera(cam_to_world=recipes.look_at_c2w((0.1, 0.5, 0.9)).unsqueeze(0).cuda(),
+                                focal=recipes.nerf_focal(48), device="cuda")
+    frames = []
+    for batch in (True, False):
+        monkeypatch.setattr(main, "BATCH_PATH", batch)
+        calls.clear()
+        torch.manual_seed(0)
+        random.seed(0)
+        with torch.no_grad():
+            img, _ = pt.pathtrace(mine["shape"], mine["lights"], cam, Path(), bsdf=mine["bsdf"],
+                                  size=48, chunk_size=24, bundle_size=1, background=0,
+                                  device="cuda", w_isect=True)
+        frames.append((img.cpu(), list(calls)))
+    (fb, cb), (ft, ct) = frames
+    assert cb == [(4, 24, 24, 1, 6)] and ct == [(1, 24, 24, 1, 6)] * 4
+    assert torch.equal(fb.abs().sum(-1) > 0, ft.abs().sum(-1) > 0)  # the same lit pixels
+    assert float((fb.abs().sum(-1) > 0).float().mean()) > 0.2
