@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-extra-legs", action="store_true",
                     help="skip the FP32 (reference precision) and scan-free timing legs")
     ap.add_argument("--scene", default="nerf_synthetic",
-                    choices=["nerf_synthetic", "colocate", "dtu", "nerfle", "train"],
+                    choices=["nerf_synthetic", "colocate", "dtu", "nerfle", "train", "path"],
                     help="nerf_synthetic = the BASELINE metric (default); the others are "
                          "BASELINE.json configs[2..4] as one-GPU workloads")
     ap.add_argument("--views", type=int, default=6, help="--scene train: views per step (N)")
@@ -82,6 +82,12 @@ def parse():
             args.size = 256
         if args.samples is None:
             args.samples = 64
+        return args
+    if args.scene == "path":
+        if args.size is None:
+            args.size = 200  # path_nerv.py:27 SIZE
+        if args.samples is None:
+            args.samples = 64  # path_nerv.py:48 max_steps
         return args
     big = args.scene == "nerfle"
     if args.size is None:
@@ -230,6 +236,8 @@ def main():
     args = parse()
     if args.scene == "train":
         return bench_train(args)
+    if args.scene == "path":
+        return bench_path(args)
     if args.scene != "nerf_synthetic":
         return bench_other(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -941,6 +949,192 @@ def _committed_pmc(kernel, scene, size, precision):
     return pm.get("hbm_bytes_per_launch"), (f"committed PMC pass, profiles/pmc_{scene}_{kernel}"
                                             f".json ({size}^2 {precision}); not measured in "
                                             "this run")
+
+
+PATH_PASSES = 32  # path_nerv.py:86 run_tests(num_samples=32): pathtrace passes per frame
+PATH_LIGHT = (0.8, 1.0, 0.6)
+# the march kernels of a Path frame per precision: the primary / secondary march and the shadow
+# march (k_occl*: intersect_test toward the point light, w_isect=True)
+PATH_KERNELS = {"fp32": ("k_march32", "k_occl32"), "fp16": ("k_march16", "k_occl16"),
+                "fp32-split": ("k_march3", "k_occl3"), "mixed": ("k_march16", "k_occl3")}
+
+
+def build_path_scene(device, samples, seed=0):
+    """path_nerv.py's scene (scripts/path_nerv.py:42-99; the models nerv.py:84-95 trains), seeded
+    random init: SDF(SphereSDF(n=128)) with max_steps 64 (radii + 0.15 and the 8x128 F32 shift at
+    default torch init, output x0.1, so the random blob has a surface), ComposeSpatialVarying of 7
+    NeuralBSDFs with act = sigmoid (path_nerv.py:52), PointLights(intensity 1, scale 300)."""
+    import neural_raytracing_amd.pathtracer as pt
+    from neural_raytracing_amd.pathtracer.bsdf import ComposeSpatialVarying, NeuralBSDF
+    from neural_raytracing_amd.pathtracer.lights import PointLights
+    from neural_raytracing_amd.pathtracer.neural_blocks import SkipConnMLP
+    from neural_raytracing_amd.pathtracer.shapes import SDF, SphereSDF
+    torch.manual_seed(seed)
+    random.seed(seed)
+    sphere = SphereSDF(n=128, device="cpu")
+    with torch.no_grad():
+        sphere.radii.add_(0.15)
+    sphere.shift = SkipConnMLP(num_layers=8, hidden_size=128, in_size=3, out=1, freqs=32,
+                               activation=F.softplus, device="cpu")
+    with torch.no_grad():
+        sphere.shift.out.weight.mul_(0.1)
+        sphere.shift.out.bias.mul_(0.1)
+    shape = SDF(sdf=sphere.to(device), max_steps=samples)
+    # act = sigmoid as path_nerv.py:52 sets it on the loaded models (here at construction: on a
+    # NeuralBSDF built with a Softplus module, torch refuses the setattr of a function)
+    comps = [NeuralBSDF(activation=torch.sigmoid, device="cpu") for _ in range(7)]
+    for c in comps:
+        c.mlp.to(device)
+    bsdf = ComposeSpatialVarying(comps, device="cpu")
+    bsdf.sp_var_fn.to(device)
+    lights = PointLights(intensity=[1.0, 1.0, 1.0], location=list(PATH_LIGHT), scale=300.0,
+                         device=device)
+    return dict(shape=shape, bsdf=bsdf, lights=lights, pt=pt)
+
+
+def bench_path(args):
+    """`--scene path`: path_nerv.py's render (scripts/path_nerv.py:86-104) -- Path() (max_depth 2,
+    the secondary-ray integrator of BASELINE cfg5, integrators.py:275-354) with shadow rays
+    (w_isect=True), 200^2 in 100^2 tiles, 32 pathtrace passes averaged per frame.  One step = one
+    frame; the unit is the metric's ray-sample (primary rays x max_steps, W H S per pass).  The
+    passes run on pathtrace's batched Path (main._path_tiles: all tiles in one primary march, one
+    bounce kernel and one compacted secondary march per bounce); the `per_tile` leg times the
+    tile-by-tile loop of the reference.  Roofline: the march kernels (primary, secondary, shadow)
+    over the SDF evaluations they executed (device counter).  One view per rank (replicas: the
+    passes' draws depend on the ray count, so rows are not dealt; the MAX time over ranks)."""
+    from neural_raytracing_amd import _lib
+    import neural_raytracing_amd as nra
+    from neural_raytracing_amd.pathtracer import main as ptmain
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    world, rank, local, dist_on = _dist_env()
+    if dist_on:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    _lib.load(require_device=True)
+    nra.set_precision(args.precision)
+    size, S = args.size, args.samples
+    sc = build_path_scene(device, S)
+    pt = sc["pt"]
+    focal = float(0.5 * size / math.tan(0.5 * 0.6911))
+    cam = pt.cameras.NeRFCamera(cam_to_world=view_c2w(rank, max(world, 1))[None].to(device),
+                                focal=focal, device=device)
+    integrator = Path()
+    chunk = min(size, 100)
+
+    def frame():
+        got = None
+        for _ in range(PATH_PASSES):
+            sample = pt.pathtrace(sc["shape"], size=size, chunk_size=chunk, bundle_size=1,
+                                  bsdf=sc["bsdf"], integrator=integrator, background=0,
+                                  cameras=cam, lights=sc["lights"], device=device, silent=True,
+                                  w_isect=True)[0]
+            got = sample if got is None else got + sample
+        return got / PATH_PASSES
+    kernels = PATH_KERNELS[args.precision]
+    with torch.no_grad():
+        el, ks, evals = _time_frames(frame, args.steps, args.warmup,
+                                     list(kernels) + ["k_path_sample", "k_light16", "k_bsdf16"])
+        elapsed = max_over_ranks(el, world, device, force=dist_on)
+        img = frame()
+        lit = float((img.abs().sum(-1) > 0).float().mean())
+        ptmain.BATCH_PATH = False
+        try:
+            el_tile, _, _ = _time_frames(frame, 1, 1, [])
+        finally:
+            ptmain.BATCH_PATH = True
+    rays_frame = size * size * PATH_PASSES
+    k_ms = sum(ks[k][0] for k in kernels) / args.steps
+    peak = PEAK_TFLOPS[args.precision]
+    products = 3 if args.precision == "fp32-split" else 1
+    exe_flop = evals * FLOP_SHIFT_8x128 * products
+    ach = exe_flop / (k_ms * 1e-3) / 1e12
+    roof = {"bound": "mfma", "kernel": "+".join(kernels), "achieved": ach, "peak": peak,
+            "unit": "TFLOP/s", "frac": ach / peak, "executed_frac": ach / peak, "traffic": None,
+            "flop_basis": "executed: the SDF evaluations the primary, secondary and shadow "
+                          "marches ran in one frame (device counter) x the 8x128 F32 shift MLP's "
+                          f"{FLOP_SHIFT_8x128} FLOP (the 128 spheres' smooth-min is VALU, not "
+                          "counted)",
+            "executed_evals_per_frame": evals,
+            "executed_evals_per_primary_ray": evals / rays_frame,
+            "kernel_ms_per_frame": k_ms,
+            "kernels_ms_per_frame": {k: ks[k][0] / args.steps for k in ks}}
+    line = {
+        "metric": f"ray-samples/sec/GPU (path {size}x{size}x{S}, {PATH_PASSES} passes)",
+        "value": world * rays_frame * S * args.steps / elapsed, "unit": "ray-samples/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1000 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": args.precision,
+        "data": "synthetic (seeded random-init weights)",
+        "config": {"workload": f"path_nerv.py-like: Path() max_depth 2 with shadow rays "
+                               f"(w_isect=True), {size}^2 in {chunk}^2 tiles, {PATH_PASSES} "
+                               f"passes per frame, SDF(SphereSDF(n=128) + 8x128 F32 shift), "
+                               f"max_steps {S}, ComposeSpatialVarying(7 x NeuralBSDF, sigmoid), "
+                               f"PointLights(scale 300)",
+                   "image": [size, size], "samples_per_ray": S, "passes_per_frame": PATH_PASSES,
+                   "parallelism": f"replicas x{world} (one view per rank)"},
+        "roofline": roof,
+        "lit_fraction": round(lit, 4),
+        "per_tile": {"ms_per_step": 1000 * el_tile,
+                     "note": "the same frame with pathtrace's tile loop (BATCH_PATH off: one "
+                             "Path.sample per 100^2 tile, as the reference)"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = path_cpu_baseline(sc, cam, size, S)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        torch.distributed.destroy_process_group()
+
+
+def path_cpu_baseline(sc, cam, size, S, crop=24):
+    """The oracle's PathRef (oracle/pathtracer_ref.py, 'port') on this host's threads: one pass of
+    a crop x crop window at the image centre with injected uniforms, and the GPU Path.sample of
+    the same rays and uniforms beside it (max |diff|)."""
+    from oracle import pathtracer_ref as R
+    from neural_raytracing_amd.pathtracer.integrators import Path
+    blob = R.SphereBlobSDF(n=128)
+    src = sc["shape"].sdf
+    with torch.no_grad():
+        blob.centers.copy_(src.centers.cpu())
+        blob.radii.copy_(src.radii.cpu())
+        blob.tfs.copy_(src.tfs.cpu())
+    _copy_to_oracle(blob.shift, src.shift)
+    parts = [R.NeuralBSDFRef(activation="sigmoid") for _ in sc["bsdf"].bsdfs]
+    for o, p in zip(parts, sc["bsdf"].bsdfs):
+        _copy_to_oracle(o.mlp, p.mlp)
+    bsdf = R.SpatialMixBSDF(parts)
+    _copy_to_oracle(bsdf.sp_var_fn, sc["bsdf"].sp_var_fn)
+    shape = R.MarchedSDF(sdf=blob, max_steps=S)
+    lights = R.PointLightRef(location=PATH_LIGHT, scale=300.0)
+    c0 = (size - crop) // 2
+    ocam = R.NeRFCameraRef(cam.cam_to_world.cpu(), cam.focal)
+    rays = ocam.sample_positions(R._tile_positions(c0, c0, crop), size)
+    g = torch.Generator().manual_seed(5)
+    lead = rays.shape[:-1]
+    nc = len(parts)
+    uniforms = [(torch.rand(*lead, nc, 2, generator=g), torch.rand(*lead, generator=g))
+                for _ in range(2)]
+    threads = torch.get_num_threads()
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        want, wmask, _ = R.PathRef().sample(shape, rays, bsdf, lights, w_isect=True,
+                                            uniforms=uniforms)
+    cpu_s = time.perf_counter() - t0
+    with torch.no_grad():
+        got, gmask, _ = Path().sample(sc["shape"], rays.cuda(), sc["bsdf"], lights=sc["lights"],
+                                      w_isect=True, uniforms=uniforms)
+    err = (got.cpu() - want).abs()
+    return {"value": crop * crop * S / cpu_s, "unit": "ray-samples/s", "cores": threads,
+            **host_cpu(), "kind": "port",
+            "sample": f"one Path pass (max_depth 2, shadow rays) over a {crop}x{crop} window at "
+                      f"the image centre with injected uniforms, oracle/pathtracer_ref.py "
+                      f"PathRef, {cpu_s:.1f} s",
+            "gpu_vs_port_maxabs": float(err.max()),
+            "gpu_vs_port_pixels_over_1e-4": int((err.amax(-1) > 1e-4).sum()),
+            "mask_equal": bool(torch.equal(gmask.cpu(), wmask)), "hits": int(wmask.sum())}
 
 
 # VALU operations per SDF evaluation of the colocate scene's SphereSDF(n=64) (sdfs.py:37-43,
