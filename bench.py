@@ -910,9 +910,15 @@ def bench_other(args):
                 ex_ms += _lib.profile_read(k)[0]
             roof["executed_achieved"] = exe / (ex_ms * 1e-3) / 1e12
             roof["executed_frac"] = roof["executed_achieved"] / peak
+    if sc["kind"] != "march":
+        # every sample of every ray is evaluated (no early stop): executed = algorithmic, up to
+        # the k_nerfle16 program's padding (which the algorithmic count does not price)
+        roof["executed_frac"] = roof["frac"]
     pmc = _committed_pmc(kernel, args.scene, size, args.precision)
     if pmc is not None:
         roof["traffic"], roof["traffic_source"] = pmc
+        if sc["kind"] != "march":
+            roof["traffic_note"] = "per launch: the frame runs in %d launches" % max(k_n // max(args.steps, 1), 1)
     line = {
         "metric": f"ray-samples/sec/GPU ({args.scene} {size}x{size}x{args.samples})",
         "value": rays_total * args.samples / elapsed, "unit": "ray-samples/s", "n_gpus": world,
@@ -1061,6 +1067,10 @@ def bench_path(args):
             "executed_evals_per_primary_ray": evals / rays_frame,
             "kernel_ms_per_frame": k_ms,
             "kernels_ms_per_frame": {k: ks[k][0] / args.steps for k in ks}}
+    pmc = _committed_pmc(kernels[0], "path", size, args.precision)
+    if pmc is not None:
+        roof["traffic"], roof["traffic_source"] = pmc
+        roof["traffic_note"] = "one launch of the primary march (40,000 rays) of the first pass"
     line = {
         "metric": f"ray-samples/sec/GPU (path {size}x{size}x{S}, {PATH_PASSES} passes)",
         "value": world * rays_frame * S * args.steps / elapsed, "unit": "ray-samples/s",
@@ -1184,28 +1194,51 @@ def bench_train(args):
 TRAIN_KERNELS = ("k_mlp_backward32", "k_wgrad", "k_mlp_grad_backward32")
 
 
-def train_roofline(steps):
-    """Roofline of the training step's backward launches over the timed steps: per kernel the
-    algorithmic FLOP the library recorded (nrt_profile_flop: the MLP backward's forward recompute
-    + input-gradient chain, the split-K weight gradients, the SDF normal's double backward, at
-    the layers' real widths) over its HIP-event time, against the 157.3 TF FP32 matrix peak; the
-    headline entry is the kernel with the most time."""
-    from neural_raytracing_amd import _lib
+TRAIN_MARCH = {"fp32": ("k_march32",), "mixed": ("k_march16", "k_refine3", "k_best3"),
+               "fp16": ("k_march16",), "fp32-split": ("k_march3",)}
+
+
+def train_roofline(steps, prec, march_evals, rays, kt, kf):
+    """Roofline of the training step over the timed steps, per kernel against the 157.3 TF FP32
+    matrix peak (the mixed / fp16 march against the 2.5 PF FP16 one):
+      * the gradient-free march + coarse scan (TRAIN_MARCH[prec]): EXECUTED FLOP = the SDF
+        evaluations its job lists ran (device counter over one more, untimed step, less the
+        sdf(best) pass's one per ray) x the SphereSDF shift MLP's 331,200 FLOP (8x128 F32; the 128
+        spheres' smooth-min is VALU, not counted) over the march kernels' HIP-event time;
+      * the backward launches: the algorithmic FLOP the library recorded (nrt_profile_flop: the MLP
+        backward's forward recompute + input-gradient chain, the split-K weight gradients, the SDF
+        normal's double backward, at the layers' real widths) over their HIP-event time.
+    kt: {kernel: (total ms, launches)} and kf: {kernel: FLOP} of the timed steps.  The headline
+    entry is the kernel with the most time."""
     per = {}
+    mk = TRAIN_MARCH[prec]
+    m_ms = sum(kt[k][0] for k in mk)
+    m_n = kt[mk[0]][1]
+    exe = max(march_evals - rays, 0) * FLOP_SHIFT_8x128 * steps
+    m_peak = PEAK_TFLOPS["fp32"] if prec == "fp32" else PEAK_TFLOPS["fp16"]
+    ach = exe / (m_ms * 1e-3) / 1e12 if m_ms > 0 else 0.0
+    per["+".join(mk)] = {"ms_per_step": m_ms / steps, "launches_per_step": m_n / steps,
+                         "flop_per_step": exe / steps, "achieved": ach, "peak": m_peak,
+                         "frac": ach / m_peak, "executed_frac": ach / m_peak,
+                         "executed_evals_per_ray": march_evals / max(rays, 1),
+                         "flop_basis": "executed SDF evaluations (device counter) x 331,200"}
     for k in TRAIN_KERNELS:
-        ms, n = _lib.profile_read(k)
-        flop = _lib.profile_flop(k)
+        ms, n = kt[k]
+        flop = kf[k]
         ach = flop / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         per[k] = {"ms_per_step": ms / steps, "launches_per_step": n / steps,
-                  "flop_per_step": flop / steps, "achieved": ach,
+                  "flop_per_step": flop / steps, "achieved": ach, "peak": PEAK_TFLOPS["fp32"],
                   "frac": ach / PEAK_TFLOPS["fp32"]}
     top = max(per, key=lambda k: per[k]["ms_per_step"])
-    return {"bound": "mfma", "kernel": top, "achieved": per[top]["achieved"],
-            "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s", "frac": per[top]["frac"],
-            "traffic": None, "flop_basis": "algorithmic: 2 FLOP per multiply-add of every layer "
-                                           "product at its real width (include/nrt.h "
-                                           "nrt_profile_flop)",
-            "kernels": per}
+    out = {"bound": "mfma", "kernel": top, "achieved": per[top]["achieved"],
+           "peak": per[top]["peak"], "unit": "TFLOP/s", "frac": per[top]["frac"],
+           "traffic": None, "flop_basis": per[top].get("flop_basis", "algorithmic: 2 FLOP per "
+                                                       "multiply-add of every layer product at "
+                                                       "its real width (nrt_profile_flop)"),
+           "kernels": per}
+    if "executed_frac" in per[top]:
+        out["executed_frac"] = per[top]["executed_frac"]
+    return out
 
 
 def train_leg(prec, steps, warmup, size=256, crop=80, views=6, samples=64, cpu=True,
@@ -1285,8 +1318,18 @@ def train_leg(prec, steps, warmup, size=256, crop=80, views=6, samples=64, cpu=T
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         _lib.profile_enable(False)
-        roof = train_roofline(steps)
-        kms = {k: _lib.profile_read(k)[0] / steps for k in ("k_intersect",) + TRAIN_KERNELS}
+        kms = {k: _lib.profile_read(k)[0] / steps
+               for k in ("k_intersect",) + TRAIN_MARCH[prec] + TRAIN_KERNELS}
+        kt = {k: _lib.profile_read(k) for k in TRAIN_MARCH[prec] + TRAIN_KERNELS}
+        kf = {k: _lib.profile_flop(k) for k in TRAIN_KERNELS}
+        # the march's executed evaluations: one more, untimed step with the device counter
+        _lib.profile_reset()
+        _lib.profile_enable(False, evals=True)
+        step(warmup + steps)
+        torch.cuda.synchronize()
+        march_evals = _lib.profile_evals()
+        _lib.profile_enable(False)
+        roof = train_roofline(steps, prec, march_evals, N * crop * crop, kt, kf)
     finally:
         nra.set_precision(old_prec)
     rays = N * crop * crop

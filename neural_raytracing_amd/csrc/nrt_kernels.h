@@ -489,7 +489,7 @@ struct OwnedRays {
 };
 
 // The SDF evaluator of a ring march: FP16 (32-ray tiles, ring::eval, fast sphere exp) or FP32
-// (16-ray tiles, ring32::eval, torch-exact transcendentals).  RPW rays per wave; lane l serves
+// (16-ray tiles, ring32::eval; softplus_exact -- a few ulp of torch's log1pf(expf), see nrt_device.h).  RPW rays per wave; lane l serves
 // ray l & (RPW - 1) and the other lanes of that ray mirror its state.
 template <int NB, int NE, int WV, bool FOLD>
 struct RingPol16 {
@@ -539,7 +539,7 @@ struct RingPol32 {
 };
 
 // FP32-accurate evaluation on FP16 matrix cores (nrt_ring3.h, the "fp32-split" precision):
-// 16-ray tiles like RingPol32, torch-exact transcendentals, sphere blobs as in ring32
+// 16-ray tiles like RingPol32 (softplus_exact: a few ulp of torch's), sphere blobs as in ring32
 template <int KH, int KQ, int WV, int ACT>
 struct RingPol3 {
   static constexpr int RPW = 16, WAVES = WV;

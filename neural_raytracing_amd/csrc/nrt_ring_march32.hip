@@ -1,6 +1,7 @@
 // FP32 (reference-precision) march + coarse scan on the block-cooperative LDS weight ring
 // (k_march32 / k_scan_best32, nrt_device.h ring32): same job lists and persistent grid as the
-// FP16 ring march (nrt_ring_march.hip), 16-ray tiles, torch-exact transcendentals.
+// FP16 ring march (nrt_ring_march.hip), 16-ray tiles; accurate sincosf / sqrtf / expf and
+// softplus_exact (a few ulp of torch's log1pf(expf), nrt_device.h).
 #include "nrt_launch.h"
 
 // waves per block of the 128-wide SDFs' FP32 ring march (timing experiments: -DNRT_R32_SMALL_WV)
