@@ -941,9 +941,9 @@ def bench_other(args):
 
 def _committed_pmc(kernel, scene, size, precision):
     """(HBM bytes per launch, source) from a committed PMC pass of this scene's kernel
-    (profiles/pmc_<scene>_<kernel>.json: FETCH_SIZE + WRITE_SIZE per launch, tools/pmc.sh), or
-    None; the pass must be of the same frame size and precision."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{scene}_{kernel}.json")
+    (profiles/pmc_<scene>_<precision>_<kernel>.json: FETCH_SIZE + WRITE_SIZE per launch,
+    tools/r06_pmc_scenes.sh), or None; the pass must be of the same frame size and precision."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{scene}_{precision}_{kernel}.json")
     if not os.path.exists(path):
         return None
     try:
@@ -952,9 +952,9 @@ def _committed_pmc(kernel, scene, size, precision):
         return None
     if pm.get("size") != size or pm.get("precision") != precision:
         return None
-    return pm.get("hbm_bytes_per_launch"), (f"committed PMC pass, profiles/pmc_{scene}_{kernel}"
-                                            f".json ({size}^2 {precision}); not measured in "
-                                            "this run")
+    return pm.get("hbm_bytes_per_launch"), (f"committed PMC pass, profiles/pmc_{scene}_"
+                                            f"{precision}_{kernel}.json ({size}^2); not measured "
+                                            "in this run")
 
 
 PATH_PASSES = 32  # path_nerv.py:86 run_tests(num_samples=32): pathtrace passes per frame

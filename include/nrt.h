@@ -495,6 +495,9 @@ int nrt_profile_read(const char* name, double* total_ms, int64_t* launches);
  * executed work behind the algorithmic count (every ray at every march step and scan point,
  * sdfs.py:119-131, 232-249), which the lane-level job lists lower.  Synchronises. */
 int nrt_profile_evals(uint64_t* evals);
+/* Rays the NRT_MIXED refinement re-marched on the split engine (the flagged rays, nrt_ring_mixed
+ * step 2) while NRT_PROF_EVALS was enabled, since the last nrt_profile_reset.  Synchronises. */
+int nrt_profile_refined(uint64_t* rays);
 /* Algorithmic FLOP of the timed launches of kernel `name` since the last nrt_profile_reset, as
  * the entries that launch it count them (the MLP backward and weight-gradient launches of the
  * training path: every multiply-add of the layers' products at their real widths, 2 FLOP each);

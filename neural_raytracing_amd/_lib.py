@@ -129,6 +129,7 @@ _SIGNATURES = {
     "nrt_profile_read": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                 ctypes.POINTER(_I64)]),
     "nrt_profile_evals": (_I32, [ctypes.POINTER(ctypes.c_uint64)]),
+    "nrt_profile_refined": (_I32, [ctypes.POINTER(ctypes.c_uint64)]),
     "nrt_profile_flop": (_I32, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]),
     "nrt_set_option": (_I32, [ctypes.c_char_p, _I64]),
     "nrt_get_option": (_I32, [ctypes.c_char_p, ctypes.POINTER(_I64)]),
@@ -259,6 +260,14 @@ def profile_evals():
     was enabled: the executed work behind an algorithmic FLOP count."""
     v = ctypes.c_uint64()
     check(load().nrt_profile_evals(ctypes.byref(v)), "nrt_profile_evals")
+    return v.value
+
+
+def profile_refined():
+    """Rays the NRT_MIXED refinement re-marched (flagged by the FP16 march) since the last reset
+    while evaluation counting was enabled."""
+    v = ctypes.c_uint64()
+    check(load().nrt_profile_refined(ctypes.byref(v)), "nrt_profile_refined")
     return v.value
 
 

@@ -72,8 +72,9 @@ unsigned long long* profile_eval_counter() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!g_evals[dev]) {
-    if (hipMalloc(&g_evals[dev], sizeof(unsigned long long)) != hipSuccess) { g_evals[dev] = nullptr; return nullptr; }
-    if (hipMemset(g_evals[dev], 0, sizeof(unsigned long long)) != hipSuccess) return nullptr;
+    // [0] SDF evaluations, [1] NRT_MIXED rays re-marched by the refinement
+    if (hipMalloc(&g_evals[dev], 2 * sizeof(unsigned long long)) != hipSuccess) { g_evals[dev] = nullptr; return nullptr; }
+    if (hipMemset(g_evals[dev], 0, 2 * sizeof(unsigned long long)) != hipSuccess) return nullptr;
   }
   return g_evals[dev];
 }
@@ -95,7 +96,7 @@ void nrt_profile_reset(void) {
   nrt::g_recs.clear();
   int dev = 0;
   if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && nrt::g_evals[dev])
-    (void)hipMemset(nrt::g_evals[dev], 0, sizeof(unsigned long long));
+    (void)hipMemset(nrt::g_evals[dev], 0, 2 * sizeof(unsigned long long));
 }
 
 int nrt_profile_evals(uint64_t* evals) {
@@ -107,6 +108,18 @@ int nrt_profile_evals(uint64_t* evals) {
   unsigned long long v = 0;
   NRT_HIP(hipMemcpy(&v, nrt::g_evals[dev], sizeof(v), hipMemcpyDeviceToHost));
   *evals = v;
+  return NRT_OK;
+}
+
+int nrt_profile_refined(uint64_t* rays) {
+  if (!rays) { set_error("nrt_profile_refined: null argument"); return NRT_EINVAL; }
+  *rays = 0;
+  int dev = 0;
+  NRT_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64 || !nrt::g_evals[dev]) return NRT_OK;
+  unsigned long long v = 0;
+  NRT_HIP(hipMemcpy(&v, nrt::g_evals[dev] + 1, sizeof(v), hipMemcpyDeviceToHost));
+  *rays = v;
   return NRT_OK;
 }
 

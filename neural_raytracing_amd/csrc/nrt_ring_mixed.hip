@@ -23,6 +23,10 @@
 
 namespace nrt {
 
+__global__ void k_add_count(const int32_t* __restrict__ count, unsigned long long* __restrict__ acc) {
+  if (threadIdx.x == 0) atomicAdd(acc, (unsigned long long)*count);
+}
+
 int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs& ma, float* t,
                      uint8_t* hit, float* p, float* n, float* raw_n, float* thr, int32_t* idx,
                      int32_t* cnt, unsigned long long* keys, char* ws, hipStream_t st) {
@@ -53,6 +57,8 @@ int ring_march_mixed(const nrt_sdf* s, const float* rays, int64_t P, const March
   k_refine_list<><<<dim3(std::min<int64_t>(ceil_div64(P, 256), 2048)), dim3(256), 0, st>>>(
       amb, P, list, lcount);
   if (int rc = check_launch("k_refine_list")) return rc;
+  if (ma.evals)  // profiling only: the flagged-ray count (nrt_profile_refined)
+    k_add_count<<<dim3(1), dim3(64), 0, st>>>(lcount, ma.evals + 1);
   MarchArgs mr = ma;
   mr.primary = 0;
   mr.scan_idx = nullptr;

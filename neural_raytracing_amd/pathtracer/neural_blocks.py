@@ -294,18 +294,24 @@ def diff_points(p):
     return q
 
 
-def _trainable_leaf(v):
-    return v is not None and v.requires_grad and not getattr(v, "_nrt_diff_points", False)
+def _trainable_leaf(v, x):
+    """A leaf of x's graph that takes gradients and is not the point set being differentiated:
+    an nn.Parameter, or a requires_grad tensor of another size than x (a learned pose or offset
+    held as a bare tensor).  A bare leaf with x's element count is the points themselves --
+    SDF.autograd_diff's p.requires_grad_() (sdfs.py:186), possibly warped into x -- as is a
+    diff_points leaf."""
+    if v is None or not v.requires_grad or getattr(v, "_nrt_diff_points", False):
+        return False
+    return isinstance(v, nn.Parameter) or v.numel() != x.numel()
 
 
 def _parameters_upstream(t, limit=20000):
-    """True when the autograd graph of `t` reaches a leaf that takes gradients -- an
-    nn.Parameter or any other requires_grad leaf (a learned pose or offset held as a bare tensor)
-    -- other than the point leaf of diff_points.  A graph larger than `limit` nodes counts as
+    """True when the autograd graph of `t` (the MLP's input) reaches a leaf that takes gradients
+    other than the point set itself (_trainable_leaf).  A graph larger than `limit` nodes counts as
     reaching one (the caller then refuses rather than dropping a term silently)."""
     fn = t.grad_fn
     if fn is None:
-        return _trainable_leaf(t)
+        return isinstance(t, nn.Parameter)
     seen, stack = set(), [fn]
     while stack:
         if len(seen) >= limit:
@@ -314,7 +320,7 @@ def _parameters_upstream(t, limit=20000):
         if f is None or f in seen:
             continue
         seen.add(f)
-        if _trainable_leaf(getattr(f, "variable", None)):  # AccumulateGrad of a leaf
+        if _trainable_leaf(getattr(f, "variable", None), t):  # AccumulateGrad of a leaf
             return True
         stack.extend(n for n, _ in getattr(f, "next_functions", ()))
     return False

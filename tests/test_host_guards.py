@@ -26,8 +26,12 @@ def test_bare_requires_grad_leaf_upstream():
     q = diff_points(torch.randn(5, 3))
     assert _parameters_upstream(q + offset)
     assert _parameters_upstream(offset.expand(5, 3) * 1.0)
-    plain = torch.randn(5, 3, requires_grad=True)  # an untagged leaf as the MLP's input itself
-    assert _parameters_upstream(plain)
+    # a bare leaf with the points' element count is the point set (sdfs.py:186's
+    # p.requires_grad_()), as the MLP input itself or warped into it
+    plain = torch.randn(5, 3, requires_grad=True)
+    assert not _parameters_upstream(plain)
+    assert not _parameters_upstream(plain * 2.0 + torch.sin(plain))
+    assert _parameters_upstream(plain + offset)
 
 
 def test_node_limit_counts_as_upstream():

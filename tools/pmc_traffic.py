@@ -6,7 +6,7 @@ Corrections (MI355X_MICROARCH.md, HBM): on gfx950 FETCH_SIZE reports half of the
 that access form); WRITE_SIZE counts bytes for 16-B stores and per-lane atomics; both are in KiB.
 Usage: python tools/pmc_traffic.py gpurun_out/pmc/p1 gpurun_out/pmc/p2 [size] [precision] [kernel]
        [scene] [profile-name]
-  scene: write profiles/pmc_<scene>_<profile-name>.json (bench.py --scene lines; profile-name is
+  scene: write profiles/pmc_<scene>_<precision>_<profile-name>.json (bench.py --scene lines; profile-name is
   the kernel's nrt_profile name, default the kernel) instead of profiles/pmc_<kernel>.json.
 """
 import csv
@@ -58,7 +58,7 @@ def main():
     if scene:
         out["scene"] = scene
         out["note"] = out["note"].replace("bench.py --size %d" % size, "bench.py --scene %s --size %d" % (scene, size))
-        path = os.path.join(ROOT, "profiles", f"pmc_{scene}_{pname}.json")
+        path = os.path.join(ROOT, "profiles", f"pmc_{scene}_{precision}_{pname}.json")
     else:
         path = os.path.join(ROOT, "profiles", f"pmc_{kernel}.json")
     json.dump(out, open(path, "w"), indent=1)

@@ -13,6 +13,9 @@ run() {  # scene precision kernel-regex size profile-name
   python3 tools/pmc_traffic.py $O/${sc}_${pr}_FETCH_SIZE $O/${sc}_${pr}_WRITE_SIZE $sz $pr $kr $sc $pn || return 1
   rm -rf $O/${sc}_${pr}_FETCH_SIZE $O/${sc}_${pr}_WRITE_SIZE
 }
+if [ -n "$1" ]; then
+  run "$@" || exit 1
+else
 run colocate fp16 k_march16 800 k_march16 && \
 run colocate mixed k_march16 800 k_march16 && \
 run colocate fp32-split k_march3 800 k_march3 && \
@@ -23,5 +26,6 @@ run dtu fp32-split k_march3 800 k_march3 && \
 run dtu fp32 k_march32 800 k_march32 && \
 run nerfle fp16 k_nerfle16 1600 k_nerfle && \
 run path fp32 k_march32 200 k_march32 || exit 1
+fi
 cp profiles/pmc_*_k_*.json $O/ 2>/dev/null
 echo done
