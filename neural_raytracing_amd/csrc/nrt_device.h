@@ -177,12 +177,22 @@ __device__ __forceinline__ void wave_lds_fence() {
 // paths are not bit-equal to torch's log1pf(expf(x)) but within a few ulp per activation; the
 // parity suite holds them at the 1e-4 bar against the oracle (measured: max 4.5e-8 on the smoke
 // crop, 0 hit / step flips on the ring32 march configurations, tests/test_gpu_ring32.py).
+//
+// Round 6: the compensation is additive, log1p(e) = log(u) + c / u with c = e - (u - 1) the exact
+// rounding error of u, and 1/u taken as 1.5 - u/2 (exact at u = 1 and 2, within 12 % between:
+// c <= 2^-24 u, so that error stays far below an ulp of the result; e < 2^-24 gives u = 1, c = e).
+// One transcendental (v_rcp) and two compare / selects fewer than Goldberg's ratio form, the same
+// accuracy (float32 emulation over x in [-30, 20] and 1e6 N(0, 5) samples against float64
+// log1p(exp(x)): max 4.8e-7 absolute, mean 2.1 ulp, both forms).  Measured (timing-only variant,
+// softplus -> max(x, 0)): the FP32 ring march spends 12 % (8x256) / 17 % (8x128) of its time in
+// the softplus VALU -- on gfx950 the f32 MFMA and the VALU of the two waves of a SIMD do not
+// overlap fully, so VALU cuts show up as time.
 __device__ __forceinline__ float softplus_exact(float x) {
   const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
   const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
   const float u = 1.f + e;
-  const float d = u - 1.f;
-  const float l1p = d == 0.f ? e : (__builtin_amdgcn_logf(u) * kLn2) * (e * __builtin_amdgcn_rcpf(d));
+  const float c = e - (u - 1.f);
+  const float l1p = fmaf(__builtin_amdgcn_logf(u), kLn2, c * fmaf(-0.5f, u, 1.5f));
   return x > 20.f ? x : fmaxf(x, 0.f) + l1p;
 }
 
@@ -1805,6 +1815,7 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
 // combined with two butterfly adds (commutative, so every lane gets the same bits)
 __device__ __forceinline__ float spheres_value16(const SdfDev& s, const float4* sp, int lane,
                                                  float x, float y, float z) {
+  const float nk2 = -s.k * 1.4426950408889634f;
   float acc = 0.f;
   for (int i = lane >> 4; i < s.n_spheres; i += 4) {
     const float4 r0 = sp[4 * i], r1 = sp[4 * i + 1], r2 = sp[4 * i + 2], r3 = sp[4 * i + 3];
@@ -1812,8 +1823,11 @@ __device__ __forceinline__ float spheres_value16(const SdfDev& s, const float4* 
     const float qx = fmaf(r0.z, z, fmaf(r0.y, y, r0.x * x)) - r2.y;
     const float qy = fmaf(r1.y, z, fmaf(r1.x, y, r0.w * x)) - r2.z;
     const float qz = fmaf(r2.x, z, fmaf(r1.w, y, r1.z * x)) - r2.w;
-    const float d = sqrtf(qx * qx + qy * qy + qz * qz) - r3.x;
-    acc += expf(-s.k * d);
+    // v_sqrt_f32 (1 ulp) and exp(-k d) as v_exp_f32 of -k log2(e) d (a few ulp; a term that
+    // leaves the normal range is 0, below the 1e-4 floor of the sum): round 6, ~15 VALU a
+    // sphere fewer than the correctly rounded sqrtf / expf, 3e-9 on the SDF value
+    const float d = __builtin_sqrtf(qx * qx + qy * qy + qz * qz) - r3.x;
+    acc += __builtin_amdgcn_exp2f(d * nk2);
   }
   acc += __shfl_xor(acc, 16);
   acc += __shfl_xor(acc, 32);

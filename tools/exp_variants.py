@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT)
 from neural_raytracing_amd import build as B  # noqa: E402
 
 B.build(verbose=False)
-out = os.path.join(ROOT, "build_var")
+out = os.path.join(ROOT, os.environ.get("VAR_DIR", "build_var"))
 os.makedirs(out, exist_ok=True)
 VARIED = os.environ.get("VARIED", "nrt_api_sdf.hip,nrt_ring_march.hip,nrt_ring_normal.hip").split(",")
 others = [os.path.join(B.OBJDIR, os.path.splitext(s)[0] + ".o") for s in B.SOURCES
