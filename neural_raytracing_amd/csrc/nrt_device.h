@@ -187,13 +187,33 @@ __device__ __forceinline__ void wave_lds_fence() {
 // softplus -> max(x, 0)): the FP32 ring march spends 12 % (8x256) / 17 % (8x128) of its time in
 // the softplus VALU -- on gfx950 the f32 MFMA and the VALU of the two waves of a SIMD do not
 // overlap fully, so VALU cuts show up as time.
+// torch's threshold (x > 20 -> x) needs no select: there e < 2.1e-9, below half an ulp of x, so
+// max(x, 0) + log1p(e) rounds to x exactly (and +-inf / NaN come out as torch's).
 __device__ __forceinline__ float softplus_exact(float x) {
   const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
-  const float e = __builtin_amdgcn_exp2f(-fabsf(x) * kLog2e);
+  const float e = __builtin_amdgcn_exp2f(fabsf(x) * -kLog2e);
   const float u = 1.f + e;
   const float c = e - (u - 1.f);
   const float l1p = fmaf(__builtin_amdgcn_logf(u), kLn2, c * fmaf(-0.5f, u, 1.5f));
-  return x > 20.f ? x : fmaxf(x, 0.f) + l1p;
+  return fmaxf(x, 0.f) + l1p;
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+// softplus_exact on two elements: the same IEEE operations, the non-transcendental ones as packed
+// f32 (v_pk_mul / v_pk_add / v_pk_fma_f32, two elements an instruction): the same bits
+__device__ __forceinline__ f2v softplus_exact2(f2v x) {
+  const float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+  const f2v one = {1.f, 1.f};
+  const f2v ax = {fabsf(x[0]), fabsf(x[1])};
+  const f2v t = ax * f2v{-kLog2e, -kLog2e};
+  const f2v e = {__builtin_amdgcn_exp2f(t[0]), __builtin_amdgcn_exp2f(t[1])};
+  const f2v u = one + e;
+  const f2v c = e - (u - one);
+  const f2v r = __builtin_elementwise_fma(f2v{-0.5f, -0.5f}, u, f2v{1.5f, 1.5f});
+  const f2v lg = {__builtin_amdgcn_logf(u[0]), __builtin_amdgcn_logf(u[1])};
+  const f2v l1p = __builtin_elementwise_fma(lg, f2v{kLn2, kLn2}, c * r);
+  const f2v m = {fmaxf(x[0], 0.f), fmaxf(x[1], 0.f)};
+  return m + l1p;
 }
 
 // torch semantics: F.leaky_relu (slope 0.01), F.softplus (beta 1, threshold 20), sigmoid, relu
@@ -733,7 +753,6 @@ __device__ __forceinline__ void build_sphere_pairs(const SdfDev& s, float4* out)
   }
 }
 
-typedef float f2v __attribute__((ext_vector_type(2)));
 // FP16-path sphere smooth-min over the pair table (the FP16 march's SDF precision: fast v_sqrt,
 // fused arithmetic, pairwise sums -- ~10 VALU per sphere instead of ~30); the two lanes of a
 // ray sum their spheres and combine with one cross-half add
@@ -1741,9 +1760,25 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
     else d = act<ACT>(pend[k >> 2][r]);
     asm volatile("" : "+v"(d));
   };
+  // elements 2q, 2q + 1 of chunk ib: softplus on packed f32 (softplus_exact2, the same bits)
+  constexpr bool PK = !TAN && ACT == ACT_SOFTPLUS;
+  auto retire2 = [&](int ib, int q) {
+    if constexpr (PK) {
+      const int k = 2 * q, r = k & 3;
+      const f2v v = softplus_exact2(f2v{pend[k >> 2][r], pend[k >> 2][r + 1]});
+      float& d0 = dst[4 * kSub * ib + k];
+      float& d1 = dst[4 * kSub * ib + k + 1];
+      d0 = v[0];
+      d1 = v[1];
+      asm volatile("" : "+v"(d0), "+v"(d1));
+    } else {
+      retire1(ib, 2 * q);
+      retire1(ib, 2 * q + 1);
+    }
+  };
   auto retire = [&](int ib) {
 #pragma unroll
-    for (int k = 0; k < 4 * kSub; ++k) retire1(ib, k);
+    for (int q = 0; q < 2 * kSub; ++q) retire2(ib, q);
   };
   // init layer (neural_blocks.py:80): raw encoding in
 #pragma unroll
@@ -1771,11 +1806,11 @@ __device__ __forceinline__ float eval(Engine<KH, KE, WV>& E, const MlpDev& m, fl
       f4v a[kSub];
 #pragma unroll
       for (int b = 0; b < kSub; ++b) a[b] = bias(1 + i, kSub * ib + b);
-      // the previous chunk's 4 kSub activations spread over this chunk's QH quads
+      // the previous chunk's 4 kSub activations spread over this chunk's QH quads, in pairs
       seg4<QH, 0, 0>(A, src, a, [&](int u) {
         if (ib > 0)
 #pragma unroll
-          for (int k = (u * 4 * kSub) / QH; k < ((u + 1) * 4 * kSub) / QH; ++k) retire1(ib - 1, k);
+          for (int q = (u * 2 * kSub) / QH; q < ((u + 1) * 2 * kSub) / QH; ++q) retire2(ib - 1, q);
       });
       E.end();
       if (skip) {  // the encoding part: a chunk of its own
