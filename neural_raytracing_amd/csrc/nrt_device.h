@@ -1514,6 +1514,36 @@ __device__ __forceinline__ f4v mfma4(float a, float b, f4v c) {
 // largest chunk (and the 2-slot ring) at 64 KiB for H = 256.
 constexpr int kSub = 4;
 
+// The FP32 ring's SphereSDF table in LDS as sphere PAIRS for packed-f32 VALU: lane group g
+// (lane >> 4) owns spheres g, g + 4, g + 8, ... and record 4 j + g holds its spheres g + 8 j and
+// g + 8 j + 4 as 13 float2 (m00 m01 m02 m10 m11 m12 m20 m21 m22 cx cy cz r) + pad = 7 float4; a
+// missing sphere has r = -inf (its term exp2(+inf * -k log2 e) is 0).  nrt_launch.h
+// ring32_sphere_bytes sizes it.
+constexpr int kPair32F4 = 7;
+__host__ __device__ inline int sphere_pairs32(int n) { return ((n + 3) / 4 + 1) / 2; }  // per group
+__device__ __forceinline__ void build_sphere_pairs32(const SdfDev& s, float4* out) {
+  const int n = s.n_spheres, R = 4 * sphere_pairs32(n);
+  const float4* src = reinterpret_cast<const float4*>(s.spheres);
+  for (int rec = threadIdx.x; rec < R; rec += blockDim.x) {
+    const int g = rec & 3, j = rec >> 2;
+    float* o = reinterpret_cast<float*>(out + rec * kPair32F4);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = g + 8 * j + 4 * u;
+      if (i < n) {
+        const float4 r0 = src[4 * i], r1 = src[4 * i + 1], r2 = src[4 * i + 2], r3 = src[4 * i + 3];
+        const float m[13] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w, r2.x, r2.y, r2.z, r2.w,
+                             r3.x};
+        for (int k = 0; k < 13; ++k) o[2 * k + u] = m[k];
+      } else {
+        for (int k = 0; k < 12; ++k) o[2 * k + u] = 0.f;
+        o[24 + u] = -__builtin_inff();
+      }
+    }
+    o[26] = 0.f; o[27] = 0.f;
+  }
+}
+
 // KH = H / 4 hidden k-steps, KE = ke / 4 encoding k-steps (ke = encoding slots padded to 16)
 template <int KH, int KE, int WV>
 struct Engine {
@@ -1575,9 +1605,7 @@ struct Engine {
     lbias = lb;
     p += (size_t)nb * 4;
     float4* ls = reinterpret_cast<float4*>(p);
-    if (s.kind == 2)
-      for (int i = threadIdx.x; i < s.n_spheres * 4; i += blockDim.x)
-        ls[i] = reinterpret_cast<const float4*>(s.spheres)[i];
+    if (s.kind == 2) build_sphere_pairs32(s, ls);
     lspheres = ls;
     bstride = m.bias16_stride;
     sbase = m.stream32;
@@ -1861,12 +1889,43 @@ __device__ __forceinline__ float spheres_value16(const SdfDev& s, const float4* 
     // v_sqrt_f32 (1 ulp) and exp(-k d) as v_exp_f32 of -k log2(e) d (a few ulp; a term that
     // leaves the normal range is 0, below the 1e-4 floor of the sum): round 6, ~15 VALU a
     // sphere fewer than the correctly rounded sqrtf / expf, 3e-9 on the SDF value
-    const float d = __builtin_sqrtf(qx * qx + qy * qy + qz * qz) - r3.x;
+    const float d = __builtin_amdgcn_sqrtf(qx * qx + qy * qy + qz * qz) - r3.x;
     acc += __builtin_amdgcn_exp2f(d * nk2);
   }
   acc += __shfl_xor(acc, 16);
   acc += __shfl_xor(acc, 32);
   return -logf(fmaxf(acc, 1e-4f)) / s.k;
+}
+
+// spheres_value16 over the pair table (build_sphere_pairs32): the same per-sphere operations in
+// the same order on packed f32 (v_pk_mul / v_pk_fma / v_pk_add: two spheres an instruction, half
+// the VALU), the two halves of a lane's sum added at the end (a different summation order than
+// spheres_value16's single running sum: an ulp of the sum)
+__device__ __forceinline__ float spheres_value16_pairs(const SdfDev& s, const float4* sp, int lane,
+                                                       float x, float y, float z) {
+  const int g = lane >> 4, NP = sphere_pairs32(s.n_spheres);
+  const float nk = -s.k * 1.4426950408889634f;
+  const f2v xx = {x, x}, yy = {y, y}, zz = {z, z}, nk2 = {nk, nk};
+  f2v acc = {0.f, 0.f};
+  for (int j = 0; j < NP; ++j) {
+    const float4* q = sp + (4 * j + g) * kPair32F4;
+    const float4 a = q[0], b = q[1], c = q[2], d = q[3], e = q[4], f = q[5], h = q[6];
+    const f2v m00 = {a.x, a.y}, m01 = {a.z, a.w}, m02 = {b.x, b.y}, m10 = {b.z, b.w};
+    const f2v m11 = {c.x, c.y}, m12 = {c.z, c.w}, m20 = {d.x, d.y}, m21 = {d.z, d.w};
+    const f2v m22 = {e.x, e.y}, cx = {e.z, e.w}, cy = {f.x, f.y}, cz = {f.z, f.w};
+    const f2v r = {h.x, h.y};
+    const f2v qx = __builtin_elementwise_fma(m02, zz, __builtin_elementwise_fma(m01, yy, m00 * xx)) - cx;
+    const f2v qy = __builtin_elementwise_fma(m12, zz, __builtin_elementwise_fma(m11, yy, m10 * xx)) - cy;
+    const f2v qz = __builtin_elementwise_fma(m22, zz, __builtin_elementwise_fma(m21, yy, m20 * xx)) - cz;
+    const f2v n2 = (qx * qx + qy * qy) + qz * qz;
+    const f2v dd = f2v{__builtin_amdgcn_sqrtf(n2.x), __builtin_amdgcn_sqrtf(n2.y)} - r;
+    const f2v t = dd * nk2;
+    acc += f2v{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+  }
+  float v = acc.x + acc.y;
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return -logf(fmaxf(v, 1e-4f)) / s.k;
 }
 
 }  // namespace ring32

@@ -526,7 +526,7 @@ struct RingPol32 {
     E.init(m, s, lds, ring32::kSub * Eng::QE);
   }
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
-    const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
+    const float d = (s.kind == 2) ? ring32::spheres_value16_pairs(s, E.lspheres, E.lane, x, y, z) : 0.f;
     return d + ring32::eval<KH, KE, WV, ACT>(E, m, x, y, z);
   }
   // forward-mode column value (ring32::eval TAN): 4 rays x (value, d/dx, d/dy, d/dz)

@@ -172,7 +172,11 @@ inline size_t ring32_bias_bytes(const nrt_sdf* s) {
   return (size_t)(s->mlp->desc.num_layers + 2) * s->mlp->host_dev.bias16_stride * 4;
 }
 inline size_t ring32_sphere_bytes(const nrt_sdf* s) {
-  return s->host_dev.kind == 2 ? (size_t)s->host_dev.n_spheres * 64 : 0;
+  // the per-sphere table (ring3) or the FP32 ring's pair table (ring32::build_sphere_pairs32)
+  if (s->host_dev.kind != 2) return 0;
+  const size_t one = (size_t)s->host_dev.n_spheres * 64;
+  const size_t pairs = (size_t)4 * ring32::sphere_pairs32(s->host_dev.n_spheres) * ring32::kPair32F4 * 16;
+  return one > pairs ? one : pairs;
 }
 inline bool ring32_supported(const nrt_sdf* s) {
   if (!s->mlp) return false;
