@@ -258,8 +258,15 @@ __global__ void k_plain_composite(const float* __restrict__ first_out, int astri
 // pair order); e2..e7 = the first MLP's output tiles in accumulator order (row 1 + k = latent k;
 // row 0 and rows > 64 have zero weight); e8 = (r_d, light) in half 0.
 // ------------------------------------------------------------------------------------------
+#ifndef NRT_NERF_TILES
+#define NRT_NERF_TILES 2
+#endif
 #ifndef NRT_NERF_WAVES
+#if NRT_NERF_TILES == 1
 #define NRT_NERF_WAVES 12  // 3 waves per SIMD (162 VGPRs with the DMA engine)
+#else
+#define NRT_NERF_WAVES 8
+#endif
 #endif
 #ifndef NRT_NERF_MAXF
 #define NRT_NERF_MAXF 32
@@ -268,6 +275,7 @@ __global__ void k_plain_composite(const float* __restrict__ first_out, int astri
 #define NRT_NERF_DMA 1
 #endif
 constexpr int kNerfWaves = NRT_NERF_WAVES;
+constexpr int kNerfTiles = NRT_NERF_TILES;  // 32-sample tiles per wave (each A read feeds them all)
 constexpr bool kNerfDma = NRT_NERF_DMA != 0;  // weight chunks by LDS-DMA (KEngine DMA mode)
 constexpr int kNerfMaxF = NRT_NERF_MAXF;  // fragments per ring slot (3 slots: 96 KiB of LDS at 32)
 constexpr int kNerfKC1 = kNerfMaxF / 4;   // k-steps per chunk of the first MLP (4 row blocks)
@@ -289,10 +297,13 @@ __device__ __forceinline__ h8 leaky_h8(const h8& v) {
   return f;
 }
 
-// acc[ib] += W[ib] * [b1[0..KS1), b2[0..KS2)] over chunks of KC k-steps
-template <int NB, int KS1, int KS2, int KC, class Eng, int N1, int N2>
-__device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
-                                           const h8 (&b1)[N1], const h8 (&b2)[N2]) {
+// acc[q][ib] += W[ib] * [b1[q][0..KS1), act(b2[q][0..KS2))] over chunks of KC k-steps, for the
+// TT 32-sample tiles q of the wave: each A fragment read from the ring feeds TT MFMAs.  ACT2:
+// act = leaky_relu on the packed halves at each use (the skip layers' act(encoding) is not kept
+// in registers), else the identity
+template <int NB, int KS1, int KS2, int KC, int TT, bool ACT2 = false, class Eng, int N1, int N2>
+__device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[TT][NB],
+                                           const h8 (&b1)[TT][N1], const h8 (&b2)[TT][N2]) {
   static_assert(KS1 <= N1 && KS2 <= N2, "fragment arrays too short");
   static_assert(KC * NB <= Eng::MAXF, "chunk larger than a ring slot");
   constexpr int KS = KS1 + KS2;
@@ -300,7 +311,8 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
 #ifndef NRT_NERF_W
 #define NRT_NERF_W 4
 #endif
-  constexpr int W = NRT_NERF_W;  // A fragments in flight (LDS latency cover)
+  // A fragments in flight (LDS latency cover: each one feeds TT MFMAs)
+  constexpr int W = (NRT_NERF_W + TT - 1) / TT;
 #pragma unroll
   for (int cc = 0; cc < NCH; ++cc) {
     const h8* A = E.begin();
@@ -313,8 +325,14 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
     for (int m = 0; m < KC * NB; ++m) {
       if (m < nf) {
         const int s = cc * KC + m / NB, ib = m % NB;
-        const h8 b = s < KS1 ? b1[s < KS1 ? s : 0] : b2[s >= KS1 ? s - KS1 : 0];
-        acc[ib] = mfma16(a[m % W], b, acc[ib]);
+#pragma unroll
+        for (int q = 0; q < TT; ++q) {
+          h8 b;
+          if (s < KS1) b = b1[q][s < KS1 ? s : 0];
+          else if (ACT2) b = leaky_h8(b2[q][s >= KS1 ? s - KS1 : 0]);
+          else b = b2[q][s >= KS1 ? s - KS1 : 0];
+          acc[q][ib] = mfma16(a[m % W], b, acc[q][ib]);
+        }
         if (m + W < nf) a[m % W] = A[(m + W) * 64];
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -323,35 +341,53 @@ __device__ __forceinline__ void nerf_layer(Eng& E, f16v (&acc)[NB],
   }
 }
 
-// the first MLP (nerf.py:162-163: 5 x 128, F = 16, 3 -> 65) with its 3 output row blocks
-template <int L, int SKIP, class Eng>
-__device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, float x0,
-                                           float x1, float x2, f16v (&o)[3]) {
+// the first MLP (nerf.py:162-163: 5 x 128, F = 16, 3 -> 65) with its 3 output row blocks, on
+// the wave's TT tiles (the layer biases read once from LDS for all of them)
+template <int L, int SKIP, int TT, class Eng>
+__device__ __forceinline__ void nerf_first(Eng& E, const ProgMlp& pm, const float (&x0)[TT],
+                                           const float (&x1)[TT], const float (&x2)[TT],
+                                           f16v (&o)[TT][3]) {
   constexpr int NB = 4, NE = 3;
   const int h = E.lane >> 5;
   const float4* basis = E.lbasis + pm.basis_off;
-  f16v acc[NB];
-  h8 hv[2 * NB];
-  h8 enc[NE];
+  f16v acc[TT][NB];
+  h8 hv[TT][2 * NB];
+  h8 enc[TT][NE];
 #pragma unroll
-  for (int s = 0; s < NE; ++s) enc[s] = ring::enc_frag_k<-1>(basis, s, NE - 1, h, x0, x1, x2);
+  for (int q = 0; q < TT; ++q)
 #pragma unroll
-  for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 0, ib, h);
-  nerf_layer<NB, NE, 0, kNerfKC1>(E, acc, enc, enc);
+    for (int s = 0; s < NE; ++s) enc[q][s] = ring::enc_frag_k<-1>(basis, s, NE - 1, h, x0[q], x1[q], x2[q]);
+  auto biases = [&](int layer) {
 #pragma unroll
-  for (int s = 0; s < NE; ++s) enc[s] = leaky_h8(enc[s]);  // act(enc) from the same halves
+    for (int ib = 0; ib < NB; ++ib) {
+      acc[0][ib] = E.bias_at(pm, layer, ib, h);
+#pragma unroll
+      for (int q = 1; q < TT; ++q) acc[q][ib] = acc[0][ib];
+    }
+  };
+  biases(0);
+  nerf_layer<NB, NE, 0, kNerfKC1, TT>(E, acc, enc, enc);
+#pragma unroll
+  for (int q = 0; q < TT; ++q)
+#pragma unroll
+    for (int s = 0; s < NE; ++s) enc[q][s] = leaky_h8(enc[q][s]);  // act(enc) from the same halves
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(pm, 1 + i, ib, h);
-    nerf_layer<NB, 2 * NB, 0, kNerfKC1>(E, acc, hv, hv);
-    if (i != L - 1 && (i % SKIP) == 0) nerf_layer<NB, NE, 0, kNerfKC1>(E, acc, enc, enc);
+    for (int q = 0; q < TT; ++q) ring::kact<NB, ACT_LEAKY>(acc[q], hv[q]);
+    biases(1 + i);
+    nerf_layer<NB, 2 * NB, 0, kNerfKC1, TT>(E, acc, hv, hv);
+    if (i != L - 1 && (i % SKIP) == 0) nerf_layer<NB, NE, 0, kNerfKC1, TT>(E, acc, enc, enc);
   }
-  ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
-  for (int ob = 0; ob < 3; ++ob) o[ob] = E.bias_at(pm, L + 1, ob, h);
-  nerf_layer<3, 2 * NB, 0, kNerfKC1>(E, o, hv, hv);
+  for (int q = 0; q < TT; ++q) ring::kact<NB, ACT_LEAKY>(acc[q], hv[q]);
+#pragma unroll
+  for (int ob = 0; ob < 3; ++ob) {
+    o[0][ob] = E.bias_at(pm, L + 1, ob, h);
+#pragma unroll
+    for (int q = 1; q < TT; ++q) o[q][ob] = o[0][ob];
+  }
+  nerf_layer<3, 2 * NB, 0, kNerfKC1, TT>(E, o, hv, hv);
 }
 
 __device__ __forceinline__ h8 h8_of(const float (&v)[8]) {
@@ -375,14 +411,14 @@ __device__ __forceinline__ void split_h8(const float (&v)[8], h8& hi, h8& lo) {
   lo = __builtin_bit_cast(h8, l);
 }
 
-template <int WV>
+template <int WV, int TT>
 __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
     const ProgDev prog, const float* __restrict__ rays, int64_t P, const float* __restrict__ ts,
     int S, const float* __restrict__ light, float* __restrict__ alpha_raw,
     float* __restrict__ rgb_raw) {
   extern __shared__ __attribute__((aligned(16))) char smem_c[];
   const int64_t n = (int64_t)S * P;
-  const int64_t per_block = 32 * WV;
+  const int64_t per_block = 32 * TT * WV;
   if ((int64_t)blockIdx.x * per_block >= n) return;
   ring::KEngine<WV, kNerfMaxF, kNerfDma> E;
   E.init(prog, smem_c);
@@ -392,82 +428,115 @@ __global__ void __launch_bounds__(64 * WV, 1) k_nerfle16(
   const ProgMlp& m2 = prog.mlp[1];
   const float lx = light[0], ly = light[1], lz = light[2];
   for (int64_t b0 = (int64_t)blockIdx.x * per_block; b0 < n; b0 += (int64_t)gridDim.x * per_block) {
-    const int64_t g = b0 + 32 * wv + (lane & 31);
-    const bool valid = g < n;
-    const int64_t gg = valid ? g : n - 1;
-    const int64_t p = gg / S, s = gg - p * S;  // ray-major: a wave's columns share a ray
-    const float t = ts[s];
-    const float* r = rays + p * 6;
-    const float dx = r[3], dy = r[4], dz = r[5];
-    // pts = r_o + t r_d (nerf.py:179, no FMA contraction)
-    const float x0 = __fadd_rn(r[0], __fmul_rn(t, dx));
-    const float x1 = __fadd_rn(r[1], __fmul_rn(t, dy));
-    const float x2 = __fadd_rn(r[2], __fmul_rn(t, dz));
-    f16v o[3];
-    nerf_first<kNerfL1, kNerfSkip>(E, m1, x0, x1, x2, o);
-    // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
-    h8 e[9], ea[9], lo[7];
+    // tile q of this wave: samples b0 + 32 (TT wv + q) + [0, 32) (recomputed where needed: the
+    // registers go to the MLPs)
+    auto sample = [&](int q) -> int64_t { return b0 + 32 * (TT * wv + q) + (lane & 31); };
+    auto ray_of = [&](int q) -> const float* {
+      const int64_t g = sample(q);
+      return rays + ((g < n ? g : n - 1) / S) * 6;  // ray-major: a tile's columns share a ray
+    };
+    float x0[TT], x1[TT], x2[TT];
 #pragma unroll
-    for (int tt = 0; tt < 6; ++tt) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = o[tt >> 1][8 * (tt & 1) + j];
-      split_h8(v, e[2 + tt], lo[tt]);
-      ea[2 + tt] = leaky_h8(e[2 + tt]);
+    for (int q = 0; q < TT; ++q) {
+      const int64_t g = sample(q);
+      const int64_t gg = g < n ? g : n - 1;
+      const float t = ts[gg - (gg / S) * S];
+      const float* r = ray_of(q);
+      // pts = r_o + t r_d (nerf.py:179, no FMA contraction)
+      x0[q] = __fadd_rn(r[0], __fmul_rn(t, r[3]));
+      x1[q] = __fadd_rn(r[1], __fmul_rn(t, r[4]));
+      x2[q] = __fadd_rn(r[2], __fmul_rn(t, r[5]));
     }
-    {
+    f16v o[TT][3];
+    nerf_first<kNerfL1, kNerfSkip, TT>(E, m1, x0, x1, x2, o);
+    // second-MLP input fragments e2..e8 (hi) and their FP16 residuals (lo) for the projection
+    h8 e[TT][9], lo[TT][7];
+#pragma unroll
+    for (int q = 0; q < TT; ++q) {
+#pragma unroll
+      for (int tt = 0; tt < 6; ++tt) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = o[q][tt >> 1][8 * (tt & 1) + j];
+        split_h8(v, e[q][2 + tt], lo[q][tt]);
+      }
       float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (h == 0) { v[0] = dx; v[1] = dy; v[2] = dz; v[3] = lx; v[4] = ly; v[5] = lz; }
-      split_h8(v, e[8], lo[6]);
-      ea[8] = leaky_h8(e[8]);
+      if (h == 0) {
+        const float* r = ray_of(q);
+        v[0] = r[3]; v[1] = r[4]; v[2] = r[5]; v[3] = lx; v[4] = ly; v[5] = lz;
+      }
+      split_h8(v, e[q][8], lo[q][6]);
     }
     // projections x @ B (utils.py:37-40) as hi*hi + lo(A)*hi + hi*lo(x): FP32-accurate
-    f16v pq;
+    f16v pq[TT];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) pq[k] = 0.f;
+    for (int q = 0; q < TT; ++q)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) pq[q][k] = 0.f;
     {
       const h8* A = E.begin();
 #pragma unroll
       for (int tt = 0; tt < 7; ++tt) {
-        pq = mfma16(A[tt * 64], e[2 + tt], pq);
-        pq = mfma16(A[(7 + tt) * 64], e[2 + tt], pq);
-        pq = mfma16(A[tt * 64], lo[tt], pq);
+        const h8 ah = A[tt * 64], al = A[(7 + tt) * 64];
+#pragma unroll
+        for (int q = 0; q < TT; ++q) {
+          pq[q] = mfma16(ah, e[q][2 + tt], pq[q]);
+          pq[q] = mfma16(al, e[q][2 + tt], pq[q]);
+          pq[q] = mfma16(ah, lo[q][tt], pq[q]);
+        }
       }
       E.end();
     }
     // rows q = (reg & 3) + 8 (reg >> 2) + 4h: regs 0..3 -> q = 4h + jj, regs 4..7 -> 8 + 4h + jj
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      float v[8];
+    for (int q = 0; q < TT; ++q) {
 #pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        v[2 * jj] = __sinf(pq[4 * s2 + jj]);
-        v[2 * jj + 1] = __cosf(pq[4 * s2 + jj]);
+      for (int s2 = 0; s2 < 2; ++s2) {
+        float v[8];
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          v[2 * jj] = __sinf(pq[q][4 * s2 + jj]);
+          v[2 * jj + 1] = __cosf(pq[q][4 * s2 + jj]);
+        }
+        e[q][s2] = h8_of(v);
       }
-      e[s2] = h8_of(v);
-      ea[s2] = leaky_h8(e[s2]);
     }
     // the second MLP (nerf.py:168-172: 8 x 64, 70 -> 3)
     constexpr int NB = 2;
-    f16v acc[NB];
-    h8 hv[2 * NB];
+    f16v acc[TT][NB];
+    h8 hv[TT][2 * NB];
+    auto biases = [&](int layer) {
 #pragma unroll
-    for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 0, ib, h);
-    nerf_layer<NB, 9, 0, kNerfKC2>(E, acc, e, e);
+      for (int ib = 0; ib < NB; ++ib) {
+        acc[0][ib] = E.bias_at(m2, layer, ib, h);
+#pragma unroll
+        for (int q = 1; q < TT; ++q) acc[q][ib] = acc[0][ib];
+      }
+    };
+    biases(0);
+    nerf_layer<NB, 9, 0, kNerfKC2, TT>(E, acc, e, e);
 #pragma unroll
     for (int i = 0; i < kNerfL2; ++i) {
-      ring::kact<NB, ACT_LEAKY>(acc, hv);
 #pragma unroll
-      for (int ib = 0; ib < NB; ++ib) acc[ib] = E.bias_at(m2, 1 + i, ib, h);
-      if (i != kNerfL2 - 1 && (i % kNerfSkip) == 0) nerf_layer<NB, 2 * NB, 9, kNerfKC2>(E, acc, hv, ea);
-      else nerf_layer<NB, 2 * NB, 0, kNerfKC2>(E, acc, hv, hv);
+      for (int q = 0; q < TT; ++q) ring::kact<NB, ACT_LEAKY>(acc[q], hv[q]);
+      biases(1 + i);
+      if (i != kNerfL2 - 1 && (i % kNerfSkip) == 0) nerf_layer<NB, 2 * NB, 9, kNerfKC2, TT, true>(E, acc, hv, e);
+      else nerf_layer<NB, 2 * NB, 0, kNerfKC2, TT>(E, acc, hv, hv);
     }
-    ring::kact<NB, ACT_LEAKY>(acc, hv);
-    f16v out[1] = {E.bias_at(m2, kNerfL2 + 1, 0, h)};
-    nerf_layer<1, 2 * NB, 0, kNerfKC2>(E, out, hv, hv);
-    if (valid && h == 0) {
-      alpha_raw[g] = o[0][0];
-      rgb_raw[g * 3] = out[0][0]; rgb_raw[g * 3 + 1] = out[0][1]; rgb_raw[g * 3 + 2] = out[0][2];
+#pragma unroll
+    for (int q = 0; q < TT; ++q) ring::kact<NB, ACT_LEAKY>(acc[q], hv[q]);
+    f16v out[TT][1];
+    out[0][0] = E.bias_at(m2, kNerfL2 + 1, 0, h);
+#pragma unroll
+    for (int q = 1; q < TT; ++q) out[q][0] = out[0][0];
+    nerf_layer<1, 2 * NB, 0, kNerfKC2, TT>(E, out, hv, hv);
+#pragma unroll
+    for (int q = 0; q < TT; ++q) {
+      const int64_t g = sample(q);
+      if (g < n && h == 0) {
+        alpha_raw[g] = o[q][0][0];
+        rgb_raw[g * 3] = out[q][0][0]; rgb_raw[g * 3 + 1] = out[q][0][1]; rgb_raw[g * 3 + 2] = out[q][0][2];
+      }
     }
   }
   E.drain();
@@ -738,7 +807,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     if (!env.empty()) light = second->nerf_prog->unit_light;
     float* alpha = (float*)ws;
     float* rgb_raw = (float*)(ws + a256(n * 4));
-    auto kern = k_nerfle16<kNerfWaves>;
+    auto kern = k_nerfle16<kNerfWaves, kNerfTiles>;
     const size_t lds = ring::KEngine<kNerfWaves, kNerfMaxF, kNerfDma>::lds_bytes(pd);
     if (int rc = set_lds(kern, lds)) return rc;
     int dev = 0, cus = 0, per_cu = 0;
@@ -747,7 +816,7 @@ int nrt_nerfle_forward(const nrt_mlp* first, const nrt_mlp* second, const float*
     NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kNerfWaves, lds));
     // persistent grid: every resident block slot (independent blocks on a CU run out of phase,
     // so one block's layer-boundary bubbles are filled by the other's MFMAs)
-    const int64_t want = ceil_div64((int64_t)n, 32 * kNerfWaves);
+    const int64_t want = ceil_div64((int64_t)n, 32 * kNerfTiles * kNerfWaves);
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)std::max(per_cu, 1) * cus));
     ProfScope prof("k_nerfle", st);
     kern<<<dim3(blocks), dim3(64 * kNerfWaves), lds, st>>>(pd, rays, P, ts, S, light, alpha, rgb_raw);

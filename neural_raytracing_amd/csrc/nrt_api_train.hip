@@ -1625,7 +1625,7 @@ int nrt_mlp_backward_multi(const nrt_mlp* const* mlps, int n, const float* x, in
   std::vector<TrainWs> ws(n);
   std::vector<BwdJob> jobs(n);
   for (int i = 0; i < n; ++i) {
-    ws[i] = carve(mlps[i], M, p);  // its first seven arrays; part / kpart are not used
+    ws[i] = carve(mlps[i], M, p);  // its first seven arrays; table / part are not used
     p += region_bytes(d, M);
     jobs[i] = BwdJob{mlps[i]->dev, dy[i], dx ? dx[i] : nullptr, ws[i].Z, ws[i].A, ws[i].Eraw,
                      ws[i].Eact, ws[i].dZ, ws[i].Et, ws[i].Gt};
