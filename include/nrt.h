@@ -577,6 +577,10 @@ int nrt_profile_flop(const char* name, double* flop);
  *                      the lists, 2 = the queue for batches of >= 131,072 rays (64 a resident
  *                      wave; the 800^2 frame 1 % faster, the 38,400-ray training march 1-5 %
  *                      slower on it); same results (a ray's values do not depend on the schedule)
+ *   "march_stage"    1  under the launch queue, the plain ring marches (k_march32 / k_march16 /
+ *                      k_march3) stage each wave's finished packed t and whole-scan keys in LDS
+ *                      per 16-ray line and write whole lines (fewer, coalesced write requests);
+ *                      0: one 4- / 8-byte store per ray; the same words either way
  * nrt_set_option returns NRT_EINVAL for an unknown name or a negative value.
  * ------------------------------------------------------------------------------------- */
 int nrt_set_option(const char* name, int64_t value);

@@ -29,9 +29,11 @@ static const OptionDef kOptions[OPT_COUNT] = {
     {"mixed_refine_d", kMixedRefineD}, {"mixed_refine_s", kMixedRefineS}, {"mixed_restart", 1},
     {"mixed_drift", 0}, {"ring_occlusion", 1}, {"mixed_zone", 500000},
     {"bwd_colsplit", 1}, {"bwd_ring", 1}, {"march_queue", 2}, {"train_save", 1}, {"wgrad_tile", 0},
+    {"march_stage", 1},
 };
 static std::atomic<int64_t> g_opts[OPT_COUNT] = {1, 1, 1, 1, 0, 1, 1, 0, 1, 1, 0,
-                                                 kMixedRefineD, kMixedRefineS, 1, 0, 1, 500000, 1, 1, 2, 1, 0};
+                                                 kMixedRefineD, kMixedRefineS, 1, 0, 1, 500000, 1, 1, 2, 1, 0,
+                                                 1};
 
 int64_t option(Option o) { return g_opts[o].load(std::memory_order_relaxed); }
 

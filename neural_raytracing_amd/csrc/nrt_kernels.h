@@ -290,8 +290,81 @@ struct MarchArgs {
   // a zeroed device counter; waves take kQueueChunk jobs at a time from the launch's whole list
   // ([march of every ray][scan segment s of every ray, s = 0 .. 7]); nullptr = per-wave lists
   unsigned int* queue = nullptr;
+  // launch-queue march (mode 0, packed t): byte offset in the block's LDS of the per-wave line
+  // stages (LineStage, kStageBytes a wave); 0 = every finished ray stores its own words
+  int stage = 0;
 };
 constexpr int kQueueChunk = 16;
+
+// ------------------------------------------------------------------------------------------
+// Line staging of the march's per-ray words (MarchArgs::stage).  Under the launch queue a wave
+// takes 16 consecutive jobs at a time, so the packed t of 16 consecutive rays (one 64-byte line)
+// and, for whole scans, their 64-bit keys (one 128-byte line) finish in one wave -- but at
+// different times, each as a lane-scattered 4- or 8-byte store (PMC: 45 MB of writes a 800^2
+// launch for ~8 MB of words).  Here a finished ray's word goes to a per-wave LDS slot of its line
+// instead; a slot whose line is complete is written by 16 lanes in one coalesced store, and a
+// slot that must make room (more than kStageSlots lines in flight) or is still open when the wave
+// ends is written with the lanes of its finished rays only.  Every ray's word is written exactly
+// once either way: the same bits as the per-ray stores.  The slot table (line, finished-ray mask)
+// lives in lanes 0 .. kStageSlots-1 of two VGPRs; all control is wave-uniform.
+constexpr int kStageSlots = 8;
+constexpr int kStageBytes = kStageSlots * 16 * (4 + 8);  // t words, then key words
+template <class W>
+struct LineStage {
+  W* data;          // [kStageSlots][16] in LDS
+  W* out;           // global: word of ray r at out[r]
+  int64_t limit;    // rays [0, limit) are staged here (a line past it completes early)
+  int tag = -1;     // lane q < kStageSlots: line held by slot q (-1 free)
+  uint32_t msk = 0; // lane q: finished rays of that line
+  int lane;
+  __device__ __forceinline__ void init(W* d, W* o, int64_t lim, int ln) {
+    data = d; out = o; limit = lim; lane = ln;
+  }
+  __device__ __forceinline__ void flush(int q, int line, uint32_t m) {
+    if (lane < 16 && ((m >> lane) & 1u)) out[(int64_t)line * 16 + lane] = data[q * 16 + lane];
+    if (lane == q) { tag = -1; msk = 0u; }
+  }
+  // lanes in `fin` (wave-uniform mask) finished their ray `ray` with word `v`
+  __device__ __forceinline__ void put(uint64_t fin, int64_t ray, W v) {
+    while (fin) {
+      const int l = __builtin_ctzll(fin);
+      fin &= fin - 1;
+      const int64_t r = ((int64_t)__builtin_amdgcn_readlane((int)(ray >> 32), l) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ray, l);
+      const int line = (int)(r >> 4), off = (int)(r & 15);
+      const uint64_t own = __ballot(lane < kStageSlots && tag == line);
+      int q;
+      if (own) {
+        q = __builtin_ctzll(own);
+      } else {
+        const uint64_t fr = __ballot(lane < kStageSlots && tag < 0);
+        if (fr) {
+          q = __builtin_ctzll(fr);
+        } else {  // evict slot 0's line (its finished rays only)
+          q = 0;
+          flush(0, __builtin_amdgcn_readlane(tag, 0), (uint32_t)__builtin_amdgcn_readlane((int)msk, 0));
+        }
+        if (lane == q) { tag = line; msk = 0u; }
+      }
+      asm volatile("" ::: "memory");
+      if (lane == l) data[q * 16 + off] = v;
+      if (lane == q) msk |= 1u << off;
+      const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)msk, q);
+      const int64_t n = limit - (int64_t)line * 16;
+      const uint32_t full = n >= 16 ? 0xffffu : ((1u << (int)n) - 1u);
+      asm volatile("" ::: "memory");
+      if (m == full) flush(q, line, m);
+      asm volatile("" ::: "memory");
+    }
+  }
+  __device__ __forceinline__ void drain() {
+#pragma unroll
+    for (int q = 0; q < kStageSlots; ++q) {
+      const int line = __builtin_amdgcn_readlane(tag, q);
+      if (line >= 0) flush(q, line, (uint32_t)__builtin_amdgcn_readlane((int)msk, q));
+    }
+  }
+};
 
 // the scan step of `ray`: max_t / 128 in double, as the reference's python float (sdfs.py:237)
 __device__ __forceinline__ double scan_step_of(const MarchArgs& a, int64_t ray) {
@@ -623,9 +696,20 @@ __device__ __forceinline__ void march_body(
   int64_t cursor = 0;  // wave-uniform
   int64_t cend = 0;    // queue: end of the wave's current chunk [cursor, cend)
   bool dry = false;    // queue: drained
+  // line staging (MarchArgs::stage): only the launch queue's plain march (job k's ray is k)
+  const bool stg = !MX && mode == 0 && dyn && a.stage != 0 && p_out == nullptr;
+  LineStage<float> st_t;
+  LineStage<unsigned long long> st_k;
+  if (stg) {
+    char* base = smem_c + a.stage + (int)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * kStageBytes;
+    st_t.init(reinterpret_cast<float*>(base), t_out, Pe, lane);
+    // whole scans are the rays [0, R - T); the segmented tail merges by atomic min in place
+    st_k.init(reinterpret_cast<unsigned long long*>(base + kStageSlots * 16 * 4), keys, R - T, lane);
+  }
   for (;;) {
     // retire ended jobs and hand out list entries until every lane has an evaluation to do
     for (;;) {
+      bool fin_t = false, fin_k = false;  // line staging: this lane's ray finished its word
       if (mode == 3 && kind == 0) {
         // intersect_test (sdfs.py:162-181): visible = t >= max_t | live after max_steps.  t only
         // grows, so a march past the light is decided (visible) and stops there
@@ -650,7 +734,8 @@ __device__ __forceinline__ void march_body(
               // packed: t >= 0 always (it only grows by d > eps) and a hit's t is finite (a NaN t
               // ends the march as a miss), so the hit flag rides in the sign bit; k_march_finish unpacks it and writes p / n / hit with coalesced stores
               // (this lane-scattered 4-byte store is the march's only per-ray output)
-              t_out[ray] = hit ? -t : t;
+              if (stg) fin_t = true;
+              else t_out[ray] = hit ? -t : t;
             }
           }
           kind = -1;
@@ -662,7 +747,8 @@ __device__ __forceinline__ void march_body(
           if (lane < RPW) {
             const unsigned long long k1 = scan_key(best, idx);
             if (whole) {
-              keys[ray] = k1;
+              if (stg) fin_k = true;
+              else keys[ray] = k1;
               if (MX && a.keys2) a.keys2[ray] = scan_key(second, idx2);
             } else {
               const unsigned long long old = atomicMin(keys + ray, k1);
@@ -678,6 +764,12 @@ __device__ __forceinline__ void march_body(
         }
       } else if (kind == 2) {
         if (ended) kind = -1;
+      }
+      if (stg) {
+        const uint64_t ft = __ballot(fin_t) & kRayMask;
+        if (ft) st_t.put(ft, ray, hit ? -t : t);
+        const uint64_t fk = __ballot(fin_k) & kRayMask;
+        if (fk) st_k.put(fk, ray, scan_key(best, idx));
       }
       const uint32_t want = (uint32_t)__ballot(kind == -1) & kRayMask;
       if (want == 0u) break;
@@ -839,6 +931,10 @@ __device__ __forceinline__ void march_body(
       }
       ended = true;
     }
+  }
+  if (stg) {
+    st_t.drain();
+    st_k.drain();
   }
   Pol::finish(E);
 }

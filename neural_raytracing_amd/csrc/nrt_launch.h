@@ -38,6 +38,7 @@ enum Option {
   OPT_MARCH_QUEUE,     // "march_queue"
   OPT_TRAIN_SAVE,      // "train_save"
   OPT_WGRAD_TILE,      // "wgrad_tile"
+  OPT_MARCH_STAGE,     // "march_stage"
   OPT_COUNT
 };
 int64_t option(Option o);
@@ -99,6 +100,17 @@ static inline int set_lds(K kernel, size_t bytes) {
     if (e != hipSuccess) return hip_fail(e, "hipFuncSetAttribute(MaxDynamicSharedMemorySize)");
   }
   return NRT_OK;
+}
+
+// MarchArgs::stage (option "march_stage"): the per-wave line stages (LineStage) after the rest
+// of the block's LDS, when the launch queue is on and they fit in the CU's 160 KiB
+static inline void stage_lds(MarchArgs& a, size_t& lds, int waves) {
+  if (!a.queue || option(OPT_MARCH_STAGE) == 0) return;
+  const size_t off = (lds + 15) & ~(size_t)15;
+  const size_t need = off + (size_t)waves * kStageBytes;
+  if (off == 0 || need > 160 * 1024) return;
+  a.stage = (int)off;
+  lds = need;
 }
 
 static inline int check_launch(const char* what) {

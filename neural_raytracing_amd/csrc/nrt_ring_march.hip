@@ -25,8 +25,15 @@ int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const Ma
     MarchArgs a = ma;
     a.lds_spheres = (sph > 0 && s->host_dev.n_spheres >= kLdsSpheresMin && ring_lds + sph <= (size_t)kLdsBytes &&
                      kLdsBytes / (ring_lds + sph) == kLdsBytes / base) ? (int)ring_lds : 0;
-    const size_t lds = a.lds_spheres ? ring_lds + sph : base;
-    auto launch = [&](auto kern, const char* name) -> int {
+    const size_t lds0 = a.lds_spheres ? ring_lds + sph : base;
+    auto launch = [&](auto kern, const char* name, bool plain = false) -> int {
+      // the plain march stages its lines (MarchArgs::stage) when that keeps the blocks per CU
+      MarchArgs b = a;
+      size_t lds = lds0;
+      if (plain) {
+        stage_lds(b, lds, kRingWaves);
+        if (b.stage && kLdsBytes / lds != kLdsBytes / lds0) { b.stage = 0; lds = lds0; }
+      }
       if (int rc = set_lds(kern, lds)) return rc;
       int per_cu = 0;
       NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kRingWaves, lds));
@@ -41,14 +48,14 @@ int ring_march16_launch(const nrt_sdf* s, const float* rays, int64_t P, const Ma
       if (a.queue) NRT_HIP(hipMemsetAsync(a.queue, 0, sizeof(unsigned int), st));
       ProfScope prof(name, st);
       kern<<<dim3(blocks), dim3(64 * kRingWaves), lds, st>>>(
-          s->host_dev, s->mlp->host_dev, rays, P, a, t, visible, nullptr, nullptr, nullptr, thr, keys);
+          s->host_dev, s->mlp->host_dev, rays, P, b, t, visible, nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     // the shadow march (visible != nullptr) and NRT_MIXED's flagging march are their own
     // instantiations (the plain march carries none of them)
     if (visible) return launch(k_occl16<NB, NE, kRingWaves, FOLD>, "k_occl16");
     if (ma.amb) return launch(k_march16<NB, NE, kRingWaves, FOLD, true>, "k_march16");
-    if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16")) return rc;
+    if (int rc = launch(k_march16<NB, NE, kRingWaves, FOLD>, "k_march16", true)) return rc;
     if (scan && best16) return launch(k_scan_best16<NB, NE, kRingWaves, FOLD>, "k_scan_best16");
     return NRT_OK;
   });

@@ -48,8 +48,10 @@ int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
   const bool scan = ma.primary != 0;
   auto run = [&]<int KH, int KQ, int ACT>() -> int {
     constexpr int WV = kRing3Waves;
-    auto launch = [&](auto kern, const char* name) -> int {
-      const size_t lds = ring3::Engine<KH, KQ, WV>::RING_BYTES + extra;
+    auto launch = [&](auto kern, const char* name, bool plain = false) -> int {
+      size_t lds = ring3::Engine<KH, KQ, WV>::RING_BYTES + extra;
+      MarchArgs mb = ma;
+      if (plain) stage_lds(mb, lds, WV);  // the plain march's line stages (one block a CU)
       if (int rc = set_lds(kern, lds)) return rc;
       int per_cu = 0;
       NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WV, lds));
@@ -59,7 +61,7 @@ int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
       if (ma.queue) NRT_HIP(hipMemsetAsync(ma.queue, 0, sizeof(unsigned int), st));
       ProfScope prof(name, st);
       // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit,
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, mb, t, hit,
                                                      nullptr, nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
@@ -68,7 +70,7 @@ int ring3_launch(const nrt_sdf* s, const float* rays, int64_t P, const MarchArgs
     if (which == 2) return launch(k_march3<KH, KQ, WV, ACT, true>, "k_refine3");
     if (which == 3) return launch(k_scan_best3<KH, KQ, WV, ACT, true>, "k_best3");
     if (which == 0)
-      if (int rc = launch(k_march3<KH, KQ, WV, ACT>, "k_march3")) return rc;
+      if (int rc = launch(k_march3<KH, KQ, WV, ACT>, "k_march3", true)) return rc;
     if (scan) return launch(k_scan_best3<KH, KQ, WV, ACT>, "k_scan_best3");
     return NRT_OK;
   };

@@ -26,8 +26,10 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
   if (scan && which == 0) NRT_HIP(hipMemsetAsync(keys, 0xff, (size_t)P * sizeof(unsigned long long), st));
   auto run = [&]<int KH, int KE, int ACT>() -> int {
     constexpr int WV = KH <= 32 ? NRT_R32_SMALL_WV : kRing32Waves;
-    auto launch = [&](auto kern, const char* name) -> int {
-      const size_t lds = ring32::Engine<KH, KE, WV>::RING_BYTES + extra;
+    auto launch = [&](auto kern, const char* name, bool plain = false) -> int {
+      size_t lds = ring32::Engine<KH, KE, WV>::RING_BYTES + extra;
+      MarchArgs mb = ma;
+      if (plain) stage_lds(mb, lds, WV);  // the march's line stages (one block a CU)
       if (int rc = set_lds(kern, lds)) return rc;
       int per_cu = 0;
       NRT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * WV, lds));
@@ -37,13 +39,13 @@ static int ring32_launch(const nrt_sdf* s, const float* rays, int64_t P, const M
       if (ma.queue) NRT_HIP(hipMemsetAsync(ma.queue, 0, sizeof(unsigned int), st));
       ProfScope prof(name, st);
       // p / n / raw_n: written by k_march_finish (the march packs hit into t's sign bit)
-      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, ma, t, hit, nullptr,
+      kern<<<dim3(blocks), dim3(64 * WV), lds, st>>>(s->host_dev, md, rays, P, mb, t, hit, nullptr,
                                                      nullptr, nullptr, thr, keys);
       return check_launch(name);
     };
     if (which == 2) return launch(k_occl32<KH, KE, WV, ACT>, "k_occl32");
     if (which == 0)
-      if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32")) return rc;
+      if (int rc = launch(k_march32<KH, KE, WV, ACT>, "k_march32", true)) return rc;
     if (scan) return launch(k_scan_best32<KH, KE, WV, ACT>, "k_scan_best32");
     return NRT_OK;
   };

@@ -267,7 +267,8 @@ def test_runtime_options_roundtrip():
     names = ["ring16", "ring32", "normals16", "scan_best32", "march_blocks", "shade_program",
              "nerf_fused", "max_waves", "shade_ring", "normals_ring", "xcd_lines",
              "mixed_refine_d", "mixed_refine_s", "mixed_restart", "mixed_drift",
-             "ring_occlusion", "mixed_zone", "bwd_colsplit", "bwd_ring", "march_queue", "train_save", "wgrad_tile"]
+             "ring_occlusion", "mixed_zone", "bwd_colsplit", "bwd_ring", "march_queue", "train_save", "wgrad_tile",
+             "march_stage"]
     defaults = {n: _lib.get_option(n) for n in names}
     assert defaults == {"ring16": 1, "ring32": 1, "normals16": 1, "scan_best32": 1,
                         "march_blocks": 0, "shade_program": 1, "nerf_fused": 1, "max_waves": 0,
@@ -275,7 +276,7 @@ def test_runtime_options_roundtrip():
                         "mixed_refine_d": 20000, "mixed_refine_s": 2000, "mixed_restart": 1,
                         "mixed_drift": 0, "ring_occlusion": 1, "mixed_zone": 500000,
                         "bwd_colsplit": 1, "bwd_ring": 1, "march_queue": 2,
-                        "train_save": 1, "wgrad_tile": 0}
+                        "train_save": 1, "wgrad_tile": 0, "march_stage": 1}
     with _lib.options(march_blocks=5, ring32=0):
         assert _lib.get_option("march_blocks") == 5 and _lib.get_option("ring32") == 0
     assert _lib.get_option("march_blocks") == 0 and _lib.get_option("ring32") == 1

@@ -200,6 +200,34 @@ def test_march_queue_matches_job_lists(prec):
         assert torch.equal(it.p, base.p) and torch.equal(it.n, base.n)
 
 
+@pytest.mark.parametrize("hidden", [128, 256])
+@pytest.mark.parametrize("prec", ["fp32", "fp16", "fp32-split", "mixed"])
+def test_march_line_staging_matches_per_ray_stores(prec, hidden):
+    """Option march_stage (the launch queue's march writes each wave's finished packed t and
+    whole-scan keys through per-wave LDS line stages, nrt_kernels.h LineStage): bit-identical t,
+    hit, p, n and throughput to one store per ray -- 37^2 = 1,369 rays (a ragged last line), 3
+    blocks (24 waves: 384 segmented scans, the rest whole, a line split between the two), and the
+    default grid; the 128- and 256-wide shifts (the headline's width)."""
+    from neural_raytracing_amd import set_precision
+    _, mine = _blob(32, hidden, 16, "softplus", seed=21)
+    rays = _rays(37, 23, eye=(0.0, 0.2, 1.1))
+    set_precision(prec)
+    _lib_opt("march_queue", 1)
+    try:
+        for blocks in (3, 0):
+            _lib_opt("march_blocks", blocks)
+            _lib_opt("march_stage", 0)
+            base, bh, _ = _march(mine, rays)
+            assert bh.any() and not bh.all()
+            _lib_opt("march_stage", 1)
+            it, h, _ = _march(mine, rays)
+            assert torch.equal(h, bh)
+            assert torch.equal(it.t, base.t) and torch.equal(it.throughput, base.throughput)
+            assert torch.equal(it.p, base.p) and torch.equal(it.n, base.n)
+    finally:
+        _lib_opt("march_stage", 1)
+
+
 @pytest.mark.parametrize("prec", ["fp32", "fp16", "fp32-split", "mixed"])
 def test_ring32_after_device_refresh_matches_fresh_pack(prec):
     """nrt_mlp_refresh re-gathers stream32 / bias32, the split stream and the FP16 ring stream
