@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r06/final
+O=${FINAL_DIR:-gpurun_out/r06/final}
 mkdir -p $O
 O=$O/tests bash tools/r06_tests.sh || exit 1
 P=$O/pmc

@@ -3,7 +3,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r06/final
+O=${FINAL_DIR:-gpurun_out/r06/final}
 mkdir -p $O
 rm -f $O/scenes.jsonl
 for SC in colocate dtu; do
