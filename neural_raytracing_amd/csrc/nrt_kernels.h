@@ -625,8 +625,10 @@ struct RingPol3 {
   // branch: both variants pass the same block barriers)
   __device__ __forceinline__ static float sdf(Eng& E, const SdfDev& s, const MlpDev& m, float x, float y, float z) {
     const float d = (s.kind == 2) ? ring32::spheres_value16(s, E.lspheres, E.lane, x, y, z) : 0.f;
+#ifndef NRT_NOGUARD_EXP  // timing experiment only (tools/exp_variants.py): results need the guard
     if (__builtin_amdgcn_readfirstlane((int)E.guarded))
       return d + ring3::eval<KH, KQ, WV, ACT, false, true>(E, m, x, y, z);
+#endif
     return d + ring3::eval<KH, KQ, WV, ACT>(E, m, x, y, z);
   }
   __device__ __forceinline__ static float tan(Eng& E, const MlpDev& m, float x, float y, float z) {
