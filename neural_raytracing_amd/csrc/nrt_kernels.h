@@ -699,7 +699,11 @@ __device__ __forceinline__ void march_body(
   int64_t cend = 0;    // queue: end of the wave's current chunk [cursor, cend)
   bool dry = false;    // queue: drained
   // line staging (MarchArgs::stage): only the launch queue's plain march (job k's ray is k)
+#ifdef NRT_NOSTAGE_EXP  // timing experiment only (tools/exp_variants.py): the staging compiled out
+  constexpr bool stg = false;
+#else
   const bool stg = !MX && mode == 0 && dyn && a.stage != 0 && p_out == nullptr;
+#endif
   LineStage<float> st_t;
   LineStage<unsigned long long> st_k;
   if (stg) {
