@@ -964,7 +964,16 @@ TrainWs carve(const nrt_mlp* m, int64_t M, void* base) {
 // accumulators are summed in wave order through LDS and the slice partials in slice order
 // (deterministic).  S is chosen from the shapes alone (same inputs, same bits).
 constexpr int kSplitMax = 64;
-constexpr int64_t kSliceRows = 256;  // batch rows per slice at least
+#ifndef NRT_WG_SLICE_ROWS
+#define NRT_WG_SLICE_ROWS 256
+#endif
+#ifndef NRT_WG_U
+#define NRT_WG_U 8
+#endif
+#ifndef NRT_WG_WPE
+#define NRT_WG_WPE 3
+#endif
+constexpr int64_t kSliceRows = NRT_WG_SLICE_ROWS;  // batch rows per slice at least
 constexpr int kWgradWaves = 4;        // waves per block
 
 // ---- every weight and bias gradient of one backward call in two launches --------------------
@@ -987,7 +996,7 @@ struct WgradJob {
 };
 
 template <int = 0>
-__global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_per_eu(3))) k_wgrad_batch(
+__global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_per_eu(NRT_WG_WPE))) k_wgrad_batch(
     const WgradJob* __restrict__ jobs, int n_jobs, int S, float* __restrict__ part) {
   typedef float f16v_ __attribute__((ext_vector_type(16)));
   __shared__ float red[kWgradWaves - 1][16][64];
@@ -1005,7 +1014,7 @@ __global__ void __launch_bounds__(64 * kWgradWaves) __attribute__((amdgpu_waves_
   const int64_t m0 = (int64_t)slice * jb.slice_rows;
   const int64_t m1 = std::min<int64_t>(jb.M, m0 + jb.slice_rows);
   f16v_ acc[4] = {};
-  constexpr int U = 8;  // k-steps (2 rows each) per group
+  constexpr int U = NRT_WG_U;  // k-steps (2 rows each) per group
   // clamped indices as in k_wgrad: loads are unconditional, rows past the slice are zeroed in
   // the A operand, clamped columns / rows feed only outputs that are never stored
   const int ia = std::min(r0 + i, R - 1), ib = std::min(r0 + 32 + i, R - 1);
