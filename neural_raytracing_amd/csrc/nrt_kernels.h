@@ -294,7 +294,14 @@ struct MarchArgs {
   // stages (LineStage, kStageBytes a wave); 0 = every finished ray stores its own words
   int stage = 0;
 };
-constexpr int kQueueChunk = 16;
+#ifndef NRT_QUEUE_CHUNK
+#define NRT_QUEUE_CHUNK 16
+#endif
+#ifndef NRT_QUEUE_TAIL
+#define NRT_QUEUE_TAIL 16
+#endif
+constexpr int kQueueChunk = NRT_QUEUE_CHUNK;  // 32 measured slower (round 5)
+constexpr int kQueueTail = NRT_QUEUE_TAIL;    // rays per wave of the grid whose scans are segmented
 
 // ------------------------------------------------------------------------------------------
 // Line staging of the march's per-ray words (MarchArgs::stage).  Under the launch queue a wave
@@ -673,7 +680,7 @@ __device__ __forceinline__ void march_body(
   // then kScanSegs segments of each of the last T rays (atomic min merge) to level the tail; the
   // launch-wide queue segments the last 16 rays per wave of the grid (every ray segmented took
   // HBM traffic per 800^2 launch from 178 to 325 MB: 8 key atomics per ray)
-  const int64_t tq = 16 * nw;
+  const int64_t tq = kQueueTail * nw;
   const int64_t T = dyn ? (R < tq ? R : tq)
                         : (kScanSplit < 0 ? R : (R < kScanSplit ? R : (int64_t)kScanSplit));
   // sdf(best) with a runner-up key: a second job per ray re-evaluates the runner-up where the
